@@ -1,0 +1,194 @@
+/*
+ * pano.h -- C-ABI of libpano.so, the MI355X (gfx950) panorama-stitching hot path.
+ *
+ * The reference (sapt36/VFX_Image_Stitching) is Python with no FFI layer; its "operator
+ * API" is a set of module-level functions.  Each entry point below replaces one of them
+ * (file:line in /root/reference) and is what a ctypes binding of that function calls
+ * (see INTEGRATION.md).  Conventions:
+ *
+ *   - Every pointer named d_* is DEVICE memory (hipMalloc / torch.cuda); h_* is host.
+ *   - Calls are asynchronous on the context's stream unless documented otherwise.
+ *   - Images are uint8 HWC BGR (row-major, 3 channels), frames of a batch share h, w.
+ *   - Return value: PANO_OK (0) or a negative PANO_E_* code; pano_last_error() has the
+ *     message.  Nothing throws across the ABI.
+ *   - Variable-length outputs use a caller capacity + a device counter; a counter larger
+ *     than the capacity means entries were dropped (PANO_E_OVERFLOW after pano_sync()).
+ *   - No entry point allocates or synchronises inside the stream order except
+ *     pano_ctx_reserve() and pano_sync(), so launch sequences are hipGraph-capturable
+ *     after a reserve.
+ */
+#ifndef PANO_H
+#define PANO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PANO_OK            0
+#define PANO_E_ARG        -1
+#define PANO_E_HIP        -2
+#define PANO_E_OVERFLOW   -3
+#define PANO_E_NOMATCH    -4
+#define PANO_E_UNSUPPORTED -5
+
+#define PANO_DESC_DIM 128
+
+typedef struct pano_ctx pano_ctx;
+
+/* cv2.KeyPoint as the reference fills it (sift_impl.py:206-210, 290-291): float32 fields,
+ * octave = octave + 256*layer + 65536*round((u2+0.5)*255), in input-image coordinates
+ * after convert_keypoints_to_input_image_size (sift_impl.py:333-343). */
+typedef struct pano_kp {
+    float x, y, size, angle, response;
+    int32_t octave;
+} pano_kp;
+
+/* compute_keypoints_and_descriptors kwargs + the hard-coded defaults of the stage
+ * functions it chains (sift_impl.py:15, 117, 170, 247, 361-362). */
+typedef struct pano_sift_params {
+    double sigma;              /* 1.6   */
+    int32_t num_intervals;     /* 3     */
+    double assumed_blur;       /* 0.5   */
+    int32_t border;            /* 5     */
+    double contrast_threshold; /* 0.04  */
+    double eigen_ratio;        /* 10    */
+    int32_t max_iter;          /* 5     */
+    double radius_factor;      /* 3     */
+    double peak_ratio;         /* 0.8   */
+    double scale_factor;       /* 1.5   */
+    double scale_multiplier;   /* 3     */
+    double descriptor_max;     /* 0.2   */
+} pano_sift_params;
+
+/* One per-pair result: ransac()'s best move and best pair (image_stitching_sift.py:86-111)
+ * plus bookkeeping.  Coordinates are the float32 keypoint coordinates widened to double. */
+typedef struct pano_pair_rec {
+    double dx, dy;             /* best move = ptA - ptB                                  */
+    double xA, yA, xB, yB;     /* the winning match                                      */
+    int32_t n_matches;         /* matches passing the descriptor threshold               */
+    int32_t votes;             /* inliers of the winner                                  */
+    int32_t best;              /* index of the winning match in match order, -1 if none  */
+    int32_t status;            /* PANO_OK or PANO_E_NOMATCH                              */
+} pano_pair_rec;
+
+/* Placement of one compositing step in the final canvas (computed on the host from the
+ * per-pair records by pano_plan_composite; image_stitching_sift.py:156-202, 369-381). */
+typedef struct pano_step {
+    int32_t frame_x, frame_y;  /* top-left of the new frame's h x w content, final canvas   */
+    int32_t canvas_x, canvas_y, canvas_h, canvas_w; /* the step's whole canvas, final coords */
+    int32_t frame_is_a;        /* 1: the new frame is imgA of the blend (dx < 0 swap branch) */
+    int32_t pad;
+    double overlap_range;      /* blend_two_images overlap_range (0 -> alpha = 0)        */
+} pano_step;
+
+/* ---------------------------------------------------------------- context */
+int pano_ctx_create(int device, void *hip_stream, pano_ctx **out);
+int pano_ctx_destroy(pano_ctx *ctx);
+int pano_ctx_set_stream(pano_ctx *ctx, void *hip_stream);
+/* Pre-size scratch for n frames of h x w with cap keypoints per frame (allocates). */
+int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap);
+int pano_sync(pano_ctx *ctx);
+const char *pano_last_error(pano_ctx *ctx);
+const char *pano_version(void);
+void pano_sift_default_params(pano_sift_params *p);
+/* Host-only helpers (no GPU): the scalar plan of S1/S2 and the f32 Gaussian taps. */
+int pano_sift_plan(const pano_sift_params *p, int h, int w, int *n_octaves, int *n_levels,
+                   double *sigma_base, double *sigma_levels);
+int pano_sift_taps(double sigma, double *taps_out /* >= 64 */, int *n_taps);
+
+/* ---------------------------------------------------------------- C1
+ * cylindrical_projection(img_bgr, focal_len)  image_stitching_sift.py:117-136
+ * Batched: d_src/d_dst [n][h][w][3]; h_focal[n].  Optional d_colnz [n][w] receives
+ * "column has any non-zero byte" flags of each output (used by the compositor). */
+int pano_cylindrical(pano_ctx *ctx, const uint8_t *d_src, uint8_t *d_dst, int n, int h, int w,
+                     const double *h_focal, uint8_t *d_colnz);
+
+/* ---------------------------------------------------------------- S0..S9
+ * compute_keypoints_and_descriptors(image, sigma, num_intervals, assumed_blur,
+ * image_border_width)  sift_impl.py:15-39.  Batched over n frames of h x w BGR uint8.
+ * d_kps [n][cap], d_desc [n][cap][128] float32 (integer valued), d_counts [n] (may exceed
+ * cap on overflow).  Keypoints come out in the reference's sorted, de-duplicated order. */
+int pano_sift(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
+              const pano_sift_params *params, pano_kp *d_kps, float *d_desc, int cap,
+              int32_t *d_counts);
+
+/* Stage access for the GUI-facing stage functions (sift_impl.py:45-111):
+ * after pano_sift (or pano_sift_pyramid) the Gaussian / DoG pyramid of frame `frame`
+ * stays in the context.  level 0..num_intervals+2 (Gaussian) / 0..num_intervals+1 (DoG).
+ * Copies one level to d_out (h_o x w_o float32); pano_sift_level_shape reports its size. */
+int pano_sift_pyramid(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
+                      const pano_sift_params *params);
+int pano_sift_level_shape(pano_ctx *ctx, int octave, int *h_out, int *w_out, int *n_octaves);
+int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int dog, float *d_out);
+
+/* ---------------------------------------------------------------- H1..H3
+ * compute_keypoints_and_descriptors_harris(img_bgr, max_points)  image_stitching_harris.py:187-214
+ * d_xy [n][max_points][2] int32 (x, y), d_desc [n][max_points][128] f32, d_counts [n]. */
+int pano_harris(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w, int max_points,
+                int32_t *d_xy, float *d_desc, int32_t *d_counts);
+
+/* ---------------------------------------------------------------- M1 / H4
+ * Brute-force L2 nearest neighbour of every row of A among rows of B
+ * (image_stitching_sift.py:63-79, image_stitching_harris.py:219-240).
+ * exact_int != 0: descriptors are integers in [0,255] (SIFT): fp32 MFMA distance GEMM,
+ *   distances exact.  exact_int == 0 (Harris): direct fp32 differences summed in the
+ *   OpenBLAS sdot order numpy uses.
+ * Batched over pairs: pair p matches frame h_pairs[2p] (A) against h_pairs[2p+1] (B) of a
+ * [frames][cap][128] descriptor array with d_counts[frames].
+ * Outputs per pair p, row i (< cap): d_best[p][i] (first minimum, -1 if B empty),
+ * d_d1[p][i] best distance, d_d2[p][i] second-best distance (Lowe ratio input). */
+int pano_match(pano_ctx *ctx, const float *d_desc, const int32_t *d_counts, int cap,
+               const int32_t *h_pairs, int n_pairs, int exact_int,
+               int32_t *d_best, float *d_d1, float *d_d2);
+
+/* ---------------------------------------------------------------- R1
+ * Match filter (distance < desc_thresh, optional Lowe ratio d1 < ratio*d2 when ratio > 0)
+ * + ransac(matches, dist_sq_thresh)  image_stitching_sift.py:74-111.
+ * Keypoint coordinates come from d_xy_f32 [frames][cap][2] (SIFT: pano_kp x,y are read
+ * when d_kps != NULL; Harris: pass d_xy_i32).  Writes d_recs[n_pairs]. */
+int pano_pair_shifts(pano_ctx *ctx, const pano_kp *d_kps, const int32_t *d_xy_i32,
+                     const int32_t *d_counts, int cap, const int32_t *h_pairs, int n_pairs,
+                     const int32_t *d_best, const float *d_d1, const float *d_d2,
+                     double desc_thresh, double ratio, double ransac_thr,
+                     pano_pair_rec *d_recs);
+
+/* ransac(matches) on an explicit move list (drop-in for the Python function):
+ * d_moves [k][2] double (dx, dy).  d_out[0] = best index (-1 if k == 0), d_out[1] = votes. */
+int pano_ransac_translate(pano_ctx *ctx, const double *d_moves, int k, double thr,
+                          int32_t *d_out);
+
+/* ---------------------------------------------------------------- B1
+ * Host planning of the whole mosaic loop from drift-corrected shifts and best pairs:
+ * h_shifts [n-1][2], h_pairs [n-1][4] (xA, yA, xB, yB); every frame h x w.  Fills
+ * h_steps[n-1] (step i blends frame i+1), frame 0's placement in h_first and the final
+ * canvas size.  Returns PANO_E_UNSUPPORTED if a step would crop (never for pad_image). */
+int pano_plan_composite(const double *h_shifts, const double *h_pairs, int n, int h, int w,
+                        pano_step *h_steps, int32_t *h_first_xy, int32_t *h_canvas_hw);
+
+/* Run the whole mosaic loop on device: d_frames [n][h][w][3] cylindrical frames,
+ * d_colnz [n][w] their column flags, d_canvas [H][W][3] (zeroed here), d_colflags [W]
+ * scratch.  Bit-identical to the reference's sequential blend_two_images fold. */
+int pano_composite(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t *d_colnz, int n,
+                   int h, int w, const pano_step *h_steps, const int32_t *h_first_xy,
+                   uint8_t *d_canvas, int H, int W);
+
+/* blend_two_images(shift_vec, ref_match, imgA, imgB) for arbitrary inputs
+ * image_stitching_sift.py:156-202.  Geometry comes from pano_blend_geometry. */
+int pano_blend_geometry(double dx, double dy, const double *h_ref4, int hA, int wA, int hB,
+                        int wB, int32_t *h_geom /* [8]: ayA axA ayB axB H W swapped pad */,
+                        double *h_overlap);
+int pano_blend_two(pano_ctx *ctx, const uint8_t *d_A, int hA, int wA, const uint8_t *d_B,
+                   int hB, int wB, const int32_t *h_geom, double overlap_range,
+                   uint8_t *d_out);
+
+/* rectangle_crop bbox (image_stitching_sift.py:208-247): d_bbox[4] = ymin ymax xmin xmax of
+ * gray > black_threshold (-1s if none). */
+int pano_gray_bbox(pano_ctx *ctx, const uint8_t *d_img, int H, int W, int black_threshold,
+                   int32_t *d_bbox);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PANO_H */

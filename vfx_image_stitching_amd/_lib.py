@@ -1,0 +1,214 @@
+"""ctypes binding of libpano.so (include/pano.h).
+
+This is the ONLY way the package reaches the GPU: every compute entry point of the
+reference-compatible API below goes through these symbols.  There is deliberately no CPU
+fallback; if the shared library is missing or no HIP device is present, calls raise.
+torch is used only to own device buffers and to provide the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpano.so")
+
+PANO_OK = 0
+PANO_E_ARG = -1
+PANO_E_HIP = -2
+PANO_E_OVERFLOW = -3
+PANO_E_NOMATCH = -4
+PANO_E_UNSUPPORTED = -5
+DESC_DIM = 128
+
+
+class PanoError(RuntimeError):
+    """Raised when a libpano call returns a non-zero status."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libpano error {code}: {msg}")
+        self.code = code
+
+
+class KP(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float),
+                ("angle", ctypes.c_float), ("response", ctypes.c_float),
+                ("octave", ctypes.c_int32)]
+
+
+KP_NP = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                  ("response", "<f4"), ("octave", "<i4")])
+
+
+class SiftParams(ctypes.Structure):
+    _fields_ = [("sigma", ctypes.c_double), ("num_intervals", ctypes.c_int32),
+                ("assumed_blur", ctypes.c_double), ("border", ctypes.c_int32),
+                ("contrast_threshold", ctypes.c_double), ("eigen_ratio", ctypes.c_double),
+                ("max_iter", ctypes.c_int32), ("radius_factor", ctypes.c_double),
+                ("peak_ratio", ctypes.c_double), ("scale_factor", ctypes.c_double),
+                ("scale_multiplier", ctypes.c_double), ("descriptor_max", ctypes.c_double)]
+
+
+class PairRec(ctypes.Structure):
+    _fields_ = [("dx", ctypes.c_double), ("dy", ctypes.c_double), ("xA", ctypes.c_double),
+                ("yA", ctypes.c_double), ("xB", ctypes.c_double), ("yB", ctypes.c_double),
+                ("n_matches", ctypes.c_int32), ("votes", ctypes.c_int32),
+                ("best", ctypes.c_int32), ("status", ctypes.c_int32)]
+
+
+PAIR_NP = np.dtype([("dx", "<f8"), ("dy", "<f8"), ("xA", "<f8"), ("yA", "<f8"),
+                    ("xB", "<f8"), ("yB", "<f8"), ("n_matches", "<i4"), ("votes", "<i4"),
+                    ("best", "<i4"), ("status", "<i4")])
+
+
+class Step(ctypes.Structure):
+    _fields_ = [("frame_x", ctypes.c_int32), ("frame_y", ctypes.c_int32),
+                ("canvas_x", ctypes.c_int32), ("canvas_y", ctypes.c_int32),
+                ("canvas_h", ctypes.c_int32), ("canvas_w", ctypes.c_int32),
+                ("frame_is_a", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("overlap_range", ctypes.c_double)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PD = ctypes.POINTER(ctypes.c_double)
+
+# symbol -> (restype, argtypes); mirrors include/pano.h one to one
+SIGNATURES = {
+    "pano_ctx_create": (_I, [_I, _P, ctypes.POINTER(_P)]),
+    "pano_ctx_destroy": (_I, [_P]),
+    "pano_ctx_set_stream": (_I, [_P, _P]),
+    "pano_ctx_reserve": (_I, [_P, _I, _I, _I, _I]),
+    "pano_sync": (_I, [_P]),
+    "pano_last_error": (ctypes.c_char_p, [_P]),
+    "pano_version": (ctypes.c_char_p, []),
+    "pano_sift_default_params": (None, [ctypes.POINTER(SiftParams)]),
+    "pano_sift_plan": (_I, [ctypes.POINTER(SiftParams), _I, _I, _PI32, _PI32, _PD, _PD]),
+    "pano_sift_taps": (_I, [_D, _PD, _PI32]),
+    "pano_cylindrical": (_I, [_P, _P, _P, _I, _I, _I, _PD, _P]),
+    "pano_sift": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P, _P, _I, _P]),
+    "pano_sift_pyramid": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams)]),
+    "pano_sift_level_shape": (_I, [_P, _I, _PI32, _PI32, _PI32]),
+    "pano_sift_copy_level": (_I, [_P, _I, _I, _I, _I, _P]),
+    "pano_harris": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "pano_match": (_I, [_P, _P, _P, _I, _PI32, _I, _I, _P, _P, _P]),
+    "pano_pair_shifts": (_I, [_P, _P, _P, _P, _I, _PI32, _I, _P, _P, _P, _D, _D, _D, _P]),
+    "pano_ransac_translate": (_I, [_P, _P, _I, _D, _P]),
+    "pano_plan_composite": (_I, [_PD, _PD, _I, _I, _I, ctypes.POINTER(Step), _PI32, _PI32]),
+    "pano_composite": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I]),
+    "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),
+    "pano_blend_two": (_I, [_P, _P, _I, _I, _P, _I, _I, _PI32, _D, _P]),
+    "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load libpano.so and declare every exported signature (no GPU needed)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise PanoError(PANO_E_ARG, f"{path} not built (run __graft_entry__.build())")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def default_sift_params(**overrides) -> SiftParams:
+    p = SiftParams()
+    load().pano_sift_default_params(ctypes.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+# ----------------------------------------------------------------------------- context
+class Context:
+    """One libpano context per (device, stream).  Owns the library's scratch memory."""
+
+    def __init__(self, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise PanoError(PANO_E_HIP, "no HIP device visible: the HIP path is the only path")
+        self.h = None
+        self.device = device
+        self.lib = load()
+        self._torch = torch
+        h = _P()
+        stream = torch.cuda.current_stream(device).cuda_stream
+        rc = self.lib.pano_ctx_create(device, _P(stream), ctypes.byref(h))
+        if rc != PANO_OK:
+            raise PanoError(rc, "pano_ctx_create failed")
+        self.h = h
+
+    def check(self, rc):
+        if rc != PANO_OK:
+            raise PanoError(rc, (self.lib.pano_last_error(self.h) or b"").decode())
+
+    def bind_stream(self):
+        stream = self._torch.cuda.current_stream(self.device).cuda_stream
+        self.check(self.lib.pano_ctx_set_stream(self.h, _P(stream)))
+
+    def sync(self):
+        self.check(self.lib.pano_sync(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pano_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_ctxs: dict = {}
+
+
+def context(device: int | None = None) -> Context:
+    import torch
+    if device is None:
+        device = torch.cuda.current_device()
+    ctx = _ctxs.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _ctxs[device] = ctx
+    ctx.bind_stream()
+    return ctx
+
+
+def ptr(t) -> _P:
+    """Device pointer of a torch tensor (must be contiguous and on a HIP device)."""
+    if not t.is_cuda:
+        raise PanoError(PANO_E_ARG, "expected a device tensor")
+    if not t.is_contiguous():
+        raise PanoError(PANO_E_ARG, "expected a contiguous tensor")
+    return _P(t.data_ptr())
+
+
+def f64p(a: np.ndarray):
+    """Pointer into a caller-owned float64 C-contiguous array (no temporaries)."""
+    if a.dtype != np.float64 or not a.flags.c_contiguous:
+        raise PanoError(PANO_E_ARG, "expected a C-contiguous float64 array")
+    return a.ctypes.data_as(_PD)
+
+
+def i32p(a: np.ndarray):
+    """Pointer into a caller-owned int32 C-contiguous array (no temporaries)."""
+    if a.dtype != np.int32 or not a.flags.c_contiguous:
+        raise PanoError(PANO_E_ARG, "expected a C-contiguous int32 array")
+    return a.ctypes.data_as(_PI32)

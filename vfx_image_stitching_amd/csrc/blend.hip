@@ -1,0 +1,403 @@
+// blend.hip -- B1: pad_image + blend_two_images (image_stitching_sift.py:139-202), the
+// mosaic loop of run_panorama (:369-381) and rectangle_crop's bbox (:208-247).
+//
+// The reference re-allocates and rewrites the whole mosaic every step (O(N^2 H W)).  Here
+// the final canvas is sized up front (pano_plan_composite replays the integer geometry of
+// every step on the host) and each step touches only the columns of the new frame: all
+// other columns of the step's result are "B only" / "neither" columns, whose values the
+// reference copies unchanged.  Per step and column:
+//   fF = frame column has a non-zero byte, fM = mosaic column has a non-zero byte
+//   both   -> out = f32(1-a) * A + f32(a) * B over the WHOLE step-canvas column,
+//             a = (#both columns to the left) / overlap_range (double), uint8 truncation
+//   fF only-> the frame column (zeros outside its rows)
+// with A/B = (new frame, mosaic) in the dx < 0 (swap) branch, (mosaic, frame) otherwise.
+// Column flags ping-pong between two arrays so a step reads the previous step's flags
+// while writing its own (columns of the previous frame range are carried across).
+#include "pano_internal.h"
+
+namespace {
+
+constexpr int CPB = 4;   // columns per workgroup
+
+__device__ __forceinline__ uint8_t blend_px(float a32, float b32, uint8_t A, uint8_t B) {
+    const float v = a32 * (float)A + b32 * (float)B;
+    return (uint8_t)(int)v;   // astype(np.uint8) on a non-negative float: truncation
+}
+
+__global__ void __launch_bounds__(256)
+place_first(const uint8_t *__restrict__ frame, const uint8_t *__restrict__ colnz, int h, int w,
+            uint8_t *__restrict__ canvas, int W, int fy, int fx, uint8_t *__restrict__ F0,
+            uint8_t *__restrict__ F1) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= w || y >= h) return;
+    const uint8_t *s = frame + ((size_t)y * w + x) * 3;
+    uint8_t *d = canvas + ((size_t)(fy + y) * W + fx + x) * 3;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+    if (y == 0) {
+        F0[fx + x] = colnz[x] ? 1 : 0;
+        F1[fx + x] = colnz[x] ? 1 : 0;
+    }
+}
+
+struct StepArg {
+    int fx, fy;             // frame content top-left (final canvas)
+    int cy, ch;             // step canvas rows [cy, cy + ch)
+    int prev_fx;            // previous step's frame column start (-1: none)
+    int frame_is_a;
+    double overlap;
+};
+
+__global__ void __launch_bounds__(256)
+composite_step(const uint8_t *__restrict__ frame, const uint8_t *__restrict__ colnz, int h,
+               int w, uint8_t *__restrict__ canvas, int W, StepArg s,
+               const uint8_t *__restrict__ Fin, uint8_t *__restrict__ Fout) {
+    __shared__ int red[256];
+    __shared__ int rank_sh[CPB];
+    __shared__ int any_sh[CPB];
+    const int tid = threadIdx.x;
+    const int c0 = blockIdx.x * CPB;
+    // carry the previous step's frame-range flags that this step does not rewrite
+    if (tid < CPB && s.prev_fx >= 0) {
+        const int X = s.prev_fx + c0 + tid;
+        if (c0 + tid < w && X >= 0 && X < W && !(X >= s.fx && X < s.fx + w)) Fout[X] = Fin[X];
+    }
+    // number of "both" columns left of c0 (redundant per workgroup, <= w flags)
+    int cntb = 0;
+    for (int c = tid; c < c0; c += 256) cntb += (colnz[c] && Fin[s.fx + c]) ? 1 : 0;
+    red[tid] = cntb;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (tid < off) red[tid] += red[tid + off];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        int r = red[0];
+        for (int q = 0; q < CPB; ++q) {
+            const int c = c0 + q;
+            rank_sh[q] = r;
+            any_sh[q] = 0;
+            if (c < w && colnz[c] && Fin[s.fx + c]) ++r;
+        }
+    }
+    __syncthreads();
+    for (int q = 0; q < CPB; ++q) {
+        const int c = c0 + q;
+        if (c >= w) break;
+        const int X = s.fx + c;
+        const bool fF = colnz[c] != 0;
+        const bool fM = Fin[X] != 0;
+        if (!fF) {
+            if (tid == 0) Fout[X] = fM ? 1 : 0;
+            continue;
+        }
+        if (!fM) {
+            // frame-only column: copy the frame column (the mosaic column is all zero)
+            for (int e = tid; e < h * 3; e += 256) {
+                const int y = e / 3, ch = e - y * 3;
+                canvas[((size_t)(s.fy + y) * W + X) * 3 + ch] = frame[((size_t)y * w + c) * 3 + ch];
+            }
+            if (tid == 0) Fout[X] = 1;
+            continue;
+        }
+        const double alpha = s.overlap != 0.0 ? (double)rank_sh[q] / s.overlap : 0.0;
+        const float a32 = (float)(1.0 - alpha), b32 = (float)alpha;
+        int any = 0;
+        for (int e = tid; e < s.ch * 3; e += 256) {
+            const int y = s.cy + e / 3, ch = e % 3;
+            const int fyl = y - s.fy;
+            const uint8_t Fv = (fyl >= 0 && fyl < h) ? frame[((size_t)fyl * w + c) * 3 + ch] : 0;
+            uint8_t *pm = canvas + ((size_t)y * W + X) * 3 + ch;
+            const uint8_t Mv = *pm;
+            const uint8_t o = s.frame_is_a ? blend_px(a32, b32, Fv, Mv) : blend_px(a32, b32, Mv, Fv);
+            *pm = o;
+            any |= o;
+        }
+        if (any) any_sh[q] = 1;   // benign race: every writer stores 1
+        __syncthreads();
+        if (tid == 0) Fout[X] = any_sh[q] ? 1 : 0;
+    }
+}
+
+// ------------------------------------------------------------------ generic blend_two_images
+__global__ void col_flags2(const uint8_t *__restrict__ A, int hA, int wA, int ayA, int axA,
+                           const uint8_t *__restrict__ B, int hB, int wB, int ayB, int axB,
+                           int WW, uint8_t *__restrict__ fa, uint8_t *__restrict__ fb) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= WW) return;
+    int ra = 0, rb = 0;
+    const int ca = c - axA, cb = c - axB;
+    if (ca >= 0 && ca < wA)
+        for (int y = 0; y < hA && !ra; ++y) {
+            const uint8_t *p = A + ((size_t)y * wA + ca) * 3;
+            ra = (p[0] | p[1] | p[2]) != 0;
+        }
+    if (cb >= 0 && cb < wB)
+        for (int y = 0; y < hB && !rb; ++y) {
+            const uint8_t *p = B + ((size_t)y * wB + cb) * 3;
+            rb = (p[0] | p[1] | p[2]) != 0;
+        }
+    fa[c] = (uint8_t)ra;
+    fb[c] = (uint8_t)rb;
+}
+
+__global__ void __launch_bounds__(1024)
+both_rank(const uint8_t *__restrict__ fa, const uint8_t *__restrict__ fb, int WW,
+          int32_t *__restrict__ rank) {
+    __shared__ int sh[1024];
+    int carry = 0;
+    const int tid = threadIdx.x;
+    for (int base = 0; base < WW; base += 1024) {
+        const int c = base + tid;
+        const int v = (c < WW && fa[c] && fb[c]) ? 1 : 0;
+        sh[tid] = v;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            const int t = tid >= off ? sh[tid - off] : 0;
+            __syncthreads();
+            sh[tid] += t;
+            __syncthreads();
+        }
+        if (c < WW) rank[c] = carry + sh[tid] - v;
+        const int tot = sh[1023];
+        __syncthreads();
+        carry += tot;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+blend_two(const uint8_t *__restrict__ A, int hA, int wA, int ayA, int axA,
+          const uint8_t *__restrict__ B, int hB, int wB, int ayB, int axB, int HH, int WW,
+          const uint8_t *__restrict__ fa, const uint8_t *__restrict__ fb,
+          const int32_t *__restrict__ rank, double overlap, uint8_t *__restrict__ out) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= WW || y >= HH) return;
+    const int ya = y - ayA, xa = x - axA, yb = y - ayB, xb = x - axB;
+    const bool ina = ya >= 0 && ya < hA && xa >= 0 && xa < wA;
+    const bool inb = yb >= 0 && yb < hB && xb >= 0 && xb < wB;
+    uint8_t *o = out + ((size_t)y * WW + x) * 3;
+    const uint8_t *pa = ina ? A + ((size_t)ya * wA + xa) * 3 : nullptr;
+    const uint8_t *pb = inb ? B + ((size_t)yb * wB + xb) * 3 : nullptr;
+    if (fa[x] && fb[x]) {
+        const double alpha = overlap != 0.0 ? (double)rank[x] / overlap : 0.0;
+        const float a32 = (float)(1.0 - alpha), b32 = (float)alpha;
+        for (int ch = 0; ch < 3; ++ch)
+            o[ch] = blend_px(a32, b32, pa ? pa[ch] : 0, pb ? pb[ch] : 0);
+    } else if (fa[x]) {
+        for (int ch = 0; ch < 3; ++ch) o[ch] = pa ? pa[ch] : 0;
+    } else if (fb[x]) {
+        for (int ch = 0; ch < 3; ++ch) o[ch] = pb ? pb[ch] : 0;
+    } else {
+        o[0] = o[1] = o[2] = 0;
+    }
+}
+
+// ------------------------------------------------------------------ rectangle_crop bbox
+__global__ void bbox_init(int32_t *bbox) {
+    bbox[0] = 0x7fffffff; bbox[1] = -1; bbox[2] = 0x7fffffff; bbox[3] = -1;
+}
+
+__global__ void __launch_bounds__(256)
+gray_bbox(const uint8_t *__restrict__ img, int H, int W, int thr, int32_t *__restrict__ bbox) {
+    __shared__ int r[4][256];
+    const int tid = threadIdx.x;
+    int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
+    const size_t total = (size_t)H * W;
+    for (size_t i = (size_t)blockIdx.x * 256 + tid; i < total; i += (size_t)gridDim.x * 256) {
+        if (gray_u8(img + i * 3) > thr) {
+            const int y = (int)(i / W), x = (int)(i % W);
+            ymin = min(ymin, y); ymax = max(ymax, y);
+            xmin = min(xmin, x); xmax = max(xmax, x);
+        }
+    }
+    r[0][tid] = ymin; r[1][tid] = ymax; r[2][tid] = xmin; r[3][tid] = xmax;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (tid < off) {
+            r[0][tid] = min(r[0][tid], r[0][tid + off]);
+            r[1][tid] = max(r[1][tid], r[1][tid + off]);
+            r[2][tid] = min(r[2][tid], r[2][tid + off]);
+            r[3][tid] = max(r[3][tid], r[3][tid + off]);
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && r[1][0] >= 0) {
+        atomicMin(&bbox[0], r[0][0]);
+        atomicMax(&bbox[1], r[1][0]);
+        atomicMin(&bbox[2], r[2][0]);
+        atomicMax(&bbox[3], r[3][0]);
+    }
+}
+
+__global__ void bbox_fix(int32_t *bbox) {
+    if (bbox[1] < 0) bbox[0] = bbox[1] = bbox[2] = bbox[3] = -1;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host geometry (exact
+// replay of the Python scalar arithmetic of blend_two_images / pad_image / run_panorama)
+static void pad_place(long long mx, long long my, int h, int w, int *top, int *left, int *ph,
+                      int *pw) {
+    *left = mx >= 0 ? (int)mx : 0;
+    *top = my >= 0 ? (int)my : 0;
+    *pw = w + (int)(mx >= 0 ? mx : -mx);
+    *ph = h + (int)(my >= 0 ? my : -my);
+}
+
+extern "C" int pano_blend_geometry(double dx, double dy, const double *ref4, int hA, int wA,
+                                   int hB, int wB, int32_t *geom, double *overlap) {
+    if (!ref4 || !geom || !overlap) return PANO_E_ARG;
+    double r00 = ref4[0], r01 = ref4[1], r10 = ref4[2], r11 = ref4[3];
+    const int swapped = dx < 0;
+    if (swapped) {
+        dx = -dx;
+        dy = -dy;
+        double t0 = r00, t1 = r01;
+        r00 = r10; r01 = r11; r10 = t0; r11 = t1;
+        int th = hA, tw = wA;
+        hA = hB; wA = wB; hB = th; wB = tw;
+    }
+    (void)r01; (void)r11;
+    const double padA_x = ((double)(wB - wA) + r00) - r10;
+    const double padB_x = r00 - r10;
+    *overlap = (r10 - r00) + wA;
+    const long long mxA = (long long)nearbyint(-padA_x), myA = (long long)nearbyint(-dy);
+    const long long mxB = (long long)nearbyint(padB_x), myB = (long long)nearbyint(dy);
+    int tA, lA, hhA, wwA, tB, lB, hhB, wwB;
+    pad_place(mxA, myA, hA, wA, &tA, &lA, &hhA, &wwA);
+    pad_place(mxB, myB, hB, wB, &tB, &lB, &hhB, &wwB);
+    // geom: ayA axA ayB axB HH WW swapped (A/B are the post-swap roles)
+    geom[0] = tA; geom[1] = lA; geom[2] = tB; geom[3] = lB;
+    geom[4] = hhA > hhB ? hhA : hhB;
+    geom[5] = wwA > wwB ? wwA : wwB;
+    geom[6] = swapped;
+    geom[7] = 0;
+    return PANO_OK;
+}
+
+extern "C" int pano_plan_composite(const double *shifts, const double *pairs, int n, int h, int w,
+                                   pano_step *steps, int32_t *first_xy, int32_t *canvas_hw) {
+    if (n < 1 || h <= 0 || w <= 0 || !first_xy || !canvas_hw || (n > 1 && (!shifts || !pairs || !steps)))
+        return PANO_E_ARG;
+    int Hm = h, Wm = w;
+    std::vector<int> yM(n), xM(n), yF(n), xF(n), padtop(n);
+    for (int i = 1; i < n; ++i) {
+        // run_panorama pads the new frame to the mosaic height first (:374-376)
+        const int diff = Hm - h;
+        int fh = h, ptop = 0;
+        if (diff > 0) { fh = h + diff; ptop = diff; }
+        else if (diff < 0) { fh = h - diff; ptop = 0; }
+        int32_t g[8];
+        double ov;
+        // blend_two_images(shift, pair, imgA = mosaic, imgB = frame)
+        int rc = pano_blend_geometry(shifts[2 * (i - 1)], shifts[2 * (i - 1) + 1], pairs + 4 * (i - 1),
+                                     Hm, Wm, fh, w, g, &ov);
+        if (rc) return rc;
+        const int swapped = g[6];
+        // post-swap A is the frame when swapped
+        const int ay = g[0], ax = g[1], by = g[2], bx = g[3];
+        if (swapped) { yF[i] = ay; xF[i] = ax; yM[i] = by; xM[i] = bx; }
+        else { yM[i] = ay; xM[i] = ax; yF[i] = by; xF[i] = bx; }
+        padtop[i] = ptop;
+        pano_step &s = steps[i - 1];
+        s.canvas_h = g[4];
+        s.canvas_w = g[5];
+        s.frame_is_a = swapped;
+        s.pad = 0;
+        s.overlap_range = ov;
+        Hm = g[4];
+        Wm = g[5];
+    }
+    // origins: the last canvas is the final one; step i's input mosaic sits at (yM, xM)
+    int oy = 0, ox = 0;
+    for (int i = n - 1; i >= 1; --i) {
+        pano_step &s = steps[i - 1];
+        s.canvas_y = oy;
+        s.canvas_x = ox;
+        s.frame_y = oy + yF[i] + padtop[i];
+        s.frame_x = ox + xF[i];
+        oy += yM[i];
+        ox += xM[i];
+    }
+    first_xy[0] = ox;
+    first_xy[1] = oy;
+    canvas_hw[0] = Hm;
+    canvas_hw[1] = Wm;
+    return PANO_OK;
+}
+
+int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                     int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
+                     int H, int W) {
+    if (n < 1 || !frames || !colnz || !canvas || !first_xy || (n > 1 && !steps))
+        return pano_fail(ctx, PANO_E_ARG, "pano_composite: bad arguments");
+    int rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, 2 * (size_t)W + 64);
+    if (rc) return rc;
+    uint8_t *F[2] = {ctx->flags, ctx->flags + W};
+    PANO_HIP(ctx, hipMemsetAsync(canvas, 0, (size_t)H * W * 3, ctx->stream));
+    PANO_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 2 * (size_t)W, ctx->stream));
+    if (first_xy[0] < 0 || first_xy[1] < 0 || first_xy[0] + w > W || first_xy[1] + h > H)
+        return pano_fail(ctx, PANO_E_ARG, "pano_composite: frame 0 outside canvas");
+    dim3 g0((w + 63) / 64, (h + 3) / 4);
+    place_first<<<g0, 256, 0, ctx->stream>>>(frames, colnz, h, w, canvas, W, first_xy[1],
+                                             first_xy[0], F[0], F[1]);
+    PANO_LAUNCH_CHECK(ctx, "place_first");
+    int prev_fx = -1;
+    for (int i = 1; i < n; ++i) {
+        const pano_step &st = steps[i - 1];
+        if (st.frame_x < 0 || st.frame_x + w > W || st.frame_y < 0 || st.frame_y + h > H ||
+            st.canvas_y < 0 || st.canvas_y + st.canvas_h > H)
+            return pano_fail(ctx, PANO_E_ARG, "pano_composite: step outside canvas");
+        StepArg s;
+        s.fx = st.frame_x;
+        s.fy = st.frame_y;
+        s.cy = st.canvas_y;
+        s.ch = st.canvas_h;
+        s.prev_fx = prev_fx;
+        s.frame_is_a = st.frame_is_a;
+        s.overlap = st.overlap_range;
+        const uint8_t *fr = frames + (size_t)i * h * w * 3;
+        composite_step<<<(w + CPB - 1) / CPB, 256, 0, ctx->stream>>>(
+            fr, colnz + (size_t)i * w, h, w, canvas, W, s, F[(i - 1) & 1], F[i & 1]);
+        PANO_LAUNCH_CHECK(ctx, "composite_step");
+        prev_fx = st.frame_x;
+    }
+    return PANO_OK;
+}
+
+int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,
+                     int wB, const int32_t *g, double overlap, uint8_t *out) {
+    if (!A || !B || !g || !out) return pano_fail(ctx, PANO_E_ARG, "pano_blend_two: bad arguments");
+    const int HH = g[4], WW = g[5];
+    const size_t need = 2 * (size_t)WW + (size_t)WW * 4 + 64;
+    int rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, need);
+    if (rc) return rc;
+    uint8_t *fa = ctx->flags, *fb = ctx->flags + WW;
+    int32_t *rank = (int32_t *)(ctx->flags + ((2 * (size_t)WW + 15) & ~size_t(15)));
+    col_flags2<<<(WW + 255) / 256, 256, 0, ctx->stream>>>(A, hA, wA, g[0], g[1], B, hB, wB, g[2],
+                                                          g[3], WW, fa, fb);
+    PANO_LAUNCH_CHECK(ctx, "col_flags2");
+    both_rank<<<1, 1024, 0, ctx->stream>>>(fa, fb, WW, rank);
+    PANO_LAUNCH_CHECK(ctx, "both_rank");
+    dim3 grid((WW + 63) / 64, (HH + 3) / 4);
+    blend_two<<<grid, 256, 0, ctx->stream>>>(A, hA, wA, g[0], g[1], B, hB, wB, g[2], g[3], HH, WW,
+                                             fa, fb, rank, overlap, out);
+    PANO_LAUNCH_CHECK(ctx, "blend_two");
+    return PANO_OK;
+}
+
+int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox) {
+    if (!img || !bbox || H <= 0 || W <= 0) return pano_fail(ctx, PANO_E_ARG, "pano_gray_bbox");
+    bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
+    const size_t total = (size_t)H * W;
+    unsigned blocks = (unsigned)((total + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    gray_bbox<<<blocks, 256, 0, ctx->stream>>>(img, H, W, thr, bbox);
+    bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
+    PANO_LAUNCH_CHECK(ctx, "gray_bbox");
+    return PANO_OK;
+}

@@ -1,0 +1,277 @@
+// match.hip -- M1 / H4: brute-force L2 nearest neighbour of descriptor rows.
+//
+//   SIFT  (image_stitching_sift.py:63-79): for each i, argmin_j ||dA_i - dB_j||^2 with a
+//         strict '<' scan (first j wins ties).  Descriptors are integers in [0, 255], so
+//         ||a||^2 + ||b||^2 - 2 a.b is an exact integer < 2^24 in f32 whatever the order:
+//         the distance matrix is an fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32, exact f32
+//         fma chains) with the argmin / second-min fused into the epilogue.
+//   Harris (image_stitching_harris.py:219-240): float descriptors; numpy's np.dot(diff,
+//         diff) is OpenBLAS sdot, whose summation order is reproduced exactly
+//         (oracle/numerics.py::sdot_skx), one distance per thread.
+//
+// Workgroup tile: 128 (rows of A) x 128 (rows of B), 4 waves as 2 x 2, each wave 64 x 64 =
+// 2 x 2 MFMA blocks of 32 x 32; K = 128 streamed through LDS in 4 chunks of 32.
+// Per (row, column tile) the workgroup writes (best, index, second) partials; a reduce
+// kernel folds the column tiles in index order.  Roofline unit M1 = 2*N*M*128 flop/pair.
+#include "pano_internal.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int MT = 128;      // tile rows / cols
+constexpr int KC = 32;       // K chunk
+constexpr int LDA = KC + 1;  // padded LDS row (conflict-free column reads)
+
+struct Part {
+    float best;
+    int32_t idx;
+    float second;
+};
+
+__device__ __forceinline__ void merge(float &b, int &j, float &s, float b2, int j2, float s2) {
+    if (b2 < b || (b2 == b && j2 < j)) {
+        s = fminf(s2, b);
+        b = b2;
+        j = j2;
+    } else {
+        s = fminf(s, b2);
+    }
+}
+
+__global__ void row_norms(const float *__restrict__ desc, const int32_t *__restrict__ counts,
+                          int cap, int n_frames, float *__restrict__ norms) {
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (size_t)n_frames * cap) return;
+    const float *d = desc + gid * PANO_DESC_DIM;
+    float s = 0.0f;
+    for (int k = 0; k < PANO_DESC_DIM; ++k) s = fmaf(d[k], d[k], s);   // exact: integers
+    norms[gid] = s;
+}
+
+struct PairArg {
+    int32_t a[256], b[256];
+};
+
+__global__ void __launch_bounds__(256)
+dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
+          const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
+          int n_jt) {
+    __shared__ float As[MT * LDA];
+    __shared__ float Bs[MT * LDA];
+    __shared__ Part red[2][MT];
+    const int p = blockIdx.z;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    int NA = counts[fa], NB = counts[fb];
+    NA = NA < cap ? NA : cap;
+    NB = NB < cap ? NB : cap;
+    const int i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
+    if (i0 >= NA || j0 >= NB) return;
+    const float *dA = desc + (size_t)fa * cap * PANO_DESC_DIM;
+    const float *dB = desc + (size_t)fb * cap * PANO_DESC_DIM;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    f32x16 acc[2][2];
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+    for (int k0 = 0; k0 < PANO_DESC_DIM; k0 += KC) {
+        // 128 rows x 32 floats per operand = 1024 float4, 4 per thread
+        for (int q = tid; q < MT * KC / 4; q += 256) {
+            const int row = q / (KC / 4), c4 = (q % (KC / 4)) * 4;
+            float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+            if (i0 + row < NA) va = *(const float4 *)(dA + (size_t)(i0 + row) * PANO_DESC_DIM + k0 + c4);
+            if (j0 + row < NB) vb = *(const float4 *)(dB + (size_t)(j0 + row) * PANO_DESC_DIM + k0 + c4);
+            float *pa = As + row * LDA + c4;
+            float *pb = Bs + row * LDA + c4;
+            pa[0] = va.x; pa[1] = va.y; pa[2] = va.z; pa[3] = va.w;
+            pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
+        }
+        __syncthreads();
+        const int lr = lane & 31, lk = lane >> 5;
+#pragma unroll 4
+        for (int kk = 0; kk < KC; kk += 2) {
+            float av[2], bv[2];
+            for (int m = 0; m < 2; ++m) av[m] = As[(wr * 64 + m * 32 + lr) * LDA + kk + lk];
+            for (int m = 0; m < 2; ++m) bv[m] = Bs[(wc * 64 + m * 32 + lr) * LDA + kk + lk];
+            for (int a = 0; a < 2; ++a)
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // epilogue: lane holds rows (reg&3) + 8*(reg>>2) + 4*(lane>>5), column lane&31
+    const int hcol = lane & 31, hrow = 4 * (lane >> 5);
+    for (int a = 0; a < 2; ++a) {
+        for (int r = 0; r < 16; ++r) {
+            const int row = wr * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + hrow;
+            const int gi = i0 + row;
+            const float na = gi < NA ? norms[(size_t)fa * cap + gi] : 0.0f;
+            float best = INFINITY, second = INFINITY;
+            int bj = 0x7fffffff;
+            for (int b = 0; b < 2; ++b) {
+                const int gj = j0 + wc * 64 + b * 32 + hcol;
+                if (gj < NB) {
+                    const float d = (na + norms[(size_t)fb * cap + gj]) - 2.0f * acc[a][b][r];
+                    merge(best, bj, second, d, gj, INFINITY);
+                }
+            }
+            // butterfly over the 32 lanes that share this row
+            for (int off = 1; off < 32; off <<= 1) {
+                const float ob = __shfl_xor(best, off);
+                const int oj = __shfl_xor(bj, off);
+                const float os = __shfl_xor(second, off);
+                merge(best, bj, second, ob, oj, os);
+            }
+            if (hcol == 0) red[wc][row] = Part{best, bj, second};
+        }
+    }
+    __syncthreads();
+    if (tid < MT) {
+        Part x = red[0][tid];
+        const Part y = red[1][tid];
+        float b = x.best, s = x.second;
+        int j = x.idx;
+        merge(b, j, s, y.best, y.idx, y.second);
+        const int gi = i0 + tid;
+        if (gi < NA) parts[((size_t)p * n_jt + blockIdx.x) * cap + gi] = Part{b, j, s};
+    }
+}
+
+__global__ void reduce_parts(const Part *__restrict__ parts, const int32_t *__restrict__ counts,
+                             int cap, PairArg pairs, int n_jt, int32_t *__restrict__ best,
+                             float *__restrict__ d1, float *__restrict__ d2) {
+    const int p = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    int NA = counts[pairs.a[p]], NB = counts[pairs.b[p]];
+    NA = NA < cap ? NA : cap;
+    NB = NB < cap ? NB : cap;
+    float b = INFINITY, s = INFINITY;
+    int j = -1;
+    if (i < NA) {
+        j = 0x7fffffff;
+        const int nt = (NB + MT - 1) / MT;
+        for (int t = 0; t < nt; ++t) {
+            const Part q = parts[((size_t)p * n_jt + t) * cap + i];
+            merge(b, j, s, q.best, q.idx, q.second);
+        }
+        if (NB == 0) j = -1;
+    }
+    best[(size_t)p * cap + i] = j;
+    d1[(size_t)p * cap + i] = b;
+    d2[(size_t)p * cap + i] = s;
+}
+
+// ---------------------------------------------------------------- Harris (float descriptors)
+__device__ float sdot_skx_diff(const float *a, const float *b) {
+    float a16[4][16];
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 16; ++j) a16[k][j] = 0.0f;
+    for (int i = 0; i < 128; i += 64)
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 16; ++j) {
+                const float t = a[i + 16 * k + j] - b[i + 16 * k + j];
+                a16[k][j] = fmaf(t, t, a16[k][j]);
+            }
+    float v[8];
+    for (int j = 0; j < 8; ++j) {
+        const float s0 = a16[0][j] + a16[0][j + 8];
+        const float s1 = a16[1][j] + a16[1][j + 8];
+        const float s2 = a16[2][j] + a16[2][j + 8];
+        const float s3 = a16[3][j] + a16[3][j + 8];
+        v[j] = ((s0 + s1) + s2) + s3;
+    }
+    float h[4];
+    for (int j = 0; j < 4; ++j) h[j] = v[j] + v[j + 4];
+    return (h[0] + h[1]) + (h[2] + h[3]);
+}
+
+__global__ void __launch_bounds__(256)
+dist_direct(const float *__restrict__ desc, const int32_t *__restrict__ counts, int cap,
+            PairArg pairs, int32_t *__restrict__ best, float *__restrict__ d1,
+            float *__restrict__ d2) {
+    __shared__ float arow[PANO_DESC_DIM];
+    __shared__ float rb[256];
+    __shared__ int rj[256];
+    __shared__ float rs[256];
+    const int p = blockIdx.y, i = blockIdx.x, tid = threadIdx.x;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    int NA = counts[fa], NB = counts[fb];
+    NA = NA < cap ? NA : cap;
+    NB = NB < cap ? NB : cap;
+    if (i >= cap) return;
+    if (i >= NA) {
+        if (tid == 0) {
+            best[(size_t)p * cap + i] = -1;
+            d1[(size_t)p * cap + i] = INFINITY;
+            d2[(size_t)p * cap + i] = INFINITY;
+        }
+        return;
+    }
+    if (tid < PANO_DESC_DIM) arow[tid] = desc[((size_t)fa * cap + i) * PANO_DESC_DIM + tid];
+    __syncthreads();
+    float b = INFINITY, s = INFINITY;
+    int j = 0x7fffffff;
+    for (int jj = tid; jj < NB; jj += 256) {
+        const float d = sdot_skx_diff(arow, desc + ((size_t)fb * cap + jj) * PANO_DESC_DIM);
+        merge(b, j, s, d, jj, INFINITY);
+    }
+    rb[tid] = b;
+    rj[tid] = j;
+    rs[tid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        float B = INFINITY, Sx = INFINITY;
+        int J = 0x7fffffff;
+        for (int t = 0; t < 256; ++t) merge(B, J, Sx, rb[t], rj[t], rs[t]);
+        best[(size_t)p * cap + i] = NB > 0 ? J : -1;
+        d1[(size_t)p * cap + i] = B;
+        d2[(size_t)p * cap + i] = Sx;
+    }
+}
+
+}  // namespace
+
+int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
+                 const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
+                 float *d2) {
+    if (cap <= 0 || n_pairs <= 0 || !desc || !counts || !best || !d1 || !d2)
+        return pano_fail(ctx, PANO_E_ARG, "pano_match: bad arguments");
+    int n_frames = 0;
+    for (int q = 0; q < 2 * n_pairs; ++q) n_frames = h_pairs[q] + 1 > n_frames ? h_pairs[q] + 1 : n_frames;
+    for (int p0 = 0; p0 < n_pairs; p0 += 256) {
+        const int np = n_pairs - p0 < 256 ? n_pairs - p0 : 256;
+        PairArg pa;
+        for (int q = 0; q < np; ++q) {
+            pa.a[q] = h_pairs[2 * (p0 + q)];
+            pa.b[q] = h_pairs[2 * (p0 + q) + 1];
+        }
+        int32_t *bp = best + (size_t)p0 * cap;
+        float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 + (size_t)p0 * cap;
+        if (!exact_int) {
+            dim3 grid(cap, np);
+            dist_direct<<<grid, 256, 0, ctx->stream>>>(desc, counts, cap, pa, bp, p1, p2);
+            PANO_LAUNCH_CHECK(ctx, "dist_direct");
+            continue;
+        }
+        const int n_t = (cap + MT - 1) / MT;
+        const size_t norm_bytes = ((size_t)n_frames * cap * sizeof(float) + 255) & ~size_t(255);
+        const size_t part_bytes = (size_t)np * n_t * cap * sizeof(Part);
+        int rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes, norm_bytes + part_bytes);
+        if (rc) return rc;
+        float *norms = (float *)ctx->mscratch;
+        Part *parts = (Part *)((char *)ctx->mscratch + norm_bytes);
+        const size_t rows = (size_t)n_frames * cap;
+        row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
+        PANO_LAUNCH_CHECK(ctx, "row_norms");
+        dim3 grid(n_t, n_t, np);
+        dist_mfma<<<grid, 256, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+        PANO_LAUNCH_CHECK(ctx, "dist_mfma");
+        dim3 g2((cap + 255) / 256, np);
+        reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_t, bp, p1, p2);
+        PANO_LAUNCH_CHECK(ctx, "reduce_parts");
+    }
+    return PANO_OK;
+}

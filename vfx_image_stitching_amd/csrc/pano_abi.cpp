@@ -1,0 +1,218 @@
+// pano_abi.cpp -- the extern "C" surface declared in include/pano.h.
+//
+// Thin: argument checks, the per-device context (stream + scratch), and dispatch to the
+// launchers of the .hip translation units.  Nothing here computes image data.
+#include <cstdio>
+#include <cstring>
+
+#include "pano_internal.h"
+
+int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p);
+int sift_plan(const pano_sift_params *p, int h, int w, int *n_oct, int *n_lvl, double *sig_base,
+              double *sig_lvl);
+int sift_set_attributes(pano_ctx *ctx);
+int harris_set_attributes(pano_ctx *ctx);
+
+int pano_fail(pano_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int pano_hip_check(pano_ctx *ctx, hipError_t e, const char *what) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    return pano_fail(ctx, PANO_E_HIP, buf);
+}
+
+int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need) {
+    if (need <= *have && *p) return PANO_OK;
+    if (*p) {
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return pano_hip_check(ctx, e, "grow sync");
+        (void)hipFree(*p);
+        *p = nullptr;
+        *have = 0;
+    }
+    size_t sz = need + need / 4 + 4096;
+    hipError_t e = hipMalloc(p, sz);
+    if (e != hipSuccess) return pano_hip_check(ctx, e, "hipMalloc scratch");
+    *have = sz;
+    return PANO_OK;
+}
+
+extern "C" {
+
+const char *pano_version(void) { return "libpano 0.1 gfx950"; }
+
+void pano_sift_default_params(pano_sift_params *p) {
+    p->sigma = 1.6;
+    p->num_intervals = 3;
+    p->assumed_blur = 0.5;
+    p->border = 5;
+    p->contrast_threshold = 0.04;
+    p->eigen_ratio = 10;
+    p->max_iter = 5;
+    p->radius_factor = 3;
+    p->peak_ratio = 0.8;
+    p->scale_factor = 1.5;
+    p->scale_multiplier = 3;
+    p->descriptor_max = 0.2;
+}
+
+// Host-only: the scalar plan of a SIFT run (octaves, per-level sigmas) -- CPU-testable.
+int pano_sift_plan(const pano_sift_params *p, int h, int w, int *n_oct, int *n_lvl,
+                   double *sig_base, double *sig_lvl) {
+    if (!p || !n_oct || !n_lvl || !sig_base || !sig_lvl || h <= 0 || w <= 0) return PANO_E_ARG;
+    return sift_plan(p, h, w, n_oct, n_lvl, sig_base, sig_lvl);
+}
+
+int pano_ctx_create(int device, void *stream, pano_ctx **out) {
+    if (!out) return PANO_E_ARG;
+    *out = nullptr;
+    pano_ctx *ctx = new pano_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete ctx;
+        return PANO_E_HIP;
+    }
+    ctx->stream = (hipStream_t)stream;
+    int rc = sift_set_attributes(ctx);
+    if (!rc) rc = harris_set_attributes(ctx);
+    if (rc) {
+        delete ctx;
+        return rc;
+    }
+    *out = ctx;
+    return PANO_OK;
+}
+
+int pano_ctx_destroy(pano_ctx *ctx) {
+    if (!ctx) return PANO_OK;
+    (void)hipStreamSynchronize(ctx->stream);
+    void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
+                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    delete ctx;
+    return PANO_OK;
+}
+
+int pano_ctx_set_stream(pano_ctx *ctx, void *stream) {
+    if (!ctx) return PANO_E_ARG;
+    ctx->stream = (hipStream_t)stream;
+    return PANO_OK;
+}
+
+int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap) {
+    if (!ctx || n <= 0 || h <= 0 || w <= 0 || cap <= 0) return PANO_E_ARG;
+    pano_sift_params p;
+    pano_sift_default_params(&p);
+    return sift_reserve_pyramid(ctx, n, h, w, &p);
+}
+
+int pano_sync(pano_ctx *ctx) {
+    if (!ctx) return PANO_E_ARG;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return pano_hip_check(ctx, e, "pano_sync");
+    if (ctx->counters && ctx->n > 0) {
+        int32_t err = 0;
+        e = hipMemcpy(&err, ctx->counters + 2 * ctx->n, sizeof err, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && err) return pano_fail(ctx, PANO_E_OVERFLOW, "keypoint capacity exceeded");
+    }
+    return PANO_OK;
+}
+
+const char *pano_last_error(pano_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pano_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
+                     const double *focal, uint8_t *colnz) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_cylindrical(ctx, src, dst, n, h, w, focal, colnz);
+}
+
+int pano_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
+                      const pano_sift_params *params) {
+    if (!ctx || !bgr || n <= 0 || h <= 0 || w <= 0) return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_pyramid") : PANO_E_ARG;
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    return launch_sift_pyramid(ctx, bgr, n, h, w, &p);
+}
+
+int pano_sift(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
+              const pano_sift_params *params, pano_kp *kps, float *desc, int cap,
+              int32_t *counts) {
+    if (!ctx) return PANO_E_ARG;
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p);
+    if (rc) return rc;
+    return launch_sift_keypoints(ctx, &p, kps, desc, cap, counts);
+}
+
+int pano_sift_level_shape(pano_ctx *ctx, int octave, int *h_out, int *w_out, int *n_octaves) {
+    if (!ctx || octave < 0 || octave >= ctx->n_oct) return PANO_E_ARG;
+    if (h_out) *h_out = ctx->oct_h[octave];
+    if (w_out) *w_out = ctx->oct_w[octave];
+    if (n_octaves) *n_octaves = ctx->n_oct;
+    return PANO_OK;
+}
+
+int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int dog, float *out) {
+    if (!ctx || !out || frame < 0 || frame >= ctx->n || octave < 0 || octave >= ctx->n_oct)
+        return PANO_E_ARG;
+    const int nl = dog ? ctx->n_lvl - 1 : ctx->n_lvl;
+    if (level < 0 || level >= nl) return PANO_E_ARG;
+    const size_t plane = (size_t)ctx->oct_h[octave] * ctx->oct_w[octave];
+    const float *src = dog ? ctx->dog + ctx->dog_off[octave][level] : ctx->pyr + ctx->gauss_off[octave][level];
+    PANO_HIP(ctx, hipMemcpyAsync(out, src + (size_t)frame * plane, plane * sizeof(float),
+                                 hipMemcpyDeviceToDevice, ctx->stream));
+    return PANO_OK;
+}
+
+int pano_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int max_points,
+                int32_t *xy, float *desc, int32_t *counts) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_harris(ctx, bgr, n, h, w, max_points, xy, desc, counts);
+}
+
+int pano_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
+               const int32_t *pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
+               float *d2) {
+    if (!ctx || !pairs) return PANO_E_ARG;
+    return launch_match(ctx, desc, counts, cap, pairs, n_pairs, exact_int, best, d1, d2);
+}
+
+int pano_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
+                     const int32_t *counts, int cap, const int32_t *pairs, int n_pairs,
+                     const int32_t *best, const float *d1, const float *d2, double desc_thresh,
+                     double ratio, double ransac_thr, pano_pair_rec *recs) {
+    if (!ctx || !pairs) return PANO_E_ARG;
+    return launch_pair_shifts(ctx, kps, xy_i32, counts, cap, pairs, n_pairs, best, d1, d2,
+                              desc_thresh, ratio, ransac_thr, recs);
+}
+
+int pano_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr, int32_t *out) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_ransac_translate(ctx, moves, k, thr, out);
+}
+
+int pano_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                   int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas, int H,
+                   int W) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_composite(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W);
+}
+
+int pano_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,
+                   int wB, const int32_t *geom, double overlap, uint8_t *out) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_blend_two(ctx, A, hA, wA, B, hB, wB, geom, overlap, out);
+}
+
+int pano_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_gray_bbox(ctx, img, H, W, thr, bbox);
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// pano_internal.h -- shared declarations of the gfx950 kernels behind include/pano.h.
+//
+// Numerics policy (DESIGN.md "Parity"): every translation unit is compiled with
+// -ffp-contract=off so that a*b+c is two roundings unless a kernel asks for fma()
+// explicitly.  fma() is used only where the product is exact (f32 x f32 in double: the
+// separable Gaussian taps) or where the reference's own arithmetic is an FMA (the OpenBLAS
+// sdot order numpy uses).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/pano.h"
+
+#define PANO_MAX_OCTAVES 16
+#define PANO_MAX_LEVELS 8      // num_intervals + 3 <= 8  -> num_intervals <= 5
+#define PANO_MAX_TAPS 64
+#define PANO_ORI_BINS 36
+
+// Raw keypoint produced by the orientation kernel (before sort/dedup/convert), in base
+// (2x upsampled) coordinates, exactly the fields sift_impl.py:206-210/290 stores, plus a
+// deterministic scan-order tie-break (candidate id << 8 | peak index).
+struct RawKp {
+    float x, y, size, angle, response;
+    int32_t octave;       // packed cv2 octave field
+    int32_t frame;
+    uint32_t order;       // scan-order tie-break
+};
+
+// Localised extremum (sift_impl.py:169-211 output) waiting for orientation assignment.
+struct Cand {
+    float x, y, size, response;   // KeyPoint fields (base coordinates)
+    int32_t octave_field;
+    int16_t octave, layer;        // octave index and localised layer
+    int32_t frame;
+    uint32_t order;               // scan order: ((octave*8 + layer0) * 2^20 ...) see extrema
+};
+
+// Device-side view of one pyramid level of a frame batch.
+struct LevelView {
+    float *ptr;      // [n][h][w]
+    int h, w;
+};
+
+struct pano_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // ---- SIFT scratch (grown on demand by reserve)
+    int n = 0, h = 0, w = 0, cap = 0;
+    int n_oct = 0, n_lvl = 0;           // octaves, Gaussian levels per octave
+    int oct_h[PANO_MAX_OCTAVES], oct_w[PANO_MAX_OCTAVES];
+    size_t pyr_bytes = 0;
+    float *pyr = nullptr;                // Gaussian levels, all octaves
+    float *dog = nullptr;                // DoG levels, all octaves
+    size_t gauss_off[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
+    size_t dog_off[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
+    Cand *cands = nullptr;   size_t cand_cap = 0;
+    RawKp *raw = nullptr;    size_t raw_cap = 0;
+    int32_t *counters = nullptr;         // [0]=cands [1]=raw [2..2+n) per-frame raw counts
+    size_t counters_n = 0;
+    int32_t *frame_off = nullptr;        // per-frame raw offsets (n+1)
+    RawKp *raw_sorted = nullptr;
+    double *taps = nullptr;              // device Gaussian taps, per level
+    // ---- match / ransac scratch
+    void *mscratch = nullptr; size_t mscratch_bytes = 0;
+    // ---- composite scratch
+    uint8_t *flags = nullptr; size_t flags_bytes = 0;
+    // ---- harris scratch
+    void *hscratch = nullptr; size_t hscratch_bytes = 0;
+    // ---- blend scratch
+    void *bscratch = nullptr; size_t bscratch_bytes = 0;
+};
+
+int pano_fail(pano_ctx *ctx, int code, const std::string &msg);
+int pano_hip_check(pano_ctx *ctx, hipError_t e, const char *what);
+int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need);
+
+#define PANO_HIP(ctx, call)                                                  \
+    do {                                                                     \
+        hipError_t e__ = (call);                                             \
+        if (e__ != hipSuccess) return pano_hip_check((ctx), e__, #call);     \
+    } while (0)
+
+#define PANO_LAUNCH_CHECK(ctx, what)                                         \
+    do {                                                                     \
+        hipError_t e__ = hipGetLastError();                                  \
+        if (e__ != hipSuccess) return pano_hip_check((ctx), e__, (what));    \
+    } while (0)
+
+// ---- host launchers implemented in the .hip translation units
+int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
+                       const double *h_focal, uint8_t *colnz);
+int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
+                        const pano_sift_params *p);
+int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
+                          int cap, int32_t *counts);
+int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int max_points,
+                  int32_t *xy, float *desc, int32_t *counts);
+int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
+                 const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
+                 float *d2);
+int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
+                       const int32_t *counts, int cap, const int32_t *h_pairs, int n_pairs,
+                       const int32_t *best, const float *d1, const float *d2,
+                       double desc_thresh, double ratio, double thr, pano_pair_rec *recs);
+int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr,
+                            int32_t *out);
+int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                     int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
+                     int H, int W);
+int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,
+                     int wB, const int32_t *geom, double overlap, uint8_t *out);
+int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox);
+
+// ---- device helpers
+__device__ __forceinline__ int reflect101(int i, int n) {
+    // BORDER_REFLECT_101, periodic beyond one reflection (cv2_compat.reflect101).
+    if (n == 1) return 0;
+    const int period = 2 * n - 2;
+    int m = i % period;
+    if (m < 0) m += period;
+    return m >= n ? period - m : m;
+}
+
+__device__ __forceinline__ uint8_t gray_u8(const uint8_t *p) {
+    // OpenCV fixed-point BGR->GRAY (cv2_compat.bgr_to_gray_u8).
+    return (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14);
+}
+
+// numpy.round / Python round: half to even.
+__device__ __forceinline__ float round_half_even_f(float v) { return rintf(v); }
+__device__ __forceinline__ double round_half_even(double v) { return rint(v); }
+
+// numpy float remainder (npy_divmod): result has the sign of the divisor.
+__device__ __forceinline__ float np_remainder_f(float a, float b) {
+    float m = fmodf(a, b);
+    if (m != 0.0f) {
+        if ((b < 0.0f) != (m < 0.0f)) m += b;
+    } else {
+        m = copysignf(0.0f, b);
+    }
+    return m;
+}
+__device__ __forceinline__ double np_remainder(double a, double b) {
+    double m = fmod(a, b);
+    if (m != 0.0) {
+        if ((b < 0.0) != (m < 0.0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}

@@ -1,0 +1,208 @@
+// ransac.hip -- R1: match filtering + exhaustive translation voting.
+//
+//   compute_shift_sift  image_stitching_sift.py:74-82   accept i if best_dist < desc_thresh
+//   ransac              image_stitching_sift.py:86-111  (= image_stitching_harris.py:242-271)
+//
+// Every accepted match is a hypothesis (no sampling): votes_m = #{j : (dx_j - dx_m)^2 +
+// (dy_j - dy_m)^2 < thr} in double (Python floats; no contraction), and the FIRST maximum
+// in match order wins (strict '>' at :107).  One 1024-thread workgroup per pair: an
+// order-preserving compaction of the accepted rows, an LDS-tiled K x K vote, and a
+// (votes desc, index asc) block reduction.
+#include "pano_internal.h"
+
+namespace {
+
+constexpr int RB = 1024;
+
+struct PairArg {
+    int32_t a[256], b[256];
+};
+
+__device__ int block_excl_scan(int v, int *sh, int &total) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < RB; off <<= 1) {
+        const int t = tid >= off ? sh[tid - off] : 0;
+        __syncthreads();
+        sh[tid] += t;
+        __syncthreads();
+    }
+    total = sh[RB - 1];
+    const int r = sh[tid] - v;
+    __syncthreads();
+    return r;
+}
+
+// votes for every move of `mv[0..k)`, then first-max; results in *best_m, *best_v
+__device__ void vote_argmax(const double2 *mv, int k, double thr, double2 *tile, int *ish,
+                            int *best_m, int *best_v) {
+    const int tid = threadIdx.x;
+    int my_best_v = -1, my_best_m = 0x7fffffff;
+    for (int m0 = 0; m0 < k; m0 += RB) {
+        const int m = m0 + tid;
+        const double2 me = m < k ? mv[m] : make_double2(0.0, 0.0);
+        int votes = 0;
+        for (int j0 = 0; j0 < k; j0 += RB) {
+            __syncthreads();
+            if (j0 + tid < k) tile[tid] = mv[j0 + tid];
+            __syncthreads();
+            const int nj = k - j0 < RB ? k - j0 : RB;
+            for (int j = 0; j < nj; ++j) {
+                const double ddx = tile[j].x - me.x;
+                const double ddy = tile[j].y - me.y;
+                const double d = ddx * ddx + ddy * ddy;
+                votes += d < thr;
+            }
+        }
+        if (m < k && votes > my_best_v) {   // m increases per thread: strict '>' keeps first
+            my_best_v = votes;
+            my_best_m = m;
+        }
+    }
+    // block reduction: max votes, then min index
+    __syncthreads();
+    ish[tid] = my_best_v;
+    ish[RB + tid] = my_best_m;
+    __syncthreads();
+    for (int off = RB / 2; off > 0; off >>= 1) {
+        if (tid < off) {
+            const int v2 = ish[tid + off], m2 = ish[RB + tid + off];
+            const int v1 = ish[tid], m1 = ish[RB + tid];
+            if (v2 > v1 || (v2 == v1 && m2 < m1)) {
+                ish[tid] = v2;
+                ish[RB + tid] = m2;
+            }
+        }
+        __syncthreads();
+    }
+    *best_v = ish[0];
+    *best_m = ish[RB];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(RB)
+pair_shifts(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
+            const int32_t *__restrict__ counts, int cap, PairArg pairs,
+            const int32_t *__restrict__ best, const float *__restrict__ d1,
+            const float *__restrict__ d2, float desc_thresh, double ratio2, double thr,
+            double2 *__restrict__ moves, int32_t *__restrict__ midx,
+            pano_pair_rec *__restrict__ recs) {
+    __shared__ int ish[2 * RB];
+    __shared__ double2 tile[RB];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    int NA = counts[fa];
+    NA = NA < cap ? NA : cap;
+    const int32_t *bp = best + (size_t)p * cap;
+    const float *p1 = d1 + (size_t)p * cap, *p2 = d2 + (size_t)p * cap;
+    double2 *mv = moves + (size_t)p * cap;
+    int32_t *mi = midx + (size_t)p * cap;
+    int K = 0;
+    for (int base = 0; base < NA; base += RB) {
+        const int i = base + tid;
+        int acc = 0;
+        if (i < NA && bp[i] >= 0 && p1[i] < desc_thresh)
+            acc = ratio2 > 0.0 ? ((double)p1[i] < ratio2 * (double)p2[i]) : 1;
+        int tot;
+        const int pos = block_excl_scan(acc, ish, tot);
+        if (acc) {
+            const int j = bp[i];
+            double xa, ya, xb, yb;
+            if (kps) {
+                const pano_kp ka = kps[(size_t)fa * cap + i], kb = kps[(size_t)fb * cap + j];
+                xa = ka.x; ya = ka.y; xb = kb.x; yb = kb.y;
+            } else {
+                xa = xy[((size_t)fa * cap + i) * 2];
+                ya = xy[((size_t)fa * cap + i) * 2 + 1];
+                xb = xy[((size_t)fb * cap + j) * 2];
+                yb = xy[((size_t)fb * cap + j) * 2 + 1];
+            }
+            mv[K + pos] = make_double2(xa - xb, ya - yb);
+            mi[K + pos] = i;
+        }
+        K += tot;
+    }
+    __syncthreads();
+    pano_pair_rec r{};
+    r.n_matches = K;
+    if (K == 0) {
+        if (tid == 0) {
+            r.best = -1;
+            r.status = PANO_E_NOMATCH;
+            recs[p] = r;
+        }
+        return;
+    }
+    int bm, bv;
+    vote_argmax(mv, K, thr, tile, ish, &bm, &bv);
+    if (tid == 0) {
+        const int i = mi[bm];
+        const int j = bp[i];
+        if (kps) {
+            const pano_kp ka = kps[(size_t)fa * cap + i], kb = kps[(size_t)fb * cap + j];
+            r.xA = ka.x; r.yA = ka.y; r.xB = kb.x; r.yB = kb.y;
+        } else {
+            r.xA = xy[((size_t)fa * cap + i) * 2];
+            r.yA = xy[((size_t)fa * cap + i) * 2 + 1];
+            r.xB = xy[((size_t)fb * cap + j) * 2];
+            r.yB = xy[((size_t)fb * cap + j) * 2 + 1];
+        }
+        r.dx = mv[bm].x;
+        r.dy = mv[bm].y;
+        r.votes = bv;
+        r.best = bm;
+        r.status = PANO_OK;
+        recs[p] = r;
+    }
+}
+
+__global__ void __launch_bounds__(RB)
+ransac_moves(const double2 *__restrict__ mv, int k, double thr, int32_t *__restrict__ out) {
+    __shared__ int ish[2 * RB];
+    __shared__ double2 tile[RB];
+    if (k <= 0) {
+        if (threadIdx.x == 0) { out[0] = -1; out[1] = 0; }
+        return;
+    }
+    int bm, bv;
+    vote_argmax(mv, k, thr, tile, ish, &bm, &bv);
+    if (threadIdx.x == 0) { out[0] = bm; out[1] = bv; }
+}
+
+}  // namespace
+
+int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
+                       const int32_t *counts, int cap, const int32_t *h_pairs, int n_pairs,
+                       const int32_t *best, const float *d1, const float *d2,
+                       double desc_thresh, double ratio, double thr, pano_pair_rec *recs) {
+    if (cap <= 0 || n_pairs <= 0 || (!kps && !xy_i32) || !counts || !best || !d1 || !d2 || !recs)
+        return pano_fail(ctx, PANO_E_ARG, "pano_pair_shifts: bad arguments");
+    const size_t need = (size_t)n_pairs * cap * (sizeof(double2) + sizeof(int32_t)) + 256;
+    int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, need);
+    if (rc) return rc;
+    double2 *moves = (double2 *)ctx->bscratch;
+    int32_t *midx = (int32_t *)(moves + (size_t)n_pairs * cap);
+    for (int p0 = 0; p0 < n_pairs; p0 += 256) {
+        const int np = n_pairs - p0 < 256 ? n_pairs - p0 : 256;
+        PairArg pa;
+        for (int q = 0; q < np; ++q) {
+            pa.a[q] = h_pairs[2 * (p0 + q)];
+            pa.b[q] = h_pairs[2 * (p0 + q) + 1];
+        }
+        pair_shifts<<<np, RB, 0, ctx->stream>>>(
+            kps, xy_i32, counts, cap, pa, best + (size_t)p0 * cap, d1 + (size_t)p0 * cap,
+            d2 + (size_t)p0 * cap, (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, thr,
+            moves + (size_t)p0 * cap, midx + (size_t)p0 * cap, recs + p0);
+        PANO_LAUNCH_CHECK(ctx, "pair_shifts");
+    }
+    return PANO_OK;
+}
+
+int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr,
+                            int32_t *out) {
+    if (k < 0 || (k > 0 && !moves) || !out) return pano_fail(ctx, PANO_E_ARG, "pano_ransac_translate");
+    ransac_moves<<<1, RB, 0, ctx->stream>>>((const double2 *)moves, k, thr, out);
+    PANO_LAUNCH_CHECK(ctx, "ransac_moves");
+    return PANO_OK;
+}

@@ -1,0 +1,608 @@
+// sift_features.hip -- S5..S9 of sift_impl.py on the pyramid built by sift_pyramid.hip.
+//
+//   extrema_localize  find_scale_space_extrema :117-140 + is_pixel_an_extremum :143-163
+//                     + localize_extremum_via_quadratic_fit :169-211 (thread per pixel)
+//   orientation       compute_keypoints_with_orientations :246-293 (wave per candidate)
+//   sort_dedup        compare_keypoints / remove_duplicate_keypoints :299-327
+//                     + convert_keypoints_to_input_image_size :333-343 (workgroup per frame)
+//   descriptor        unpack_octave :349-358 + generate_descriptors :361-526
+//                     (workgroup per keypoint)
+//
+// Parity notes (DESIGN.md "Parity"):
+//  * extrema decisions are exact f32 comparisons; the cube / gradient / Hessian are the
+//    reference's f32 expressions in its evaluation order (no contraction);
+//  * lstsq (numpy: LAPACK dgelsd in double, result cast to f32) is a Jacobi
+//    pseudo-inverse in double with numpy's rcond = 3 * DBL_EPSILON cut;
+//  * np.dot of two 3-vectors = f32 products summed in double (OpenBLAS tail loop);
+//  * histograms accumulate in 64-bit fixed point (order independent => deterministic, and
+//    more accurate than the reference's sequential sums);
+//  * np.linalg.norm of the 128-vector reproduces OpenBLAS's SkylakeX sdot order exactly;
+//  * numpy's SIMD expf/atan2f are not correctly rounded (1-3 ulp); the kernels use
+//    (near) correctly rounded versions, so angles and descriptor bins agree to ulps and
+//    integer descriptors to <= 1 LSB.
+#include "pano_internal.h"
+
+namespace {
+
+constexpr float kRad2DegF32 = 180.0f / 3.14159265358979323846f;   // numpy f32 rad2deg
+constexpr double kHistScale = 1099511627776.0;                    // 2^40 fixed point
+constexpr double kHistInv = 1.0 / 1099511627776.0;
+constexpr double kDescScale = 1099511627776.0;
+constexpr double kDescInv = 1.0 / 1099511627776.0;
+constexpr int kSortMax = 8192;
+
+struct OctArgs {
+    const float *dog[PANO_MAX_LEVELS];
+    const float *gauss[PANO_MAX_LEVELS];
+    int H, W;
+};
+
+struct PyrArgs {   // all octaves, for the descriptor (level pointers are per frame batch)
+    const float *gauss[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
+    int H[PANO_MAX_OCTAVES], W[PANO_MAX_OCTAVES];
+    int n_oct;
+};
+
+struct LocParams {
+    double thresh;          // floor(0.5 * contrast / ni * 255)
+    float contrast;         // f32(contrast_threshold)
+    float edge_lhs;         // f32(eigen_ratio)
+    float edge_rhs;         // f32((eigen_ratio + 1)^2)
+    float sigma_f;          // f32(sigma)
+    int ni, border, max_iter, octave;
+};
+
+// ------------------------------------------------------------------ 3x3 lstsq
+// Symmetric Jacobi eigen-decomposition -> min-norm least-squares solution, cutting
+// singular values <= rcond * s_max like LAPACK dgelsd with numpy's default rcond.
+__device__ void lstsq3_sym(const double A[3][3], const double b[3], double x[3]) {
+    double a[3][3], v[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            a[i][j] = A[i][j];
+            v[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 16; ++sweep) {
+        const double off = fabs(a[0][1]) + fabs(a[0][2]) + fabs(a[1][2]);
+        if (off == 0.0) break;
+        for (int pq = 0; pq < 3; ++pq) {
+            const int p = pq == 2 ? 1 : 0;
+            const int q = pq == 0 ? 1 : 2;
+            const double apq = a[p][q];
+            if (apq == 0.0) continue;
+            const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+            const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            const double c = 1.0 / sqrt(t * t + 1.0);
+            const double s = t * c;
+            for (int k = 0; k < 3; ++k) {   // A <- A J
+                const double akp = a[k][p], akq = a[k][q];
+                a[k][p] = c * akp - s * akq;
+                a[k][q] = s * akp + c * akq;
+            }
+            for (int k = 0; k < 3; ++k) {   // A <- J^T A
+                const double apk = a[p][k], aqk = a[q][k];
+                a[p][k] = c * apk - s * aqk;
+                a[q][k] = s * apk + c * aqk;
+            }
+            a[p][q] = a[q][p] = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                const double vkp = v[k][p], vkq = v[k][q];
+                v[k][p] = c * vkp - s * vkq;
+                v[k][q] = s * vkp + c * vkq;
+            }
+        }
+    }
+    double smax = 0.0;
+    for (int k = 0; k < 3; ++k) smax = fmax(smax, fabs(a[k][k]));
+    const double cut = 3.0 * 2.220446049250313e-16 * smax;
+    x[0] = x[1] = x[2] = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double lam = a[k][k];
+        if (!(fabs(lam) > cut)) continue;
+        const double coef = (v[0][k] * b[0] + v[1][k] * b[1] + v[2][k] * b[2]) / lam;
+        for (int i = 0; i < 3; ++i) x[i] += coef * v[i][k];
+    }
+}
+
+__device__ __forceinline__ float dog_at(const OctArgs &a, int lvl, int f, int y, int x) {
+    return a.dog[lvl][((size_t)f * a.H + y) * a.W + x];
+}
+
+// ------------------------------------------------------------------ S5 + S6
+__global__ void __launch_bounds__(256)
+extrema_localize(OctArgs a, LocParams lp, Cand *__restrict__ cands,
+                 int32_t *__restrict__ cand_cnt, int cand_cap) {
+    const int ni = lp.ni, border = lp.border;
+    const int x = border + blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = border + blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int layer0 = 1 + (int)(blockIdx.z % ni);
+    const int f = (int)(blockIdx.z / ni);
+    const int H = a.H, W = a.W;
+    if (x >= W - border || y >= H - border) return;
+    const float v = dog_at(a, layer0, f, y, x);
+    if (!((double)fabsf(v) > lp.thresh)) return;
+    bool ok = true;
+    if (v > 0) {
+        for (int dz = -1; dz <= 1 && ok; ++dz)
+            for (int dy = -1; dy <= 1 && ok; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (!(v >= dog_at(a, layer0 + dz, f, y + dy, x + dx))) { ok = false; break; }
+                }
+    } else {
+        for (int dz = -1; dz <= 1 && ok; ++dz)
+            for (int dy = -1; dy <= 1 && ok; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (!(v <= dog_at(a, layer0 + dz, f, y + dy, x + dx))) { ok = false; break; }
+                }
+    }
+    if (!ok) return;
+
+    // ---- quadratic fit (sift_impl.py:169-211), keeping the max_iter quirk
+    int xi = x, yi = y, li = layer0;
+    float c[3][3][3];
+    float g[3], Hs[3][3], u[3];
+    for (int it = 0; it < lp.max_iter; ++it) {
+        for (int dz = 0; dz < 3; ++dz)
+            for (int dy = 0; dy < 3; ++dy)
+                for (int dx = 0; dx < 3; ++dx)
+                    c[dz][dy][dx] = dog_at(a, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx) / 255.0f;
+        const float cv = c[1][1][1];
+        g[0] = 0.5f * (c[1][1][2] - c[1][1][0]);
+        g[1] = 0.5f * (c[1][2][1] - c[1][0][1]);
+        g[2] = 0.5f * (c[2][1][1] - c[0][1][1]);
+        const float v2 = 2.0f * cv;
+        const float dxx = (c[1][1][2] - v2) + c[1][1][0];
+        const float dyy = (c[1][2][1] - v2) + c[1][0][1];
+        const float dss = (c[2][1][1] - v2) + c[0][1][1];
+        const float dxy = 0.25f * (((c[1][2][2] - c[1][2][0]) - c[1][0][2]) + c[1][0][0]);
+        const float dxs = 0.25f * (((c[2][1][2] - c[2][1][0]) - c[0][1][2]) + c[0][1][0]);
+        const float dys = 0.25f * (((c[2][2][1] - c[2][0][1]) - c[0][2][1]) + c[0][0][1]);
+        Hs[0][0] = dxx; Hs[0][1] = dxy; Hs[0][2] = dxs;
+        Hs[1][0] = dxy; Hs[1][1] = dyy; Hs[1][2] = dys;
+        Hs[2][0] = dxs; Hs[2][1] = dys; Hs[2][2] = dss;
+        double A[3][3], b[3], sol[3];
+        for (int i = 0; i < 3; ++i) {
+            b[i] = g[i];
+            for (int j = 0; j < 3; ++j) A[i][j] = Hs[i][j];
+        }
+        lstsq3_sym(A, b, sol);
+        for (int i = 0; i < 3; ++i) u[i] = -(float)sol[i];
+        if (fabsf(u[0]) < 0.5f && fabsf(u[1]) < 0.5f && fabsf(u[2]) < 0.5f) break;
+        xi += (int)rintf(u[0]);
+        yi += (int)rintf(u[1]);
+        li += (int)rintf(u[2]);
+        if (yi < border || yi >= H - border || xi < border || xi >= W - border || li < 1 ||
+            li > ni)
+            return;
+    }
+    double dacc = 0.0;
+    for (int i = 0; i < 3; ++i) dacc += (double)(g[i] * u[i]);
+    const float val = c[1][1][1] + 0.5f * (float)dacc;
+    if (fabsf(val) * (float)ni < lp.contrast) return;
+    const float tr = Hs[0][0] + Hs[1][1];
+    const float det = (float)((double)Hs[0][0] * (double)Hs[1][1] -
+                              (double)Hs[0][1] * (double)Hs[1][0]);
+    if (det <= 0.0f || lp.edge_lhs * (tr * tr) >= lp.edge_rhs * det) return;
+
+    const int o = lp.octave;
+    const float so = (float)(1 << o);
+    Cand k;
+    k.x = ((float)xi + u[0]) * so;
+    k.y = ((float)yi + u[1]) * so;
+    k.octave_field = o + li * 256 + (int)rintf((u[2] + 0.5f) * 255.0f) * 65536;
+    const float e = ((float)li + u[2]) / (float)ni;
+    const float p2 = (float)exp2((double)e);            // 2 ** np.float32 (libm powf)
+    k.size = (lp.sigma_f * p2) * (float)(1 << (o + 1));
+    k.response = fabsf(val);
+    k.octave = (int16_t)o;
+    k.layer = (int16_t)li;
+    k.frame = f;
+    k.order = ((uint32_t)(o * 8 + layer0) << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    const int slot = atomicAdd(&cand_cnt[f], 1);
+    if (slot < cand_cap) cands[(size_t)f * cand_cap + slot] = k;
+}
+
+// ------------------------------------------------------------------ S7
+struct OriParams {
+    double scale_factor, radius_factor, peak_ratio;
+};
+
+__global__ void __launch_bounds__(256)
+orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
+            const int32_t *__restrict__ cand_cnt, int cand_cap, RawKp *__restrict__ raw,
+            int32_t *__restrict__ raw_cnt, int raw_cap) {
+    __shared__ unsigned long long hist[4][PANO_ORI_BINS];
+    __shared__ double hd[4][PANO_ORI_BINS];
+    __shared__ double sm[4][PANO_ORI_BINS];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int ci = blockIdx.x * 4 + wv;
+    int cnt = cand_cnt[f];
+    cnt = cnt < cand_cap ? cnt : cand_cap;
+    if ((int)blockIdx.x * 4 >= cnt) return;   // uniform: no wave of this block is active
+    const bool active = ci < cnt;
+    if (lane < PANO_ORI_BINS) hist[wv][lane] = 0ull;
+    __syncthreads();
+    Cand k{};
+    if (active) {
+        k = cands[(size_t)f * cand_cap + ci];
+        const int o = k.octave;
+        const int H = pa.H[o], W = pa.W[o];
+        const float *img = pa.gauss[o][k.layer] + (size_t)f * H * W;
+        const float scale = (float)(op.scale_factor * (double)k.size) / (float)(1 << (o + 1));
+        const int radius = (int)rintf((float)op.radius_factor * scale);
+        const float wfac = -0.5f / (scale * scale);
+        const int cy = (int)rintf(k.y / (float)(1 << o));
+        const int cx = (int)rintf(k.x / (float)(1 << o));
+        const int side = 2 * radius + 1;
+        const int S = side * side;
+        for (int s = lane; s < S; s += 64) {
+            const int dy = s / side - radius;
+            const int dx = s - (s / side) * side - radius;
+            const int yy = cy + dy, xx = cx + dx;
+            if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
+            const float gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
+            const float gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+            const float mag = sqrtf(gx * gx + gy * gy);
+            const float ang =
+                np_remainder_f((float)atan2((double)gy, (double)gx) * kRad2DegF32, 360.0f);
+            const float w = (float)exp((double)(wfac * (float)(dx * dx + dy * dy)));
+            const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
+            const double val = (double)(w * mag);
+            atomicAdd(&hist[wv][bin], (unsigned long long)llrint(val * kHistScale));
+        }
+    }
+    __syncthreads();
+    if (lane < PANO_ORI_BINS) hd[wv][lane] = (double)(long long)hist[wv][lane] * kHistInv;
+    __syncthreads();
+    if (lane < PANO_ORI_BINS) {
+        const int b = lane, nb = PANO_ORI_BINS;
+        const double *h = hd[wv];
+        sm[wv][b] = ((6 * h[b] + 4 * (h[(b + nb - 1) % nb] + h[(b + 1) % nb])) +
+                     h[(b + nb - 2) % nb]) + h[(b + 2) % nb];
+        sm[wv][b] = sm[wv][b] / 16.0;
+    }
+    __syncthreads();
+    if (!active || lane >= PANO_ORI_BINS) return;
+    const int nb = PANO_ORI_BINS;
+    const double *s = sm[wv];
+    double mx = s[0];
+    for (int b = 1; b < nb; ++b) mx = fmax(mx, s[b]);
+    const int p = lane;
+    const double l = s[(p + nb - 1) % nb], r = s[(p + 1) % nb];
+    if (!(s[p] > l && s[p] > r)) return;
+    if (!(s[p] >= op.peak_ratio * mx)) return;
+    const double interp = np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * s[p]) + r), (double)nb);
+    double angle = 360.0 - interp * 360.0 / nb;
+    if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
+    RawKp q;
+    q.x = k.x;
+    q.y = k.y;
+    q.size = k.size;
+    q.angle = (float)angle;
+    q.response = k.response;
+    q.octave = k.octave_field;
+    q.frame = f;
+    q.order = ((uint64_t)k.order << 6) | (uint64_t)p;
+    const int slot = atomicAdd(&raw_cnt[f], 1);
+    if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = q;
+}
+
+// ------------------------------------------------------------------ S8
+__device__ __forceinline__ uint32_t sortable(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// strict "a before b" of compare_keypoints (x, y asc; size desc; angle asc; response desc),
+// ties by scan order (the reference's stable sort keeps scan order)
+__device__ __forceinline__ bool rec_before(const RawKp &a, const RawKp &b) {
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.angle != b.angle) return a.angle < b.angle;
+    if (a.response != b.response) return a.response > b.response;
+    return a.order < b.order;
+}
+
+__global__ void __launch_bounds__(1024)
+sort_dedup(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
+           pano_kp *__restrict__ out, int cap, int32_t *__restrict__ counts,
+           int32_t *__restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    unsigned long long *key = (unsigned long long *)smem_raw;      // [kSortMax]
+    uint32_t *idx = (uint32_t *)(key + kSortMax);                  // [kSortMax]
+    __shared__ int32_t scan[1024];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const RawKp *rec = raw + (size_t)f * raw_cap;
+    int cnt = raw_cnt[f];
+    if (cnt > raw_cap || cnt > kSortMax) {
+        if (tid == 0) { err[0] = PANO_E_OVERFLOW; counts[f] = -1; }
+        return;
+    }
+    int n2 = 1;
+    while (n2 < cnt) n2 <<= 1;
+    for (int i = tid; i < n2; i += 1024) {
+        if (i < cnt) {
+            key[i] = ((unsigned long long)sortable(rec[i].x) << 32) | sortable(rec[i].y);
+            idx[i] = (uint32_t)i;
+        } else {
+            key[i] = ~0ull;
+            idx[i] = 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= n2; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < n2; i += 1024) {
+                const int l = i ^ j;
+                if (l <= i) continue;
+                const bool asc = (i & kk) == 0;
+                bool lt;   // element l strictly before element i
+                const unsigned long long ki = key[i], kl = key[l];
+                const uint32_t ii = idx[i], il = idx[l];
+                if (ki != kl) lt = kl < ki;
+                else if (ii == 0xFFFFFFFFu || il == 0xFFFFFFFFu) lt = ii == 0xFFFFFFFFu && il != 0xFFFFFFFFu;
+                else lt = rec_before(rec[il], rec[ii]);
+                if (asc == lt) {
+                    key[i] = kl; key[l] = ki;
+                    idx[i] = il; idx[l] = ii;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // de-duplicate consecutive equal (pt, size, angle), then block-wide exclusive scan
+    const int per = (n2 + 1023) / 1024;
+    const int beg = tid * per;
+    int mine = 0;
+    for (int t = 0; t < per; ++t) {
+        const int i = beg + t;
+        if (i >= cnt) break;
+        bool keep = true;
+        if (i > 0) {
+            const RawKp &a = rec[idx[i - 1]], &b = rec[idx[i]];
+            keep = !(a.x == b.x && a.y == b.y && a.size == b.size && a.angle == b.angle);
+        }
+        mine += keep;
+    }
+    scan[tid] = mine;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int v = tid >= off ? scan[tid - off] : 0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+    }
+    int pos = scan[tid] - mine;
+    for (int t = 0; t < per; ++t) {
+        const int i = beg + t;
+        if (i >= cnt) break;
+        const RawKp &b = rec[idx[i]];
+        bool keep = true;
+        if (i > 0) {
+            const RawKp &a = rec[idx[i - 1]];
+            keep = !(a.x == b.x && a.y == b.y && a.size == b.size && a.angle == b.angle);
+        }
+        if (!keep) continue;
+        if (pos < cap) {
+            pano_kp q;
+            q.x = b.x * 0.5f;
+            q.y = b.y * 0.5f;
+            q.size = b.size * 0.5f;
+            q.angle = b.angle;
+            q.response = b.response;
+            q.octave = (b.octave & ~255) | ((b.octave - 1) & 255);
+            out[(size_t)f * cap + pos] = q;
+        }
+        ++pos;
+    }
+    if (tid == 1023) counts[f] = scan[1023];
+}
+
+// ------------------------------------------------------------------ S9
+// OpenBLAS 0.3.29 SkylakeX sdot order (oracle/numerics.py::sdot_skx), one thread.
+__device__ float sdot_skx(const float *x, int n) {
+    const int n64 = n & ~63, n32 = n & ~31;
+    float a16[4][16];
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 16; ++j) a16[k][j] = 0.0f;
+    for (int i = 0; i < n64; i += 64)
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 16; ++j) {
+                const float t = x[i + 16 * k + j];
+                a16[k][j] = fmaf(t, t, a16[k][j]);
+            }
+    float a8[4][8];
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 8; ++j) a8[k][j] = a16[k][j] + a16[k][j + 8];
+    for (int i = n64; i < n32; i += 32)
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 8; ++j) {
+                const float t = x[i + 8 * k + j];
+                a8[k][j] = fmaf(t, t, a8[k][j]);
+            }
+    float v[8];
+    for (int j = 0; j < 8; ++j) v[j] = ((a8[0][j] + a8[1][j]) + a8[2][j]) + a8[3][j];
+    float h[4];
+    for (int j = 0; j < 4; ++j) h[j] = v[j] + v[j + 4];
+    const float kern = (h[0] + h[1]) + (h[2] + h[3]);
+    double tail = 0.0;
+    for (int j = n32; j < n; ++j) tail += (double)(x[j] * x[j]);
+    return (float)((double)kern + tail);
+}
+
+struct DescParams {
+    float hw_mult;     // f32(scale_multiplier * 0.5)
+    float max_value;   // f32(descriptor_max_value)
+};
+
+__global__ void __launch_bounds__(256)
+descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
+           const int32_t *__restrict__ counts, int cap, float *__restrict__ desc) {
+    __shared__ unsigned long long acc[128];
+    __shared__ float vec[128];
+    __shared__ float sh_norm;
+    const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    int cnt = counts[f];
+    cnt = cnt < cap ? cnt : cap;
+    if (k >= cnt) return;
+    if (tid < 128) acc[tid] = 0ull;
+    const pano_kp kp = kps[(size_t)f * cap + k];
+    int oct = kp.octave & 255;
+    if (oct >= 128) oct |= -128;
+    const int lyr = (kp.octave >> 8) & 255;
+    const float scl = oct >= 0 ? 1.0f / (float)(1 << oct) : (float)(1 << -oct);
+    const int O = oct + 1;
+    const int rows = pa.H[O], cols = pa.W[O];
+    const float *img = pa.gauss[O][lyr] + (size_t)f * rows * cols;
+    const int px = (int)rint((double)scl * (double)kp.x);
+    const int py = (int)rint((double)scl * (double)kp.y);
+    const double angle = 360.0 - (double)kp.angle;
+    const double rad = angle * (3.141592653589793 / 180.0);
+    const double cos_a = cos(rad), sin_a = sin(rad);
+    const float hw = (dp.hw_mult * scl) * kp.size;
+    const double hwd = (double)hw;
+    int half = (int)rint(hwd * 1.4142135623730951 * 5.0 * 0.5);
+    const int diag = (int)sqrt((double)(rows * rows + cols * cols));
+    half = half < diag ? half : diag;
+    const int side = 2 * half + 1;
+    const int S = side * side;
+    const float angle_f = (float)angle;
+    const float bins_per_deg = (float)(8.0 / 360.0);
+    __syncthreads();
+    for (int s = tid; s < S; s += 256) {
+        const int ys = s / side - half;
+        const int xs = s - (s / side) * side - half;
+        const int rr = py + ys, cc = px + xs;
+        if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
+        const double rrot = (double)xs * sin_a + (double)ys * cos_a;
+        const double crot = (double)xs * cos_a - (double)ys * sin_a;
+        const double rq = rrot / hwd, cq = crot / hwd;
+        const double rbin = (rq + 2.0) - 0.5;
+        const double cbin = (cq + 2.0) - 0.5;
+        if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) continue;
+        const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
+        const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
+        const float mag = sqrtf(gx * gx + gy * gy);
+        const float ori =
+            np_remainder_f((float)atan2((double)gy, (double)gx) * kRad2DegF32, 360.0f);
+        const double w = exp(-0.125 * (rq * rq + cq * cq));
+        const double wm = w * (double)mag;
+        const float ob = np_remainder_f((ori - angle_f) * bins_per_deg, 8.0f);
+        const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
+        const int o0 = ((int)floorf(ob)) % 8;
+        const double rf = rbin - r0, cf = cbin - c0;
+        const double of = (double)ob - (double)o0;
+        const double c1 = wm * rf;
+        const double c0w = wm - c1;
+        const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rb = r0 + 1 + (q >> 1), cb = c0 + 1 + (q & 1);
+            if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
+            const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
+            const double v0 = part[q] * (1 - of);
+            const double v1 = part[q] * of;
+            atomicAdd(&acc[base + o0], (unsigned long long)llrint(v0 * kDescScale));
+            atomicAdd(&acc[base + (o0 + 1) % 8], (unsigned long long)llrint(v1 * kDescScale));
+        }
+    }
+    __syncthreads();
+    if (tid < 128) vec[tid] = (float)((double)(long long)acc[tid] * kDescInv);
+    __syncthreads();
+    if (tid == 0) sh_norm = sqrtf(sdot_skx(vec, 128)) * dp.max_value;
+    __syncthreads();
+    if (tid < 128 && vec[tid] > sh_norm) vec[tid] = sh_norm;
+    __syncthreads();
+    if (tid == 0) {
+        float nv = sqrtf(sdot_skx(vec, 128));
+        if (nv < 1e-7f) nv = 1e-7f;
+        sh_norm = nv;
+    }
+    __syncthreads();
+    if (tid < 128) {
+        float d = rintf(512.0f * (vec[tid] / sh_norm));
+        d = d < 0.0f ? 0.0f : (d > 255.0f ? 255.0f : d);
+        desc[((size_t)f * cap + k) * PANO_DESC_DIM + tid] = d;
+    }
+}
+
+}  // namespace
+
+int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p);
+
+int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
+                          int cap, int32_t *counts) {
+    const int n = ctx->n, no = ctx->n_oct, nl = ctx->n_lvl, ni = p->num_intervals;
+    if (cap <= 0 || !kps || !desc || !counts) return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
+    // per-frame candidate / raw capacities (raw <= sort capacity)
+    const size_t cand_cap = (size_t)kSortMax;
+    const size_t raw_cap = (size_t)kSortMax;
+    int rc = pano_grow(ctx, (void **)&ctx->cands, &ctx->cand_cap, cand_cap * n * sizeof(Cand));
+    if (rc) return rc;
+    rc = pano_grow(ctx, (void **)&ctx->raw, &ctx->raw_cap, raw_cap * n * sizeof(RawKp));
+    if (rc) return rc;
+    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, (2 * (size_t)n + 8) * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *cand_cnt = ctx->counters;
+    int32_t *raw_cnt = ctx->counters + n;
+    int32_t *err = ctx->counters + 2 * n;
+    PANO_HIP(ctx, hipMemsetAsync(ctx->counters, 0, (2 * (size_t)n + 8) * sizeof(int32_t), ctx->stream));
+
+    LocParams lp;
+    lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);
+    lp.contrast = (float)p->contrast_threshold;
+    lp.edge_lhs = (float)p->eigen_ratio;
+    lp.edge_rhs = (float)((p->eigen_ratio + 1) * (p->eigen_ratio + 1));
+    lp.sigma_f = (float)p->sigma;
+    lp.ni = ni;
+    lp.border = p->border;
+    lp.max_iter = p->max_iter;
+    for (int o = 0; o < no; ++o) {
+        OctArgs a{};
+        a.H = ctx->oct_h[o];
+        a.W = ctx->oct_w[o];
+        for (int l = 0; l < nl; ++l) a.gauss[l] = ctx->pyr + ctx->gauss_off[o][l];
+        for (int l = 0; l < nl - 1; ++l) a.dog[l] = ctx->dog + ctx->dog_off[o][l];
+        const int iw = a.W - 2 * p->border, ih = a.H - 2 * p->border;
+        if (iw <= 0 || ih <= 0) continue;
+        lp.octave = o;
+        dim3 grid((iw + 63) / 64, (ih + 3) / 4, n * ni);
+        extrema_localize<<<grid, 256, 0, ctx->stream>>>(a, lp, ctx->cands, cand_cnt, (int)cand_cap);
+        PANO_LAUNCH_CHECK(ctx, "extrema_localize");
+    }
+    PyrArgs pa{};
+    pa.n_oct = no;
+    for (int o = 0; o < no; ++o) {
+        pa.H[o] = ctx->oct_h[o];
+        pa.W[o] = ctx->oct_w[o];
+        for (int l = 0; l < nl; ++l) pa.gauss[o][l] = ctx->pyr + ctx->gauss_off[o][l];
+    }
+    OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio};
+    {
+        dim3 grid((unsigned)((cand_cap + 3) / 4), n);
+        orientation<<<grid, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap,
+                                                   ctx->raw, raw_cnt, (int)raw_cap);
+        PANO_LAUNCH_CHECK(ctx, "orientation");
+    }
+    {
+        const size_t sm = kSortMax * (sizeof(unsigned long long) + sizeof(uint32_t));
+        sort_dedup<<<n, 1024, sm, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, kps, cap, counts, err);
+        PANO_LAUNCH_CHECK(ctx, "sort_dedup");
+    }
+    {
+        DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
+        dim3 grid(cap, n);
+        descriptor<<<grid, 256, 0, ctx->stream>>>(pa, dp, kps, counts, cap, desc);
+        PANO_LAUNCH_CHECK(ctx, "descriptor");
+    }
+    return PANO_OK;
+}
+
+int sift_set_attributes(pano_ctx *ctx) {
+    const int sm = kSortMax * (sizeof(unsigned long long) + sizeof(uint32_t));
+    PANO_HIP(ctx, hipFuncSetAttribute((const void *)sort_dedup,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, sm));
+    return PANO_OK;
+}

@@ -1,0 +1,37 @@
+"""Drop-in for /root/reference/image_stitching_sift.py (per-pair loop + warp/blend on GPU).
+
+Same function names and signatures; ``run_panorama`` takes its three interactive answers
+as arguments.  compute_shift_sift (image_stitching_sift.py:52-83) extracts both frames'
+features in one batched pano_sift launch, matches with the fp32 MFMA distance GEMM and
+votes the translation on the GPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .sift_impl import compute_keypoints_and_descriptors  # noqa: F401  (reference import)
+from .stitching import (blend_two_images, cylindrical_projection, pad_image,  # noqa: F401
+                        ransac, read_pano_data, rectangle_crop)
+from .stitching import run_panorama as _run
+
+
+def compute_shift_sift(imgA, imgB, ransac_thr=3, desc_thresh=25000):
+    from .sift_impl import _as_bgr_u8, _stitcher
+    a, b = _as_bgr_u8(imgA), _as_bgr_u8(imgB)
+    if a.shape != b.shape:
+        raise ValueError("compute_shift_sift: frames must have the same shape (run_panorama pads)")
+    st = _stitcher(1.6, 3, 0.5, 5)
+    st.ransac_thr = float(ransac_thr)
+    st.desc_thresh = float(desc_thresh)
+    feats = st.features(st.upload(np.stack([a, b])))
+    recs, _ = st.pair_records(feats, [(0, 1)])
+    r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
+    if r["status"] != _lib.PANO_OK:
+        return (0, 0), None
+    return (float(r["dx"]), float(r["dy"])), ((float(r["xA"]), float(r["yA"])),
+                                              (float(r["xB"]), float(r["yB"])))
+
+
+def run_panorama(folder_path=".", pano_file=None, margin=15, **kw):
+    return _run(folder_path, pano_file, margin, method="sift", **kw)

@@ -1,0 +1,201 @@
+"""Batched MI355X stitching pipeline: the numeric body of run_panorama on the GPU.
+
+Reference flow (image_stitching_sift.py:290-384, image_stitching_harris.py:460-542):
+cylindrical projection of every frame -> per adjacent pair: features of both frames, NN
+match, translation RANSAC -> vertical drift correction -> sequential pad + blend fold ->
+rectangle crop.
+
+Here every stage runs as libpano kernels over the whole frame batch, on one HIP stream:
+
+    pano_cylindrical   all frames, one launch pair
+    pano_sift/harris   all frames once (the reference recomputes interior frames for both
+                       of their pairs; features are a pure function of the frame)
+    pano_match         all pairs (fp32 MFMA distance GEMM for SIFT)
+    pano_pair_shifts   all pairs (match filter + exhaustive vote RANSAC)
+      -- host: 17 records come back (~1 KB); drift correction + composite plan (C) --
+    pano_composite     pre-sized canvas, one launch per step over the new frame's columns
+    pano_gray_bbox     crop box (16 bytes come back)
+
+Two small device->host reads are the only synchronisation points.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import PanoError, context, ptr
+
+
+@dataclass
+class StitchResult:
+    panorama: "object"                 # torch uint8 [H', W', 3] on device (a view of canvas)
+    canvas: "object"                   # full mosaic before the crop, torch uint8 on device
+    shifts: list                       # raw per-pair (dx, dy), reference order
+    pairs: list                        # per-pair best match ((xA, yA), (xB, yB)) or None
+    records: np.ndarray                # PAIR_NP records
+    bbox: tuple                        # (y0, y1, x0, x1) crop rows/cols, inclusive
+    timings: dict = field(default_factory=dict)
+
+
+def drift_correct(shifts):
+    """run_panorama :336-365 -- spread the accumulated dy evenly over the pairs."""
+    total = 0
+    for _, dy in shifts:
+        total = total + dy
+    n = len(shifts) + 1
+    avg = total / (n - 1) if n > 1 else 0
+    return [(dx, dy - avg) for dx, dy in shifts]
+
+
+class Stitcher:
+    """Reusable device state for stitching sequences of equally sized frames."""
+
+    def __init__(self, method: str = "sift", device: int | None = None, cap: int = 4096,
+                 max_points: int = 200, ransac_thr: float = 3.0, desc_thresh: float | None = None,
+                 sift_params: dict | None = None):
+        import torch
+        self.torch = torch
+        self.method = method
+        self.ctx = context(device)
+        self.device = torch.device("cuda", self.ctx.device)
+        self.cap = cap if method == "sift" else max_points
+        self.max_points = max_points
+        self.ransac_thr = float(ransac_thr)
+        self.desc_thresh = float(desc_thresh if desc_thresh is not None
+                                 else (25000 if method == "sift" else 1.0))
+        self.params = _lib.default_sift_params(**(sift_params or {}))
+        self._buf = {}
+
+    # ------------------------------------------------------------------ buffers
+    def _get(self, name, shape, dtype):
+        t = self._buf.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = self.torch.empty(shape, dtype=dtype, device=self.device)
+            self._buf[name] = t
+        return t
+
+    def upload(self, frames) -> "object":
+        """uint8 [n, h, w, 3] host array (or list of frames) -> device tensor."""
+        if isinstance(frames, (list, tuple)):
+            frames = np.stack(frames)
+        frames = np.ascontiguousarray(frames, np.uint8)
+        return self.torch.from_numpy(frames).to(self.device, non_blocking=False)
+
+    # ------------------------------------------------------------------ stages
+    def cylindrical(self, frames_dev, focals):
+        n, h, w, _ = frames_dev.shape
+        out = self._get("cyl", (n, h, w, 3), self.torch.uint8)
+        colnz = self._get("colnz", (n, w), self.torch.uint8)
+        f = np.ascontiguousarray(focals, np.float64)
+        self.ctx.check(self.ctx.lib.pano_cylindrical(self.ctx.h, ptr(frames_dev), ptr(out), n, h, w,
+                                                     _lib.f64p(f), ptr(colnz)))
+        return out, colnz
+
+    def features(self, frames_dev):
+        n, h, w, _ = frames_dev.shape
+        T = self.torch
+        if self.method == "sift":
+            kps = self._get("kps", (n, self.cap, 6), T.int32)
+            desc = self._get("desc", (n, self.cap, 128), T.float32)
+            counts = self._get("counts", (n,), T.int32)
+            self.ctx.check(self.ctx.lib.pano_sift(self.ctx.h, ptr(frames_dev), n, h, w,
+                                                  ctypes.byref(self.params), ptr(kps), ptr(desc),
+                                                  self.cap, ptr(counts)))
+            return kps, desc, counts
+        xy = self._get("xy", (n, self.max_points, 2), T.int32)
+        desc = self._get("desc", (n, self.max_points, 128), T.float32)
+        counts = self._get("counts", (n,), T.int32)
+        self.ctx.check(self.ctx.lib.pano_harris(self.ctx.h, ptr(frames_dev), n, h, w,
+                                                self.max_points, ptr(xy), ptr(desc), ptr(counts)))
+        return xy, desc, counts
+
+    def pair_records(self, feats, pairs):
+        T = self.torch
+        pts, desc, counts = feats
+        P = len(pairs)
+        cap = desc.shape[1]
+        hp = np.ascontiguousarray(np.array(pairs, np.int32).reshape(-1))
+        best = self._get("best", (P, cap), T.int32)
+        d1 = self._get("d1", (P, cap), T.float32)
+        d2 = self._get("d2", (P, cap), T.float32)
+        exact = 1 if self.method == "sift" else 0
+        self.ctx.check(self.ctx.lib.pano_match(self.ctx.h, ptr(desc), ptr(counts), cap,
+                                               _lib.i32p(hp), P, exact, ptr(best), ptr(d1), ptr(d2)))
+        recs = self._get("recs", (P, 64), T.uint8)
+        kps_p = ptr(pts) if self.method == "sift" else None
+        xy_p = None if self.method == "sift" else ptr(pts)
+        self.ctx.check(self.ctx.lib.pano_pair_shifts(self.ctx.h, kps_p, xy_p, ptr(counts), cap,
+                                                     _lib.i32p(hp), P, ptr(best), ptr(d1), ptr(d2),
+                                                     self.desc_thresh, 0.0, self.ransac_thr,
+                                                     ptr(recs)))
+        return recs, (best, d1, d2)
+
+    def composite(self, cyl, colnz, shifts_corr, pairs_xy):
+        n, h, w, _ = cyl.shape
+        sh = np.ascontiguousarray(np.array(shifts_corr, np.float64).reshape(-1, 2))
+        pr = np.ascontiguousarray(np.array(pairs_xy, np.float64).reshape(-1, 4))
+        steps = (_lib.Step * max(n - 1, 1))()
+        first = np.zeros(2, np.int32)
+        hw = np.zeros(2, np.int32)
+        rc = self.ctx.lib.pano_plan_composite(_lib.f64p(sh), _lib.f64p(pr), n, h, w, steps,
+                                              _lib.i32p(first), _lib.i32p(hw))
+        if rc:
+            raise PanoError(rc, "pano_plan_composite")
+        H, W = int(hw[0]), int(hw[1])
+        canvas = self._get("canvas", (H, W, 3), self.torch.uint8)
+        self.ctx.check(self.ctx.lib.pano_composite(self.ctx.h, ptr(cyl), ptr(colnz), n, h, w, steps,
+                                                   _lib.i32p(first), ptr(canvas), H, W))
+        return canvas
+
+    def bbox(self, img, thr=0):
+        H, W, _ = img.shape
+        bb = self._get("bbox", (4,), self.torch.int32)
+        self.ctx.check(self.ctx.lib.pano_gray_bbox(self.ctx.h, ptr(img), H, W, thr, ptr(bb)))
+        return bb
+
+    # ------------------------------------------------------------------ whole run
+    def run(self, frames_dev, focals, margin: int = 15, timers: bool = False) -> StitchResult:
+        T = self.torch
+        t = {}
+        tick = time.perf_counter
+        t0 = tick()
+        n = frames_dev.shape[0]
+        cyl, colnz = self.cylindrical(frames_dev, focals)
+        feats = self.features(cyl)
+        pairs = [(i, i + 1) for i in range(n - 1)]
+        if not pairs:
+            raise PanoError(_lib.PANO_E_ARG, "need at least two frames")
+        recs_dev, _ = self.pair_records(feats, pairs)
+        recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)   # sync point 1
+        t["features_match_ransac"] = tick() - t0
+        self.ctx.sync()
+        shifts, best_pairs = [], []
+        for r in recs:
+            if r["status"] != _lib.PANO_OK:
+                # the reference's blend would fail on a None pair (image_stitching_sift.py:164)
+                raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+            if self.method == "sift":
+                shifts.append((float(r["dx"]), float(r["dy"])))
+                best_pairs.append(((float(r["xA"]), float(r["yA"])), (float(r["xB"]), float(r["yB"]))))
+            else:
+                shifts.append((int(r["dx"]), int(r["dy"])))
+                best_pairs.append(((int(r["xA"]), int(r["yA"])), (int(r["xB"]), int(r["yB"]))))
+        corr = drift_correct(shifts)
+        pxy = [(a[0], a[1], b[0], b[1]) for a, b in best_pairs]
+        canvas = self.composite(cyl, colnz, corr, pxy)
+        bb = self.bbox(canvas).cpu().numpy()                             # sync point 2
+        H = canvas.shape[0]
+        if bb[1] < 0:
+            y0, y1, x0, x1 = 0, H - 1, 0, canvas.shape[1] - 1
+            pano = canvas
+        else:
+            y0 = max(0, int(bb[0]) + margin)
+            y1 = min(H - 1, int(bb[1]) - margin)
+            x0, x1 = int(bb[2]), int(bb[3])
+            pano = canvas if (y0 > y1 or x0 > x1) else canvas[y0:y1 + 1, x0:x1 + 1]
+        t["total"] = tick() - t0
+        return StitchResult(pano, canvas, shifts, best_pairs, recs, (y0, y1, x0, x1), t)
