@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""GPU diagnostic: stage-by-stage comparison of libpano against the oracle / golden data.
+
+Development tool (not a test): prints one line per check, never stops at the first
+mismatch, so one GPU call shows the state of every kernel.  Usage on the GPU box:
+    python tools/diag_gpu.py [--full]
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from oracle import harris as oharris  # noqa: E402
+from oracle import sift as osift  # noqa: E402
+from oracle import stitch as ostitch  # noqa: E402
+from vfx_image_stitching_amd import _lib, data  # noqa: E402
+from vfx_image_stitching_amd.pipeline import Stitcher  # noqa: E402
+
+G = os.path.join(ROOT, "tests", "golden")
+
+
+def check(name, fn):
+    t0 = time.time()
+    try:
+        msg = fn()
+        print(f"[ok ] {name}: {msg}  ({time.time() - t0:.1f}s)", flush=True)
+    except Exception as e:  # noqa: BLE001
+        print(f"[BAD] {name}: {e!r}", flush=True)
+        traceback.print_exc(limit=3)
+
+
+def main(full):
+    frames, focals = data.pair_frame("parrington", "prtn00.jpg", "prtn01.jpg")
+    st = Stitcher("sift")
+    dev = st.upload(frames)
+    state = {}
+
+    def c_cyl():
+        cyl, colnz = st.cylindrical(dev, focals)
+        h = cyl.cpu().numpy()
+        state["cyl"] = h
+        state["cyl_dev"] = cyl
+        bad = []
+        for i in range(2):
+            ref = ostitch.cylindrical(frames[i], focals[i])
+            if not np.array_equal(h[i], ref):
+                bad.append((i, int((h[i] != ref).any(-1).sum())))
+            cz = colnz.cpu().numpy()[i].astype(bool)
+            if not np.array_equal(cz, (ref != 0).any(axis=(0, 2))):
+                bad.append(("colnz", i))
+        return "exact" if not bad else f"MISMATCH {bad}"
+    check("C1 cylindrical", c_cyl)
+
+    def c_pyr():
+        cyl = state["cyl"]
+        kps, desc, counts = st.features(state["cyl_dev"])
+        state["feats"] = (kps, desc, counts)
+        torch.cuda.synchronize()
+        _, _, stg = osift.detect_and_describe(cyl[0], return_stages=True)
+        state["ostages"] = stg
+        from vfx_image_stitching_amd.sift_impl import _DevicePyramid  # noqa: F401
+        import ctypes
+        ctx = st.ctx
+        lines = []
+        for o in range(9):
+            h, w, no = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+            ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(h), ctypes.byref(w), ctypes.byref(no)))
+            for l in range(6):
+                out = torch.empty((h.value, w.value), dtype=torch.float32, device=st.device)
+                ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, 0, o, l, 0, _lib.ptr(out)))
+                g = out.cpu().numpy()
+                r = stg["gauss"][o][l]
+                if g.shape != r.shape or not np.array_equal(g, r):
+                    d = np.abs(g - r) if g.shape == r.shape else None
+                    lines.append(f"G{o}.{l}: {int((g != r).sum()) if d is not None else 'shape'} diff, max {d.max() if d is not None else '-'}")
+            for l in range(5):
+                out = torch.empty((h.value, w.value), dtype=torch.float32, device=st.device)
+                ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, 0, o, l, 1, _lib.ptr(out)))
+                g = out.cpu().numpy()
+                r = stg["dog"][o][l]
+                if not np.array_equal(g, r):
+                    lines.append(f"D{o}.{l}: {int((g != r).sum())} diff")
+        return "all levels exact" if not lines else "; ".join(lines[:12])
+    check("S1-S4 pyramid (frame 0 vs oracle)", c_pyr)
+
+    def c_kp():
+        kps, desc, counts = state["feats"]
+        gz = np.load(os.path.join(G, "sift_pair.npz"))
+        n = counts.cpu().numpy()
+        out = [f"counts {n.tolist()} golden {[len(gz['prtn00_kp_x']), len(gz['prtn01_kp_x'])]}"]
+        for i, stem in enumerate(["prtn00", "prtn01"]):
+            rec = kps[i, :n[i]].cpu().numpy().view(_lib.KP_NP).reshape(-1)
+            gx = gz[f"{stem}_kp_x"]
+            if len(rec) != len(gx):
+                out.append(f"{stem}: count differs")
+                m = min(len(rec), len(gx))
+            else:
+                m = len(gx)
+            for k in ("x", "y", "size", "angle", "response", "octave"):
+                a = rec[k][:m]
+                b = gz[f"{stem}_kp_{k}"][:m].astype(a.dtype)
+                ne = int((a != b).sum())
+                if ne:
+                    out.append(f"{stem}.{k}: {ne} differ (max {np.abs(a.astype(np.float64) - b).max():.3g})")
+            d = desc[i, :m].cpu().numpy()
+            gd = gz[f"{stem}_desc"][:m].astype(np.float32)
+            dd = np.abs(d - gd)
+            out.append(f"{stem}.desc: {int((dd > 0).sum())}/{dd.size} elems differ, max {dd.max():.0f}, "
+                       f"{int((dd.max(1) > 0).sum())} rows")
+        return "; ".join(out)
+    check("S5-S9 keypoints + descriptors vs golden", c_kp)
+
+    def c_pair():
+        kps, desc, counts = state["feats"]
+        recs, (best, d1, d2) = st.pair_records((kps, desc, counts), [(0, 1)])
+        r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
+        gold = json.load(open(os.path.join(G, "sift_pair.json")))["shift_prtn00_prtn01"]
+        gz = np.load(os.path.join(G, "sift_pair.npz"))
+        b = best.cpu().numpy()[0][:counts.cpu().numpy()[0]]
+        # match exactness on the GPU's own descriptors vs the numpy NN on them
+        n0, n1 = counts.cpu().numpy()[:2]
+        dA = desc[0, :n0].cpu().numpy()
+        dB = desc[1, :n1].cpu().numpy()
+        j, dist = ostitch.nn_match_sift(dA, dB)
+        same = np.array_equal(j, b)
+        dd = np.array_equal(d1.cpu().numpy()[0][:n0], dist.astype(np.float32))
+        return (f"shift ({float(r["dx"]):.4f},{float(r["dy"]):.4f}) golden {gold['move']}; matches {r['n_matches']} votes {r['votes']}; "
+                f"NN idx == numpy on GPU desc: {same}, dist exact: {dd}; golden idx agree {np.mean(b == gz['match_prtn00_prtn01_idx'][:len(b)]) if len(b) == len(gz['match_prtn00_prtn01_idx']) else 'n/a'}")
+    check("M1+R1 pair prtn00/prtn01", c_pair)
+
+    def c_harris_feat():
+        names, fr, fo, margin = data.load_set("parrington")
+        sh = Stitcher("harris")
+        cyl, _ = sh.cylindrical(sh.upload(fr), fo)
+        xy, desc, counts = sh.features(cyl)
+        hz = np.load(os.path.join(G, "harris_parrington_features.npz"))
+        n = counts.cpu().numpy()
+        bad = []
+        maxd = 0.0
+        for i in range(len(fr)):
+            k = xy[i, :n[i]].cpu().numpy()
+            gk = hz[f"kps_{i}"]
+            if k.shape != gk.shape or not np.array_equal(k, gk):
+                bad.append(i)
+                continue
+            d = desc[i, :n[i]].cpu().numpy()
+            maxd = max(maxd, float(np.abs(d - hz[f"desc_{i}"]).max()) if len(d) else 0.0)
+            if not np.array_equal(d, hz[f"desc_{i}"]):
+                bad.append(("desc", i, float(np.abs(d - hz[f"desc_{i}"]).max())))
+        return f"frames with corner/desc mismatch: {bad[:8]} (max desc diff {maxd:.3g})"
+    check("H1-H3 Harris corners + descriptors (18 frames)", c_harris_feat)
+
+    def run_set(method, s):
+        names, fr, fo, margin = data.load_set(s)
+        stt = Stitcher(method)
+        d = stt.upload(fr)
+        res = stt.run(d, fo, margin=margin)
+        torch.cuda.synchronize()
+        gold = json.load(open(os.path.join(G, f"{method}_{s}.json")))
+        gs = [tuple(x["move"]) for x in gold["shifts"]]
+        diffs = [(i, a, b) for i, (a, b) in enumerate(zip(res.shifts, gs)) if abs(a[0] - b[0]) > 1e-9 or abs(a[1] - b[1]) > 1e-9]
+        pano = res.panorama.cpu().numpy()
+        import hashlib
+        h = hashlib.sha256()
+        h.update(f"{pano.dtype.str}{pano.shape}".encode())
+        h.update(pano.tobytes())
+        exact = h.hexdigest() == gold["pano_digest"]
+        times = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            stt.run(d, fo, margin=margin)
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) * 1e3)
+        return (f"shape {pano.shape} golden {gold['pano_shape']}; pano bit-exact {exact}; "
+                f"{len(diffs)} pair shifts differ {diffs[:3]}; run ms {['%.2f' % t for t in times]}")
+    check("end-to-end Harris parrington", lambda: run_set("harris", "parrington"))
+    check("end-to-end SIFT parrington", lambda: run_set("sift", "parrington"))
+    if full:
+        check("end-to-end SIFT grail", lambda: run_set("sift", "grail"))
+        check("end-to-end Harris grail", lambda: run_set("harris", "grail"))
+
+
+if __name__ == "__main__":
+    main("--full" in sys.argv)
