@@ -134,7 +134,7 @@ def main(full):
         j, dist = ostitch.nn_match_sift(dA, dB)
         same = np.array_equal(j, b)
         dd = np.array_equal(d1.cpu().numpy()[0][:n0], dist.astype(np.float32))
-        return (f"shift ({float(r["dx"]):.4f},{float(r["dy"]):.4f}) golden {gold['move']}; matches {r['n_matches']} votes {r['votes']}; "
+        return (f"shift ({float(r['dx']):.4f},{float(r['dy']):.4f}) golden {gold['move']}; matches {r['n_matches']} votes {r['votes']}; "
                 f"NN idx == numpy on GPU desc: {same}, dist exact: {dd}; golden idx agree {np.mean(b == gz['match_prtn00_prtn01_idx'][:len(b)]) if len(b) == len(gz['match_prtn00_prtn01_idx']) else 'n/a'}")
     check("M1+R1 pair prtn00/prtn01", c_pair)
 
