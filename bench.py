@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpixels/s stitched, 18-image parrington, SIFT path, MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload parrington|grail|synthetic]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+A step = one whole stitch of one rank's sequence, inputs resident in HBM:
+cylindrical projection -> SIFT features of every frame -> NN match (fp32 MFMA) -> RANSAC
+-> [N>1: all_gather of per-pair records] -> drift correction + composite plan -> composite
+(band) -> crop bounding box [N>1: 4-int all_reduce].  Rank r stitches the parrington loop
+starting at frame 17 r (18 frames, 17 pairs): per-GPU work is fixed ("weak" scaling) and the
+job is one panorama of N laps, N*17 + 1 distinct frames.
+
+value  = distinct input Mpx of the job / max-over-ranks seconds per step.
+roofline: the dominant kernel, timed live with HIP events on the library's stream over the
+timed region (libpano pano_prof_*), against its algorithmic bytes (DESIGN.md "Roofline").
+cpu_baseline: the oracle (numpy restatement, bit-exact vs the reference) on rank 0 at N=1
+over a bounded sample (first 4 frames = 3 pairs of the same workload), 1 thread.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec (the blur's arithmetic)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="parrington", choices=["parrington", "grail", "synthetic"])
+    ap.add_argument("--method", default="sift", choices=["sift", "harris"])
+    ap.add_argument("--roofline-kernel", default="auto")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=4)
+    return ap.parse_args()
+
+
+def workload(name, rank, world):
+    from vfx_image_stitching_amd import data
+    if name == "synthetic":
+        frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920)
+        per = 143 // world
+        s = rank * per
+        return frames[s:s + per + 1], focals[s:s + per + 1], 15, (1080, 1920), 143
+    names, frames, focals, margin = data.load_set(name)
+    n = len(frames)
+    fr, fo = data.cyclic_sequence(frames, focals, start=(n - 1) * rank, count=n)
+    return fr, fo, margin, frames.shape[1:3], world * (n - 1) + 1
+
+
+def kernel_bytes(name, st, n_frames, h, w):
+    """Algorithmic HBM bytes of all launches of one kernel class in one step."""
+    ctx = st.ctx
+    import ctypes
+    if name == "blur_level":
+        tot = 0
+        no = ctypes.c_int32()
+        hh, ww = ctypes.c_int32(), ctypes.c_int32()
+        ctx.lib.pano_sift_level_shape(ctx.h, 0, ctypes.byref(hh), ctypes.byref(ww), ctypes.byref(no))
+        for o in range(no.value):
+            ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(hh), ctypes.byref(ww), None)
+            px = n_frames * hh.value * ww.value
+            # 5 cascaded levels: read input 4 B, write level 4 B + DoG 4 B
+            tot += 5 * 12 * px
+            if o > 0:
+                tot += 4 * px                      # level-1 launch also stores the octave base
+        # base launch: 3 B/pixel of BGR in, 4 B per base pixel out
+        tot += n_frames * h * w * 3 + 4 * n_frames * 4 * h * w
+        return tot, "GB/s"
+    if name == "composite_step":
+        return 9 * n_frames * h * w, "GB/s"
+    if name in ("cyl_scatter", "cyl_gather"):
+        return 6 * n_frames * h * w, "GB/s"
+    if name == "extrema_localize":
+        tot = 0
+        no = ctypes.c_int32()
+        hh, ww = ctypes.c_int32(), ctypes.c_int32()
+        ctx.lib.pano_sift_level_shape(ctx.h, 0, ctypes.byref(hh), ctypes.byref(ww), ctypes.byref(no))
+        for o in range(no.value):
+            ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(hh), ctypes.byref(ww), None)
+            tot += 20 * n_frames * hh.value * ww.value
+        return tot, "GB/s"
+    return None, None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from vfx_image_stitching_amd import distributed as D
+    from vfx_image_stitching_amd.pipeline import Stitcher
+
+    frames, focals, margin, (h, w), distinct = workload(args.workload, rank, world)
+    n_local = len(frames)
+    cap = 4096 if args.workload != "synthetic" else 8192
+    st = Stitcher(args.method, cap=cap)
+    dev = st.upload(frames)                                   # resident in HBM
+    counts = [c for _, c in D.shard_ranges(distinct - 1, world)] if args.workload == "synthetic" \
+        else [n_local - 1] * world
+    pair_start = sum(counts[:rank])
+
+    def step():
+        if world > 1:
+            return D.run_rank(st, dev, focals, pair_start, counts, margin=margin)
+        return st.run(dev, focals, margin=margin)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # pick the dominant kernel from one profiled (untimed) step
+    ctx = st.ctx
+    rk = args.roofline_kernel
+    per_kernel = {}
+    if rk == "auto":
+        # per-class breakdown: one profiled (untimed) step per kernel class
+        from vfx_image_stitching_amd._lib import KERNELS
+        for k in KERNELS:
+            ctx.prof_enable(k)
+            step()
+            r = ctx.prof_read(k)
+            if r["launches"]:
+                per_kernel[k] = r
+        ctx.prof_enable(-1)
+        rk = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
+
+    # timed region: the dominant kernel's launches are bracketed by HIP events
+    ctx.prof_enable(rk)
+    ctx.prof_read(rk)                                          # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kr = ctx.prof_read(rk)
+    ctx.prof_enable(-1)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    ms_step = el / args.steps * 1e3
+    mpx = distinct * h * w / 1e6
+    value = mpx / (el / args.steps)
+
+    roof = None
+    byts, unit = kernel_bytes(rk, st, n_local, h, w)
+    if kr["launches"]:
+        per_step_ms = kr["total_ms"] / args.steps
+        per_launch_ms = kr["total_ms"] / kr["launches"]
+        launches_per_step = kr["launches"] / args.steps
+        if byts is not None:
+            per_launch_bytes = byts / launches_per_step
+            ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": rk, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "avg_launch_ms": round(per_launch_ms, 5), "launches_per_step": launches_per_step,
+                    "kernel_ms_per_step": round(per_step_ms, 4)}
+        else:
+            roof = {"bound": "latency", "kernel": rk, "achieved": None, "peak": None, "unit": None,
+                    "frac": None, "traffic": None, "avg_launch_ms": round(per_launch_ms, 5),
+                    "launches_per_step": launches_per_step,
+                    "kernel_ms_per_step": round(per_step_ms, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "synthetic":
+        cpu = cpu_baseline(frames, focals, args.cpu_frames, args.method, h, w)
+
+    line = {
+        "metric": "Mpixels/s stitched (18-img parrington, SIFT path)" if args.workload == "parrington"
+        else f"Mpixels/s stitched ({args.workload}, {args.method})",
+        "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "reference parrington JPEGs (packed under data/), decoded, resident in HBM"
+        if args.workload != "synthetic" else "synthetic 1080p sequence (SURVEY 8d config 5)",
+        "config": {"workload": f"{args.workload} {args.method} end-to-end: {distinct} frames "
+                               f"{h}x{w}, {distinct - 1} pairs, {world} rank(s) x {n_local} frames",
+                   "frames": distinct, "frame_hw": [h, w], "parallelism": f"pairs sharded x{world}",
+                   "method": args.method},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "kernels_ms_per_step": {k: round(v["total_ms"], 4) for k, v in per_kernel.items()},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(frames, focals, n, method, h, w):
+    """Oracle (bit-exact numpy restatement) on the first n frames, single thread."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:                                         # pragma: no cover
+        threadpool_limits = None
+    from oracle import stitch as ostitch
+    ctxm = threadpool_limits(1) if threadpool_limits else None
+    try:
+        t0 = time.perf_counter()
+        ostitch.stitch(list(frames[:n]), list(focals[:n]), method=method, margin=15)
+        el = time.perf_counter() - t0
+    finally:
+        if ctxm is not None:
+            ctxm.unregister() if hasattr(ctxm, "unregister") else None
+    mpx = n * h * w / 1e6
+    return {"value": round(mpx / el, 5), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "sample": f"oracle end-to-end stitch of the first {n} frames ({n - 1} pairs), {el:.1f} s",
+            "reference_container_value": 0.00448,
+            "reference_container_note": "reference sift_impl path re-measured in the build "
+                                        "container: 789.35 s for 18 frames (BASELINE.md)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -188,6 +188,36 @@ int pano_blend_two(pano_ctx *ctx, const uint8_t *d_A, int hA, int wA, const uint
 int pano_gray_bbox(pano_ctx *ctx, const uint8_t *d_img, int H, int W, int black_threshold,
                    int32_t *d_bbox);
 
+/* ---------------------------------------------------------------- live kernel timing
+ * pano_prof_enable(ctx, k) records a hipEvent pair on the context's stream around every
+ * launch of kernel class k (PANO_K_*; PANO_K_ALL = every class; -1 = off).
+ * pano_prof_read synchronises the stream and returns launches and elapsed milliseconds of
+ * class k since the last read (PANO_K_ALL: all recorded launches), then resets. */
+#define PANO_K_CYL_SCATTER 0
+#define PANO_K_CYL_GATHER 1
+#define PANO_K_BLUR 2
+#define PANO_K_EXTREMA 3
+#define PANO_K_ORIENT 4
+#define PANO_K_SORT 5
+#define PANO_K_DESC 6
+#define PANO_K_NORMS 7
+#define PANO_K_DIST_MFMA 8
+#define PANO_K_DIST_DIRECT 9
+#define PANO_K_REDUCE 10
+#define PANO_K_PAIR_SHIFTS 11
+#define PANO_K_COMPOSITE 12
+#define PANO_K_BBOX 13
+#define PANO_K_H_GRAY 14
+#define PANO_K_H_BLUR 15
+#define PANO_K_H_RESP 16
+#define PANO_K_H_NMS 17
+#define PANO_K_H_SELECT 18
+#define PANO_K_H_DESC 19
+#define PANO_K_ALL 20
+int pano_prof_enable(pano_ctx *ctx, int kernel_class);
+int pano_prof_read(pano_ctx *ctx, int kernel_class, int *launches, double *total_ms,
+                   double *min_ms, double *max_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,334 @@
+"""GPU parity: libpano kernels (through the C-ABI) vs the oracle and the golden vectors.
+
+Bars (DESIGN.md "Parity"):
+  C1 cylindrical, S1-S4 pyramid, S5 extrema/positions, M1 match, R1 ransac, B1 blend and
+  the Harris path H1-H4  -> bit-exact;
+  S6-S9 (size/angle via numpy's libm powf / SIMD atan2f, expf) -> ulp-level, integer
+  descriptors within 1 LSB;  final panoramas -> bit-exact on parrington and grail.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import digest
+from oracle import harris as oharris
+from oracle import sift as osift
+from oracle import stitch as ostitch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def st_sift(gpu):
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    return Stitcher("sift")
+
+
+@pytest.fixture(scope="module")
+def parr_dev(st_sift, parrington):
+    names, frames, focals, margin = parrington
+    dev = st_sift.upload(frames)
+    cyl, colnz = st_sift.cylindrical(dev, focals)
+    return dev, cyl.clone(), colnz.clone()
+
+
+# ------------------------------------------------------------------ C1
+@pytest.mark.parametrize("setname", ["parrington", "grail", "out"])
+def test_cylindrical_bit_exact(gpu, setname, gold_json):
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, _ = data.load_set(setname)
+    st = Stitcher("sift")
+    cyl, colnz = st.cylindrical(st.upload(frames), focals)
+    h = cyl.cpu().numpy()
+    cz = colnz.cpu().numpy()
+    rows = gold_json("cylindrical.json")[setname]
+    for i, r in enumerate(rows):
+        assert digest(h[i]) == r["out"], f"frame {i}"
+        assert np.array_equal(cz[i].astype(bool), (h[i] != 0).any(axis=(0, 2)))
+
+
+# ------------------------------------------------------------------ S1..S4
+def test_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl):
+    dev, cyl, _ = parr_dev
+    st_sift.features(cyl[:1].contiguous())
+    _, _, stg = osift.detect_and_describe(parrington_cyl[0], return_stages=True)
+    ctx = st_sift.ctx
+    import torch
+    for o in range(len(stg["gauss"])):
+        h, w, no = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(h), ctypes.byref(w),
+                                                ctypes.byref(no)))
+        assert no.value == len(stg["gauss"])
+        for dog, levels in ((0, stg["gauss"][o]), (1, stg["dog"][o])):
+            for l, ref in enumerate(levels):
+                out = torch.empty((h.value, w.value), dtype=torch.float32, device=st_sift.device)
+                from vfx_image_stitching_amd import _lib
+                ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, 0, o, l, dog, _lib.ptr(out)))
+                assert np.array_equal(out.cpu().numpy(), ref), (o, l, dog)
+
+
+# ------------------------------------------------------------------ S5..S9
+def _gpu_feats(st, cyl):
+    from vfx_image_stitching_amd import _lib
+    kps, desc, counts = st.features(cyl)
+    n = counts.cpu().numpy()
+    out = []
+    for i in range(len(n)):
+        rec = kps[i, :n[i]].cpu().numpy().view(_lib.KP_NP).reshape(-1)
+        out.append((rec, desc[i, :n[i]].cpu().numpy()))
+    return out
+
+
+def _compare_features(rec, desc, gold_rec, gold_desc):
+    assert len(rec) == len(gold_rec["x"]), "keypoint count"
+    for k in ("x", "y", "response", "octave"):
+        np.testing.assert_array_equal(rec[k], gold_rec[k].astype(rec[k].dtype), err_msg=k)
+    # size: 2 ** f32 is glibc powf in the reference (not always correctly rounded)
+    np.testing.assert_allclose(rec["size"], gold_rec["size"], rtol=3e-7, atol=0)
+    # angles: numpy's AVX-512 atan2f / expf are 1-3 ulp from correctly rounded
+    np.testing.assert_allclose(rec["angle"], gold_rec["angle"], rtol=0, atol=2e-3)
+    d = np.abs(desc - gold_desc.astype(np.float32))
+    assert d.max() <= 1, "descriptor element off by more than 1 LSB"
+    assert (d > 0).mean() < 1e-3, "more than 0.1 % of descriptor elements differ"
+
+
+def test_sift_keypoints_descriptors_every_parrington_frame(st_sift, parr_dev, gold_npz):
+    _, cyl, _ = parr_dev
+    feats = _gpu_feats(st_sift, cyl)
+    z = gold_npz("sift_parrington_features.npz")
+    for i, (rec, desc) in enumerate(feats):
+        g = {k: z[f"f{i}_{k}"] for k in ("x", "y", "size", "angle", "response", "octave")}
+        _compare_features(rec, desc, g, z[f"f{i}_desc"])
+
+
+def test_sift_grail_frames(gpu, grail, gold_npz):
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, _ = grail
+    st = Stitcher("sift")
+    cyl, _ = st.cylindrical(st.upload(frames), focals)
+    feats = _gpu_feats(st, cyl)
+    z = gold_npz("sift_grail_features.npz")
+    for i, (rec, desc) in enumerate(feats):
+        g = {k: z[f"f{i}_{k}"] for k in ("x", "y", "size", "angle", "response", "octave")}
+        _compare_features(rec, desc, g, z[f"f{i}_desc"])
+
+
+def test_sift_odd_size_frames_vs_oracle(gpu, outset):
+    """out/ frames are 571 x 428: odd octave sizes exercise INTER_NEAREST flooring."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, _ = outset
+    st = Stitcher("sift")
+    cyl, _ = st.cylindrical(st.upload(frames[:1]), focals[:1])
+    (rec, desc), = _gpu_feats(st, cyl)
+    kps, odesc = osift.detect_and_describe(cyl.cpu().numpy()[0])
+    g = {k: kps[k] for k in ("x", "y", "size", "angle", "response", "octave")}
+    _compare_features(rec, desc, g, odesc)
+
+
+def test_sift_blank_and_tiny_inputs(gpu):
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    st = Stitcher("sift")
+    blank = np.zeros((2, 64, 48, 3), np.uint8)
+    kps, desc, counts = st.features(st.upload(blank))
+    assert counts.cpu().numpy().tolist() == [0, 0]
+    recs, _ = st.pair_records((kps, desc, counts), [(0, 1)])
+    from vfx_image_stitching_amd import _lib
+    r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
+    assert r["status"] == _lib.PANO_E_NOMATCH and r["n_matches"] == 0
+
+
+# ------------------------------------------------------------------ M1 + R1
+def test_match_exact_on_golden_descriptors(gpu, gold_npz):
+    """Feed the reference's own descriptors: NN indices and distances are exact."""
+    import torch
+    from vfx_image_stitching_amd import _lib
+    g = gold_npz("sift_pair.npz")
+    dA = g["prtn00_desc"].astype(np.float32)
+    dB = g["prtn01_desc"].astype(np.float32)
+    cap = 2048
+    d = np.zeros((2, cap, 128), np.float32)
+    d[0, :len(dA)] = dA
+    d[1, :len(dB)] = dB
+    ctx = gpu
+    desc = torch.from_numpy(d).cuda()
+    counts = torch.tensor([len(dA), len(dB)], dtype=torch.int32).cuda()
+    best = torch.empty((1, cap), dtype=torch.int32).cuda()
+    d1 = torch.empty((1, cap)).cuda()
+    d2 = torch.empty((1, cap)).cuda()
+    hp = np.array([0, 1], np.int32)
+    ctx.check(ctx.lib.pano_match(ctx.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), 1, 1,
+                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2)))
+    b = best.cpu().numpy()[0][:len(dA)]
+    np.testing.assert_array_equal(b, g["match_prtn00_prtn01_idx"])
+    np.testing.assert_array_equal(d1.cpu().numpy()[0][:len(dA)], g["match_prtn00_prtn01_dist"].astype(np.float32))
+    # second-best distance (Lowe ratio input) equals the numpy second minimum
+    full = ((dA.astype(np.float64)[:, None, :] - dB[None]) ** 2).sum(-1)
+    np.testing.assert_array_equal(d2.cpu().numpy()[0][:len(dA)], np.sort(full, axis=1)[:, 1].astype(np.float32))
+
+
+def test_match_ties_pick_first_index(gpu):
+    import torch
+    from vfx_image_stitching_amd import _lib
+    rng = np.random.default_rng(7)
+    cap = 300
+    A = rng.integers(0, 256, (cap, 128)).astype(np.float32)
+    B = np.repeat(rng.integers(0, 256, (cap // 3, 128)), 3, axis=0).astype(np.float32)  # triplets
+    d = np.stack([A, B])
+    desc = torch.from_numpy(d).cuda()
+    counts = torch.tensor([cap, cap], dtype=torch.int32).cuda()
+    best = torch.empty((1, cap), dtype=torch.int32).cuda()
+    d1 = torch.empty((1, cap)).cuda()
+    d2 = torch.empty((1, cap)).cuda()
+    hp = np.array([0, 1], np.int32)
+    gpu.check(gpu.lib.pano_match(gpu.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), 1, 1,
+                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2)))
+    j, dist = ostitch.nn_match_sift(A, B)
+    np.testing.assert_array_equal(best.cpu().numpy()[0], j)
+    assert (best.cpu().numpy()[0] % 3 == 0).all()          # first of each tied triplet
+    np.testing.assert_array_equal(d2.cpu().numpy()[0], d1.cpu().numpy()[0])
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 5, 300, 2500])
+def test_ransac_translate_vs_oracle(gpu, k):
+    import torch
+    from vfx_image_stitching_amd import _lib
+    rng = np.random.default_rng(k)
+    pts = []
+    for _ in range(k):
+        a = tuple(float(np.float32(v)) for v in rng.uniform(0, 400, 2))
+        dx = -245.7 + rng.choice([0.0, 0.0, rng.normal(0, 0.8), rng.uniform(-100, 100)])
+        b = (float(np.float32(a[0] - dx)), float(np.float32(a[1] + rng.normal(4, 0.5))))
+        pts.append((a, b))
+    want = ostitch.ransac(pts, 3)
+    mv = np.array([(a[0] - b[0], a[1] - b[1]) for a, b in pts], np.float64).reshape(-1, 2)
+    dmv = torch.from_numpy(mv).cuda()
+    out = torch.empty(2, dtype=torch.int32).cuda()
+    gpu.check(gpu.lib.pano_ransac_translate(gpu.h, _lib.ptr(dmv) if k else None, k, 3.0, _lib.ptr(out)))
+    o = out.cpu().numpy()
+    if k == 0:
+        assert o[0] == -1 and want == ((0, 0), None)
+    else:
+        assert pts[o[0]] == want[1]
+
+
+# ------------------------------------------------------------------ Harris H1..H4
+@pytest.mark.parametrize("setname", ["parrington", "grail"])
+def test_harris_features_bit_exact(gpu, setname, gold_npz):
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, _ = data.load_set(setname)
+    st = Stitcher("harris")
+    cyl, _ = st.cylindrical(st.upload(frames), focals)
+    xy, desc, counts = st.features(cyl)
+    z = gold_npz(f"harris_{setname}_features.npz")
+    n = counts.cpu().numpy()
+    for i in range(len(frames)):
+        np.testing.assert_array_equal(xy[i, :n[i]].cpu().numpy(), z[f"kps_{i}"])
+        np.testing.assert_array_equal(desc[i, :n[i]].cpu().numpy(), z[f"desc_{i}"])
+
+
+def test_harris_match_sdot_order(gpu, gold_npz):
+    import torch
+    from vfx_image_stitching_amd import _lib
+    z = gold_npz("harris_parrington_features.npz")
+    dA, dB = z["desc_0"], z["desc_1"]
+    cap = max(len(dA), len(dB))
+    d = np.zeros((2, cap, 128), np.float32)
+    d[0, :len(dA)] = dA
+    d[1, :len(dB)] = dB
+    desc = torch.from_numpy(d).cuda()
+    counts = torch.tensor([len(dA), len(dB)], dtype=torch.int32).cuda()
+    best = torch.empty((1, cap), dtype=torch.int32).cuda()
+    d1 = torch.empty((1, cap)).cuda()
+    d2 = torch.empty((1, cap)).cuda()
+    hp = np.array([0, 1], np.int32)
+    gpu.check(gpu.lib.pano_match(gpu.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), 1, 0,
+                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2)))
+    j, dist = ostitch.nn_match_harris(dA, dB)
+    np.testing.assert_array_equal(best.cpu().numpy()[0][:len(dA)], j)
+    np.testing.assert_array_equal(d1.cpu().numpy()[0][:len(dA)], dist)
+
+
+# ------------------------------------------------------------------ B1 composite / blend / crop
+def test_composite_from_golden_shifts_bit_exact(st_sift, parr_dev, gold_json):
+    from vfx_image_stitching_amd.pipeline import drift_correct
+    _, cyl, colnz = parr_dev
+    gold = gold_json("sift_parrington.json")
+    shifts = [tuple(s["move"]) for s in gold["shifts"]]
+    pairs = [(p[0][0], p[0][1], p[1][0], p[1][1]) for p in (s["pair"] for s in gold["shifts"])]
+    canvas = st_sift.composite(cyl, colnz, drift_correct(shifts), pairs)
+    assert digest(canvas.cpu().numpy()) == gold["steps"][-1]["digest"]
+
+
+def test_blend_two_images_vs_oracle(gpu):
+    from vfx_image_stitching_amd.stitching import blend_two_images
+    rng = np.random.default_rng(11)
+    for trial in range(12):
+        hA, wA = rng.integers(20, 60, 2)
+        A = rng.integers(0, 256, (hA, wA, 3)).astype(np.uint8)
+        B = rng.integers(0, 256, (int(hA + rng.integers(0, 4)), int(rng.integers(20, 60)), 3)).astype(np.uint8)
+        A[:, :3] = 0                                    # zero columns: flags must see them
+        dx = float(rng.uniform(-30, 30)) if trial % 3 else float(-rng.integers(5, 20))
+        ref = ((float(rng.uniform(0, 30)), float(rng.uniform(0, 20))),
+               (float(rng.uniform(0, 30)), float(rng.uniform(0, 20))))
+        dy = float(rng.uniform(-3, 3))
+        want = ostitch.blend_two_images((dx, dy), ref, A, B)
+        got = blend_two_images((dx, dy), ref, A, B)
+        assert np.array_equal(got, want), trial
+
+
+def test_rectangle_crop_vs_oracle(gpu):
+    from vfx_image_stitching_amd.stitching import rectangle_crop
+    rng = np.random.default_rng(5)
+    img = np.zeros((80, 120, 3), np.uint8)
+    img[10:70, 7:111] = rng.integers(1, 255, (60, 104, 3))
+    img[12, 3] = (0, 0, 1)                              # gray 0: below threshold
+    for margin in (0, 5, 40):
+        assert np.array_equal(rectangle_crop(img, 0, margin), ostitch.rectangle_crop(img, 0, margin))
+    blank = np.zeros((8, 8, 3), np.uint8)
+    assert rectangle_crop(blank, 0, 3) is blank
+
+
+# ------------------------------------------------------------------ end to end
+@pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("sift", "grail"),
+                                            ("harris", "parrington"), ("harris", "grail"),
+                                            ("harris", "out")])
+def test_end_to_end_panorama_bit_exact(gpu, method, setname, gold_json):
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = data.load_set(setname)
+    st = Stitcher(method)
+    res = st.run(st.upload(frames), focals, margin=margin)
+    gold = gold_json(f"{method}_{setname}.json")
+    assert [list(s) for s in res.shifts] == [s["move"] for s in gold["shifts"]]
+    pano = res.panorama.cpu().numpy()
+    assert list(pano.shape) == gold["pano_shape"]
+    assert digest(pano) == gold["pano_digest"]          # PSNR = inf vs the reference
+
+
+def test_determinism(gpu, parrington):
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = parrington
+    st = Stitcher("sift")
+    d = st.upload(frames)
+    outs = [digest(st.run(d, focals, margin=margin).panorama.cpu().numpy()) for _ in range(3)]
+    feats = []
+    for _ in range(2):
+        k, de, c = st.features(st.cylindrical(d, focals)[0])
+        feats.append((k.cpu().numpy().tobytes(), de.cpu().numpy().tobytes()))
+    assert len(set(outs)) == 1 and feats[0] == feats[1]
+
+
+def test_synthetic_sequence_recovers_known_shift(gpu):
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    frames, focals, jit = data.synthetic_sequence(n_frames=5, h=270, w=480, step=300, focal=400.0)
+    st = Stitcher("sift")
+    res = st.run(st.upload(frames), focals, margin=3)
+    for i, (dx, dy) in enumerate(res.shifts):
+        assert abs(dx + 300) <= 1.5, (i, dx)
+        assert abs(dy - (jit[i + 1] - jit[i])) <= 1.5, (i, dy)

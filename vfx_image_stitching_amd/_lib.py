@@ -104,7 +104,16 @@ SIGNATURES = {
     "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),
     "pano_blend_two": (_I, [_P, _P, _I, _I, _P, _I, _I, _PI32, _D, _P]),
     "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),
+    "pano_prof_enable": (_I, [_P, _I]),
+    "pano_prof_read": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int), _PD, _PD, _PD]),
 }
+
+# kernel classes of pano_prof_enable (include/pano.h PANO_K_*)
+KERNELS = ["cyl_scatter", "cyl_gather", "blur_level", "extrema_localize", "orientation",
+           "sort_dedup", "descriptor", "row_norms", "dist_mfma", "dist_direct", "reduce_parts",
+           "pair_shifts", "composite_step", "gray_bbox", "to_gray", "structure_blur", "response",
+           "nms", "select_top", "harris_desc"]
+K_ALL = len(KERNELS)
 
 _lib = None
 _lock = threading.Lock()
@@ -163,6 +172,18 @@ class Context:
 
     def sync(self):
         self.check(self.lib.pano_sync(self.h))
+
+    def prof_enable(self, kernel):
+        k = kernel if isinstance(kernel, int) else (K_ALL if kernel == "all" else KERNELS.index(kernel))
+        self.check(self.lib.pano_prof_enable(self.h, k))
+
+    def prof_read(self, kernel):
+        k = kernel if isinstance(kernel, int) else (K_ALL if kernel == "all" else KERNELS.index(kernel))
+        n = ctypes.c_int()
+        tot, mn, mx = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        self.check(self.lib.pano_prof_read(self.h, k, ctypes.byref(n), ctypes.byref(tot),
+                                           ctypes.byref(mn), ctypes.byref(mx)))
+        return {"launches": n.value, "total_ms": tot.value, "min_ms": mn.value, "max_ms": mx.value}
 
     def close(self):
         if getattr(self, "h", None):

@@ -343,8 +343,11 @@ int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz,
     if (first_xy[0] < 0 || first_xy[1] < 0 || first_xy[0] + w > W || first_xy[1] + h > H)
         return pano_fail(ctx, PANO_E_ARG, "pano_composite: frame 0 outside canvas");
     dim3 g0((w + 63) / 64, (h + 3) / 4);
-    place_first<<<g0, 256, 0, ctx->stream>>>(frames, colnz, h, w, canvas, W, first_xy[1],
-                                             first_xy[0], F[0], F[1]);
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        place_first<<<g0, 256, 0, ctx->stream>>>(frames, colnz, h, w, canvas, W, first_xy[1],
+                                                 first_xy[0], F[0], F[1]);
+    }
     PANO_LAUNCH_CHECK(ctx, "place_first");
     int prev_fx = -1;
     for (int i = 1; i < n; ++i) {
@@ -361,8 +364,11 @@ int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz,
         s.frame_is_a = st.frame_is_a;
         s.overlap = st.overlap_range;
         const uint8_t *fr = frames + (size_t)i * h * w * 3;
-        composite_step<<<(w + CPB - 1) / CPB, 256, 0, ctx->stream>>>(
-            fr, colnz + (size_t)i * w, h, w, canvas, W, s, F[(i - 1) & 1], F[i & 1]);
+        {
+            PanoProf prof_(ctx, PK_COMPOSITE);
+            composite_step<<<(w + CPB - 1) / CPB, 256, 0, ctx->stream>>>(
+                fr, colnz + (size_t)i * w, h, w, canvas, W, s, F[(i - 1) & 1], F[i & 1]);
+        }
         PANO_LAUNCH_CHECK(ctx, "composite_step");
         prev_fx = st.frame_x;
     }
@@ -381,11 +387,17 @@ int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint
     col_flags2<<<(WW + 255) / 256, 256, 0, ctx->stream>>>(A, hA, wA, g[0], g[1], B, hB, wB, g[2],
                                                           g[3], WW, fa, fb);
     PANO_LAUNCH_CHECK(ctx, "col_flags2");
-    both_rank<<<1, 1024, 0, ctx->stream>>>(fa, fb, WW, rank);
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        both_rank<<<1, 1024, 0, ctx->stream>>>(fa, fb, WW, rank);
+    }
     PANO_LAUNCH_CHECK(ctx, "both_rank");
     dim3 grid((WW + 63) / 64, (HH + 3) / 4);
-    blend_two<<<grid, 256, 0, ctx->stream>>>(A, hA, wA, g[0], g[1], B, hB, wB, g[2], g[3], HH, WW,
-                                             fa, fb, rank, overlap, out);
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        blend_two<<<grid, 256, 0, ctx->stream>>>(A, hA, wA, g[0], g[1], B, hB, wB, g[2], g[3], HH, WW,
+                                                 fa, fb, rank, overlap, out);
+    }
     PANO_LAUNCH_CHECK(ctx, "blend_two");
     return PANO_OK;
 }
@@ -396,7 +408,10 @@ int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, i
     const size_t total = (size_t)H * W;
     unsigned blocks = (unsigned)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    gray_bbox<<<blocks, 256, 0, ctx->stream>>>(img, H, W, thr, bbox);
+    {
+        PanoProf prof_(ctx, PK_BBOX);
+        gray_bbox<<<blocks, 256, 0, ctx->stream>>>(img, H, W, thr, bbox);
+    }
     bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
     PANO_LAUNCH_CHECK(ctx, "gray_bbox");
     return PANO_OK;

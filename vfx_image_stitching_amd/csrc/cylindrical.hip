@@ -79,11 +79,17 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
         FocalArg fa;
         for (int i = 0; i < nf; ++i) fa.f[i] = h_focal[f0 + i];
         dim3 grid((w + 63) / 64, (h + 3) / 4, nf);
-        cyl_scatter<<<grid, 256, 0, ctx->stream>>>(win + f0 * plane, h, w, fa);
+        {
+            PanoProf prof_(ctx, PK_CYL_SCATTER);
+            cyl_scatter<<<grid, 256, 0, ctx->stream>>>(win + f0 * plane, h, w, fa);
+        }
         PANO_LAUNCH_CHECK(ctx, "cyl_scatter");
-        cyl_gather<<<grid, 256, 0, ctx->stream>>>(src + f0 * plane * 3, dst + f0 * plane * 3,
-                                                  win + f0 * plane,
-                                                  colnz ? colnz + (size_t)f0 * w : nullptr, h, w);
+        {
+            PanoProf prof_(ctx, PK_CYL_GATHER);
+            cyl_gather<<<grid, 256, 0, ctx->stream>>>(src + f0 * plane * 3, dst + f0 * plane * 3,
+                                                      win + f0 * plane,
+                                                      colnz ? colnz + (size_t)f0 * w : nullptr, h, w);
+        }
         PANO_LAUNCH_CHECK(ctx, "cyl_gather");
     }
     return PANO_OK;

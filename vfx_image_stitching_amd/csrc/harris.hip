@@ -354,27 +354,45 @@ int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int ma
     int32_t *err = (int32_t *)(base + o_err);
     HCand *cands = (HCand *)(base + o_c);
     PANO_HIP(ctx, hipMemsetAsync(base + o_max, 0, o_c - o_max, ctx->stream));
-    to_gray<<<(unsigned)((plane * n + 255) / 256), 256, 0, ctx->stream>>>(bgr, gray, plane * n);
+    {
+        PanoProf prof_(ctx, PK_H_GRAY);
+        to_gray<<<(unsigned)((plane * n + 255) / 256), 256, 0, ctx->stream>>>(bgr, gray, plane * n);
+    }
     PANO_LAUNCH_CHECK(ctx, "to_gray");
     Taps21 t21;
     gauss_f64<21>(2.0, t21.k);
     dim3 gb((w + HT - 1) / HT, (h + HT - 1) / HT, 3 * n);
-    structure_blur<<<gb, 256, 0, ctx->stream>>>(gray, h, w, t21, S);
+    {
+        PanoProf prof_(ctx, PK_H_BLUR);
+        structure_blur<<<gb, 256, 0, ctx->stream>>>(gray, h, w, t21, S);
+    }
     PANO_LAUNCH_CHECK(ctx, "structure_blur");
     unsigned rb = (unsigned)((plane + 255) / 256);
     if (rb > 512) rb = 512;
-    response<<<dim3(rb, n), 256, 0, ctx->stream>>>(S, n, h, w, 0.05, R, fmx);
+    {
+        PanoProf prof_(ctx, PK_H_RESP);
+        response<<<dim3(rb, n), 256, 0, ctx->stream>>>(S, n, h, w, 0.05, R, fmx);
+    }
     PANO_LAUNCH_CHECK(ctx, "response");
     dim3 gn((w - 2 + 63) / 64, (h - 2 + 3) / 4, n);
-    nms<<<gn, 256, 0, ctx->stream>>>(R, h, w, 0.02, fmx, cands, cnt);
+    {
+        PanoProf prof_(ctx, PK_H_NMS);
+        nms<<<gn, 256, 0, ctx->stream>>>(R, h, w, 0.02, fmx, cands, cnt);
+    }
     PANO_LAUNCH_CHECK(ctx, "nms");
     const size_t sm = kSel * (sizeof(unsigned long long) + sizeof(uint32_t));
-    select_top<<<n, 1024, sm, ctx->stream>>>(cands, cnt, h, w, max_points, xy, counts, err);
+    {
+        PanoProf prof_(ctx, PK_H_SELECT);
+        select_top<<<n, 1024, sm, ctx->stream>>>(cands, cnt, h, w, max_points, xy, counts, err);
+    }
     PANO_LAUNCH_CHECK(ctx, "select_top");
     Taps9 t9;
     gauss_f64<9>(1.5 * 3, t9.k);
     dim3 gd((max_points + 3) / 4, n);
-    harris_desc<<<gd, 256, 0, ctx->stream>>>(gray, h, w, t9, xy, counts, max_points, desc);
+    {
+        PanoProf prof_(ctx, PK_H_DESC);
+        harris_desc<<<gd, 256, 0, ctx->stream>>>(gray, h, w, t9, xy, counts, max_points, desc);
+    }
     PANO_LAUNCH_CHECK(ctx, "harris_desc");
     return PANO_OK;
 }

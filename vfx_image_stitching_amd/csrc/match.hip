@@ -252,7 +252,10 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
         float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 + (size_t)p0 * cap;
         if (!exact_int) {
             dim3 grid(cap, np);
-            dist_direct<<<grid, 256, 0, ctx->stream>>>(desc, counts, cap, pa, bp, p1, p2);
+            {
+                PanoProf prof_(ctx, PK_DIST_DIRECT);
+                dist_direct<<<grid, 256, 0, ctx->stream>>>(desc, counts, cap, pa, bp, p1, p2);
+            }
             PANO_LAUNCH_CHECK(ctx, "dist_direct");
             continue;
         }
@@ -264,13 +267,22 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
         float *norms = (float *)ctx->mscratch;
         Part *parts = (Part *)((char *)ctx->mscratch + norm_bytes);
         const size_t rows = (size_t)n_frames * cap;
-        row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
+        {
+            PanoProf prof_(ctx, PK_NORMS);
+            row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
+        }
         PANO_LAUNCH_CHECK(ctx, "row_norms");
         dim3 grid(n_t, n_t, np);
-        dist_mfma<<<grid, 256, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+        {
+            PanoProf prof_(ctx, PK_DIST_MFMA);
+            dist_mfma<<<grid, 256, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+        }
         PANO_LAUNCH_CHECK(ctx, "dist_mfma");
         dim3 g2((cap + 255) / 256, np);
-        reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_t, bp, p1, p2);
+        {
+            PanoProf prof_(ctx, PK_REDUCE);
+            reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_t, bp, p1, p2);
+        }
         PANO_LAUNCH_CHECK(ctx, "reduce_parts");
     }
     return PANO_OK;

@@ -94,6 +94,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
     delete ctx;
     return PANO_OK;
 }
@@ -213,6 +214,36 @@ int pano_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_
 int pano_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox) {
     if (!ctx) return PANO_E_ARG;
     return launch_gray_bbox(ctx, img, H, W, thr, bbox);
+}
+
+int pano_prof_enable(pano_ctx *ctx, int kernel_class) {
+    if (!ctx || kernel_class < -1 || kernel_class > PK_COUNT) return PANO_E_ARG;
+    ctx->prof.kernel = kernel_class;
+    ctx->prof.used = 0;
+    return PANO_OK;
+}
+
+int pano_prof_read(pano_ctx *ctx, int kernel_class, int *launches, double *total_ms,
+                   double *min_ms, double *max_ms) {
+    if (!ctx || !launches || !total_ms) return PANO_E_ARG;
+    PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int n = 0;
+    double tot = 0.0, mn = 1e30, mx = 0.0;
+    for (size_t i = 0; i + 1 < ctx->prof.used; i += 2) {
+        if (kernel_class != PK_COUNT && ctx->prof.kid[i / 2] != kernel_class) continue;
+        float ms = 0.0f;
+        PANO_HIP(ctx, hipEventElapsedTime(&ms, ctx->prof.ev[i], ctx->prof.ev[i + 1]));
+        ++n;
+        tot += ms;
+        mn = ms < mn ? ms : mn;
+        mx = ms > mx ? ms : mx;
+    }
+    *launches = n;
+    *total_ms = tot;
+    if (min_ms) *min_ms = n ? mn : 0.0;
+    if (max_ms) *max_ms = mx;
+    ctx->prof.used = 0;
+    return PANO_OK;
 }
 
 }  // extern "C"

@@ -21,12 +21,13 @@
 
 // Raw keypoint produced by the orientation kernel (before sort/dedup/convert), in base
 // (2x upsampled) coordinates, exactly the fields sift_impl.py:206-210/290 stores, plus a
-// deterministic scan-order tie-break (candidate id << 8 | peak index).
+// deterministic scan-order tie-break.
 struct RawKp {
     float x, y, size, angle, response;
     int32_t octave;       // packed cv2 octave field
     int32_t frame;
-    uint32_t order;       // scan-order tie-break
+    int32_t pad;
+    uint64_t order;       // scan-order tie-break: (candidate scan order << 6) | peak bin
 };
 
 // Localised extremum (sift_impl.py:169-211 output) waiting for orientation assignment.
@@ -42,6 +43,20 @@ struct Cand {
 struct LevelView {
     float *ptr;      // [n][h][w]
     int h, w;
+};
+
+// Kernel classes for the live HIP-event profiler (pano_prof_enable / pano_prof_read).
+enum PanoKernel {
+    PK_CYL_SCATTER = 0, PK_CYL_GATHER, PK_BLUR, PK_EXTREMA, PK_ORIENT, PK_SORT, PK_DESC,
+    PK_NORMS, PK_DIST_MFMA, PK_DIST_DIRECT, PK_REDUCE, PK_PAIR_SHIFTS, PK_COMPOSITE, PK_BBOX,
+    PK_H_GRAY, PK_H_BLUR, PK_H_RESP, PK_H_NMS, PK_H_SELECT, PK_H_DESC, PK_COUNT
+};
+
+struct ProfState {
+    int kernel = -1;                 // -1 off, PK_COUNT = every kernel
+    std::vector<hipEvent_t> ev;      // pairs (start, stop)
+    std::vector<int> kid;            // kernel class of each pair
+    size_t used = 0;                 // events used
 };
 
 struct pano_ctx {
@@ -72,6 +87,35 @@ struct pano_ctx {
     void *hscratch = nullptr; size_t hscratch_bytes = 0;
     // ---- blend scratch
     void *bscratch = nullptr; size_t bscratch_bytes = 0;
+    // ---- live profiler
+    ProfState prof;
+};
+
+// RAII: records a start/stop hipEvent pair on the context's stream around one launch
+// when the profiler is enabled for this kernel class.
+struct PanoProf {
+    pano_ctx *ctx;
+    bool on;
+    PanoProf(pano_ctx *c, int kid) : ctx(c), on(false) {
+        ProfState &p = c->prof;
+        if (p.kernel != kid && p.kernel != PK_COUNT) return;
+        if (p.used + 2 > p.ev.size()) {
+            for (int i = 0; i < 64; ++i) {
+                hipEvent_t e;
+                if (hipEventCreate(&e) != hipSuccess) return;
+                p.ev.push_back(e);
+            }
+        }
+        p.kid.resize(p.ev.size() / 2);
+        p.kid[p.used / 2] = kid;
+        on = hipEventRecord(p.ev[p.used], c->stream) == hipSuccess;
+    }
+    ~PanoProf() {
+        if (!on) return;
+        ProfState &p = ctx->prof;
+        (void)hipEventRecord(p.ev[p.used + 1], ctx->stream);
+        p.used += 2;
+    }
 };
 
 int pano_fail(pano_ctx *ctx, int code, const std::string &msg);

@@ -190,10 +190,13 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
             pa.a[q] = h_pairs[2 * (p0 + q)];
             pa.b[q] = h_pairs[2 * (p0 + q) + 1];
         }
-        pair_shifts<<<np, RB, 0, ctx->stream>>>(
-            kps, xy_i32, counts, cap, pa, best + (size_t)p0 * cap, d1 + (size_t)p0 * cap,
-            d2 + (size_t)p0 * cap, (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, thr,
-            moves + (size_t)p0 * cap, midx + (size_t)p0 * cap, recs + p0);
+        {
+            PanoProf prof_(ctx, PK_PAIR_SHIFTS);
+            pair_shifts<<<np, RB, 0, ctx->stream>>>(
+                kps, xy_i32, counts, cap, pa, best + (size_t)p0 * cap, d1 + (size_t)p0 * cap,
+                d2 + (size_t)p0 * cap, (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, thr,
+                moves + (size_t)p0 * cap, midx + (size_t)p0 * cap, recs + p0);
+        }
         PANO_LAUNCH_CHECK(ctx, "pair_shifts");
     }
     return PANO_OK;
@@ -202,7 +205,10 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
 int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr,
                             int32_t *out) {
     if (k < 0 || (k > 0 && !moves) || !out) return pano_fail(ctx, PANO_E_ARG, "pano_ransac_translate");
-    ransac_moves<<<1, RB, 0, ctx->stream>>>((const double2 *)moves, k, thr, out);
+    {
+        PanoProf prof_(ctx, PK_PAIR_SHIFTS);
+        ransac_moves<<<1, RB, 0, ctx->stream>>>((const double2 *)moves, k, thr, out);
+    }
     PANO_LAUNCH_CHECK(ctx, "ransac_moves");
     return PANO_OK;
 }

@@ -569,7 +569,10 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         if (iw <= 0 || ih <= 0) continue;
         lp.octave = o;
         dim3 grid((iw + 63) / 64, (ih + 3) / 4, n * ni);
-        extrema_localize<<<grid, 256, 0, ctx->stream>>>(a, lp, ctx->cands, cand_cnt, (int)cand_cap);
+        {
+            PanoProf prof_(ctx, PK_EXTREMA);
+            extrema_localize<<<grid, 256, 0, ctx->stream>>>(a, lp, ctx->cands, cand_cnt, (int)cand_cap);
+        }
         PANO_LAUNCH_CHECK(ctx, "extrema_localize");
     }
     PyrArgs pa{};
@@ -582,19 +585,28 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio};
     {
         dim3 grid((unsigned)((cand_cap + 3) / 4), n);
-        orientation<<<grid, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap,
-                                                   ctx->raw, raw_cnt, (int)raw_cap);
+        {
+            PanoProf prof_(ctx, PK_ORIENT);
+            orientation<<<grid, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap,
+                                                       ctx->raw, raw_cnt, (int)raw_cap);
+        }
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
     {
         const size_t sm = kSortMax * (sizeof(unsigned long long) + sizeof(uint32_t));
-        sort_dedup<<<n, 1024, sm, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, kps, cap, counts, err);
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            sort_dedup<<<n, 1024, sm, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, kps, cap, counts, err);
+        }
         PANO_LAUNCH_CHECK(ctx, "sort_dedup");
     }
     {
         DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
         dim3 grid(cap, n);
-        descriptor<<<grid, 256, 0, ctx->stream>>>(pa, dp, kps, counts, cap, desc);
+        {
+            PanoProf prof_(ctx, PK_DESC);
+            descriptor<<<grid, 256, 0, ctx->stream>>>(pa, dp, kps, counts, cap, desc);
+        }
         PANO_LAUNCH_CHECK(ctx, "descriptor");
     }
     return PANO_OK;

@@ -153,7 +153,10 @@ int launch_blur(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float
     if (sm > 65536)
         PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_level<MODE>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    blur_level<MODE><<<grid, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+    {
+        PanoProf prof_(ctx, PK_BLUR);
+        blur_level<MODE><<<grid, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+    }
     PANO_LAUNCH_CHECK(ctx, "blur_level");
     return PANO_OK;
 }

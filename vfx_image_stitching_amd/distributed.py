@@ -1,0 +1,181 @@
+"""Multi-GPU stitching: pairs shard across ranks, one gather of per-pair records.
+
+SURVEY.md section 8(e): pairs are independent until drift correction / compositing, so
+
+  1. rank r owns a contiguous range of pairs and the frames they touch (+1 boundary
+     frame); it runs cylindrical projection, features, matching and RANSAC locally;
+  2. ONE all_gather (RCCL over xGMI for backend "nccl", gloo on CPU tests) of the 64-byte
+     pano_pair_rec records of every pair -- the only data-path exchange;
+  3. every rank replays drift correction and the composite plan for the WHOLE sequence
+     on the host (a few microseconds), then composites its own band of the canvas.
+     Bands are independent when no column is covered by three frames (frame i never
+     reaches frame i-2: true whenever |dx| > w/2, e.g. parrington / grail / synthetic);
+     otherwise band compositing is refused (``BandError``).
+  4. rectangle_crop needs the global bounding box: a 4-int all_reduce (min/max).
+
+The host logic here is device-agnostic so it is unit-tested with gloo on the CPU; the
+GPU work is the libpano calls of pipeline.Stitcher.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import PanoError
+
+
+class BandError(PanoError):
+    def __init__(self, msg):
+        super().__init__(_lib.PANO_E_UNSUPPORTED, msg)
+
+
+def shard_ranges(n_pairs: int, world: int):
+    """Contiguous balanced pair ranges: rank r -> (first pair, pair count)."""
+    base, extra = divmod(n_pairs, world)
+    out, start = [], 0
+    for r in range(world):
+        c = base + (1 if r < extra else 0)
+        out.append((start, c))
+        start += c
+    return out
+
+
+def gather_records(local: "object", counts, group=None):
+    """all_gather of fixed-size uint8 [P_max, 64] record blocks -> global PAIR_NP array."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    pmax = max(counts)
+    buf = torch.zeros((pmax, 64), dtype=torch.uint8, device=local.device)
+    buf[:local.shape[0]] = local
+    out = torch.empty((world * pmax, 64), dtype=torch.uint8, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    h = out.cpu().numpy().reshape(world, pmax, 64)
+    recs = [h[r, :counts[r]] for r in range(world)]
+    return np.ascontiguousarray(np.concatenate(recs)).view(_lib.PAIR_NP).reshape(-1)
+
+
+def records_to_shifts(recs, integer=False):
+    shifts, pairs = [], []
+    for r in recs:
+        if r["status"] != _lib.PANO_OK:
+            raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+        cast = int if integer else float
+        shifts.append((cast(r["dx"]), cast(r["dy"])))
+        pairs.append(((cast(r["xA"]), cast(r["yA"])), (cast(r["xB"]), cast(r["yB"]))))
+    return shifts, pairs
+
+
+def global_plan(shifts_corr, pairs, n_frames, h, w):
+    """pano_plan_composite over the whole sequence -> (steps list, first_xy, (H, W))."""
+    lib = _lib.load()
+    sh = np.ascontiguousarray(np.array(shifts_corr, np.float64).reshape(-1, 2))
+    pr = np.ascontiguousarray(np.array([[a[0], a[1], b[0], b[1]] for a, b in pairs],
+                                       np.float64).reshape(-1, 4))
+    steps = (_lib.Step * max(n_frames - 1, 1))()
+    first = np.zeros(2, np.int32)
+    hw = np.zeros(2, np.int32)
+    rc = lib.pano_plan_composite(_lib.f64p(sh), _lib.f64p(pr), n_frames, h, w, steps,
+                                 _lib.i32p(first), _lib.i32p(hw))
+    if rc:
+        raise PanoError(rc, "pano_plan_composite")
+    return list(steps)[:n_frames - 1], first.copy(), (int(hw[0]), int(hw[1]))
+
+
+def frame_xy(steps, first, i):
+    """Final-canvas top-left of frame i's content."""
+    if i == 0:
+        return int(first[0]), int(first[1])
+    s = steps[i - 1]
+    return int(s.frame_x), int(s.frame_y)
+
+
+def check_bands(steps, first, w):
+    """Band compositing is exact iff frame i never overlaps frame i-2 (see module doc)."""
+    for i in range(2, len(steps) + 1):
+        xi = frame_xy(steps, first, i)[0]
+        xk = frame_xy(steps, first, i - 2)[0]
+        if not (xi + w <= xk or xk + w <= xi):
+            raise BandError(f"frames {i} and {i - 2} overlap: bands are not independent")
+
+
+def band_plan(steps, first, w, H, f0, count):
+    """Local composite plan for frames f0 .. f0+count (rank's range incl. boundary frame).
+
+    Returns (local_steps, local_first_xy, x_offset, band_width, owned (x0, x1)).
+    The band starts from frame f0 as it stands before step f0+1 (its raw pixels in the
+    columns the next frame can reach) and applies global steps f0+1 .. f0+count.
+    Owned columns: everything the band's frames cover, minus frame f0's overlap with the
+    previous rank's frames (that rank blended those columns).
+    """
+    xs = [frame_xy(steps, first, f0 + k)[0] for k in range(count + 1)]
+    x_lo, x_hi = min(xs), max(xs) + w
+    loc = (_lib.Step * max(count, 1))()
+    for k in range(count):
+        g = steps[f0 + k]
+        s = loc[k]
+        for name, _ in _lib.Step._fields_:
+            setattr(s, name, getattr(g, name))
+        s.frame_x = g.frame_x - x_lo
+        s.canvas_x = g.canvas_x - x_lo
+    fx, fy = frame_xy(steps, first, f0)
+    first_loc = np.array([fx - x_lo, fy], np.int32)
+    own_lo, own_hi = x_lo, x_hi
+    if f0 > 0:
+        px = frame_xy(steps, first, f0 - 1)[0]
+        if px > fx:                        # previous frame to the right (dx < 0 sequences)
+            own_hi = min(own_hi, px)
+        else:
+            own_lo = max(own_lo, px + w)
+    return loc, first_loc, x_lo, x_hi - x_lo, (own_lo, own_hi)
+
+
+def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15):
+    """One rank's share of a sharded stitch (frames_dev = its pair range + boundary frame).
+
+    Returns dict(records=global PAIR_NP, band=device canvas of the owned band,
+    bbox=global crop box, x_offset=band's first column in the final canvas).
+    """
+    import torch
+    import torch.distributed as dist
+    n_local = frames_dev.shape[0]
+    h, w = frames_dev.shape[1], frames_dev.shape[2]
+    cyl, colnz = stitcher.cylindrical(frames_dev, focals)
+    feats = stitcher.features(cyl)
+    recs_dev, _ = stitcher.pair_records(feats, [(i, i + 1) for i in range(n_local - 1)])
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world > 1:
+        recs = gather_records(recs_dev, pair_counts, group)
+    else:
+        recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)
+    from .pipeline import drift_correct
+    shifts, pairs = records_to_shifts(recs, integer=stitcher.method != "sift")
+    steps, first, (H, W) = global_plan(drift_correct(shifts), pairs, len(shifts) + 1, h, w)
+    if world > 1:
+        check_bands(steps, first, w)
+    loc, first_loc, x0, bw, (own_lo, own_hi) = band_plan(steps, first, w, H, pair_start,
+                                                         n_local - 1)
+    band = stitcher._get("band", (H, bw, 3), torch.uint8)
+    ctx = stitcher.ctx
+    ctx.check(ctx.lib.pano_composite(ctx.h, _lib.ptr(cyl), _lib.ptr(colnz), n_local, h, w, loc,
+                                     _lib.i32p(first_loc), _lib.ptr(band), H, bw))
+    owned = band[:, own_lo - x0:own_hi - x0].contiguous()
+    bb = stitcher.bbox(owned).to(torch.int64)
+    lo = torch.where(bb[1] >= 0, bb, torch.tensor([1 << 30, -1, 1 << 30, -1], device=bb.device))
+    lo[2] += own_lo
+    lo[3] = torch.where(lo[3] >= 0, lo[3] + own_lo, lo[3])
+    if world > 1:
+        mins = torch.stack([lo[0], lo[2]])
+        maxs = torch.stack([lo[1], lo[3]])
+        dist.all_reduce(mins, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(maxs, op=dist.ReduceOp.MAX, group=group)
+        g = (int(mins[0]), int(maxs[0]), int(mins[1]), int(maxs[1]))
+    else:
+        v = lo.cpu().numpy()
+        g = (int(v[0]), int(v[1]), int(v[2]), int(v[3]))
+    if g[1] >= 0:
+        y0, y1 = max(0, g[0] + margin), min(H - 1, g[1] - margin)
+    else:
+        y0, y1 = 0, H - 1
+    return {"records": recs, "band": owned, "x_offset": own_lo, "canvas_hw": (H, W),
+            "bbox": (y0, y1, g[2], g[3])}
