@@ -14,7 +14,7 @@ timeout -k 10 600 python bench.py --steps $STEPS --warmup 3 ${BENCH_ARGS:-} > gp
 rc=$?; echo "bench rc=$rc"; tail -n 3 gpurun_out/bench.txt
 fatal $rc && exit $rc
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"
   find gpurun_out/prof -name "*stats*" | head
 fi
