@@ -174,6 +174,18 @@ int pano_composite(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t *d_coln
                    int h, int w, const pano_step *h_steps, const int32_t *h_first_xy,
                    uint8_t *d_canvas, int H, int W);
 
+/* pano_composite + rectangle_crop's bounding box in the same pass: d_bbox[4] = ymin ymax
+ * xmin xmax of gray > black_threshold over the canvas (-1s if none).  When no canvas
+ * column is covered by three frames (checked on the host) the fold runs as one parallel
+ * pass over the canvas (3 launches); otherwise it is the sequential per-step fold.
+ * pano_composite_sequential forces the per-step fold (reference-shaped; used by tests). */
+int pano_composite_bbox(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t *d_colnz, int n,
+                        int h, int w, const pano_step *h_steps, const int32_t *h_first_xy,
+                        uint8_t *d_canvas, int H, int W, int black_threshold, int32_t *d_bbox);
+int pano_composite_sequential(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t *d_colnz,
+                              int n, int h, int w, const pano_step *h_steps,
+                              const int32_t *h_first_xy, uint8_t *d_canvas, int H, int W);
+
 /* blend_two_images(shift_vec, ref_match, imgA, imgB) for arbitrary inputs
  * image_stitching_sift.py:156-202.  Geometry comes from pano_blend_geometry. */
 int pano_blend_geometry(double dx, double dy, const double *h_ref4, int hA, int wA, int hB,

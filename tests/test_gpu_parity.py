@@ -270,6 +270,25 @@ def test_composite_from_golden_shifts_bit_exact(st_sift, parr_dev, gold_json):
     assert digest(canvas.cpu().numpy()) == gold["steps"][-1]["digest"]
 
 
+@pytest.mark.parametrize("method,setname", [("sift", "grail"), ("harris", "parrington")])
+def test_sequential_and_parallel_fold_agree(gpu, method, setname, gold_json):
+    """The parallel compositor and the reference-shaped per-step fold give the same mosaic."""
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher, drift_correct
+    names, frames, focals, margin = data.load_set(setname)
+    st = Stitcher(method)
+    cyl, colnz = st.cylindrical(st.upload(frames), focals)
+    gold = gold_json(f"{method}_{setname}.json")
+    shifts = [tuple(s["move"]) for s in gold["shifts"]]
+    pairs = [(p[0][0], p[0][1], p[1][0], p[1][1]) for p in (s["pair"] for s in gold["shifts"])]
+    seq = st.composite(cyl, colnz, drift_correct(shifts), pairs, sequential=True).cpu().numpy()
+    par, bb = st.composite(cyl, colnz, drift_correct(shifts), pairs, bbox=True)
+    assert digest(seq) == gold["steps"][-1]["digest"]
+    assert np.array_equal(par.cpu().numpy(), seq)
+    ys, xs = np.nonzero(ostitch.cv2_compat.bgr_to_gray_u8(seq) > 0)
+    assert bb.cpu().numpy().tolist() == [ys.min(), ys.max(), xs.min(), xs.max()]
+
+
 def test_blend_two_images_vs_oracle(gpu):
     from vfx_image_stitching_amd.stitching import blend_two_images
     rng = np.random.default_rng(11)

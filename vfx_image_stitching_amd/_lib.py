@@ -101,6 +101,10 @@ SIGNATURES = {
     "pano_ransac_translate": (_I, [_P, _P, _I, _D, _P]),
     "pano_plan_composite": (_I, [_PD, _PD, _I, _I, _I, ctypes.POINTER(Step), _PI32, _PI32]),
     "pano_composite": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I]),
+    "pano_composite_bbox": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I,
+                                 _I, _P]),
+    "pano_composite_sequential": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P,
+                                       _I, _I]),
     "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),
     "pano_blend_two": (_I, [_P, _P, _I, _I, _P, _I, _I, _PI32, _D, _P]),
     "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),

@@ -121,6 +121,139 @@ composite_step(const uint8_t *__restrict__ frame, const uint8_t *__restrict__ co
     }
 }
 
+// ------------------------------------------------------------------ parallel composite
+// Valid when frame i's columns never meet frame j <= i-2 (pano_plan_composite geometry,
+// checked on the host): then at step i the mosaic in frame i's columns is exactly frame
+// i-1's raw pixels (its A-only region of step i-1), the mosaic column flags there are
+// frame i-1's own flags, and every canvas column's final value is written by the LAST
+// step whose frame has a non-zero byte in it.  So the fold needs no sequential pass:
+//   composite_tables  per (step, frame column): mode (0 none, 1 frame only, 2 both) and
+//                     the f32 blend weights of the overlap ramp (block scan for the rank)
+//   composite_owner   per canvas column: owning step
+//   composite_pixels  per canvas pixel: copy or blend from the raw frames, and the
+//                     rectangle_crop bounding box of gray > thr (fused)
+constexpr int kMaxSeq = 256;
+struct SeqArg {
+    int fx[kMaxSeq], fy[kMaxSeq];
+    unsigned char is_a[kMaxSeq];
+    double overlap[kMaxSeq];
+};
+
+__global__ void __launch_bounds__(256)
+composite_tables(const uint8_t *__restrict__ colnz, int w, SeqArg sa, uint8_t *__restrict__ mode,
+                 float2 *__restrict__ wgt) {
+    __shared__ int sh[256];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    int carry = 0;
+    for (int base = 0; base < w; base += 256) {
+        const int c = base + tid;
+        int fF = 0, fM = 0;
+        if (c < w) {
+            fF = colnz[(size_t)i * w + c] != 0;
+            if (i > 0) {
+                const int xm = sa.fx[i] + c - sa.fx[i - 1];
+                fM = (xm >= 0 && xm < w) ? colnz[(size_t)(i - 1) * w + xm] != 0 : 0;
+            }
+        }
+        const int both = fF && fM;
+        sh[tid] = both;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            const int t = tid >= off ? sh[tid - off] : 0;
+            __syncthreads();
+            sh[tid] += t;
+            __syncthreads();
+        }
+        if (c < w) {
+            const int rank = carry + sh[tid] - both;
+            mode[(size_t)i * w + c] = (uint8_t)(fF ? (both ? 2 : 1) : 0);
+            const double ov = sa.overlap[i];
+            const double alpha = ov != 0.0 ? (double)rank / ov : 0.0;
+            wgt[(size_t)i * w + c] = make_float2((float)(1.0 - alpha), (float)alpha);
+        }
+        carry += sh[255];
+        __syncthreads();
+    }
+}
+
+__global__ void composite_owner(const uint8_t *__restrict__ mode, int n, int w, int W, SeqArg sa,
+                                int32_t *__restrict__ owner) {
+    const int X = blockIdx.x * blockDim.x + threadIdx.x;
+    if (X >= W) return;
+    int o = -1;
+    for (int i = n - 1; i >= 0; --i) {
+        const int c = X - sa.fx[i];
+        if (c >= 0 && c < w && mode[(size_t)i * w + c]) { o = i; break; }
+    }
+    owner[X] = o;
+}
+
+__global__ void __launch_bounds__(256)
+composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const uint8_t *__restrict__ mode,
+                 const float2 *__restrict__ wgt, const int32_t *__restrict__ owner, SeqArg sa,
+                 uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox) {
+    __shared__ int r[4][256];
+    const int tid = threadIdx.x;
+    const int X = blockIdx.x * 64 + (tid & 63);
+    const int y = blockIdx.y * 4 + (tid >> 6);
+    int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
+    if (X < W && y < H) {
+        const int i = owner[X];
+        uint8_t o0 = 0, o1 = 0, o2 = 0;
+        if (i >= 0) {
+            const int c = X - sa.fx[i];
+            const int fyl = y - sa.fy[i];
+            uint8_t F[3] = {0, 0, 0};
+            if (fyl >= 0 && fyl < h) {
+                const uint8_t *p = frames + (((size_t)i * h + fyl) * w + c) * 3;
+                F[0] = p[0]; F[1] = p[1]; F[2] = p[2];
+            }
+            if (mode[(size_t)i * w + c] == 2) {
+                uint8_t M[3] = {0, 0, 0};
+                const int cm = X - sa.fx[i - 1], ym = y - sa.fy[i - 1];
+                if (cm >= 0 && cm < w && ym >= 0 && ym < h) {
+                    const uint8_t *q = frames + (((size_t)(i - 1) * h + ym) * w + cm) * 3;
+                    M[0] = q[0]; M[1] = q[1]; M[2] = q[2];
+                }
+                const float2 ab = wgt[(size_t)i * w + c];
+                if (sa.is_a[i]) {
+                    o0 = blend_px(ab.x, ab.y, F[0], M[0]);
+                    o1 = blend_px(ab.x, ab.y, F[1], M[1]);
+                    o2 = blend_px(ab.x, ab.y, F[2], M[2]);
+                } else {
+                    o0 = blend_px(ab.x, ab.y, M[0], F[0]);
+                    o1 = blend_px(ab.x, ab.y, M[1], F[1]);
+                    o2 = blend_px(ab.x, ab.y, M[2], F[2]);
+                }
+            } else {
+                o0 = F[0]; o1 = F[1]; o2 = F[2];
+            }
+        }
+        uint8_t *d = canvas + ((size_t)y * W + X) * 3;
+        d[0] = o0; d[1] = o1; d[2] = o2;
+        const uint8_t px[3] = {o0, o1, o2};
+        if (bbox && gray_u8(px) > thr) { ymin = ymax = y; xmin = xmax = X; }
+    }
+    if (!bbox) return;
+    r[0][tid] = ymin; r[1][tid] = ymax; r[2][tid] = xmin; r[3][tid] = xmax;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (tid < off) {
+            r[0][tid] = min(r[0][tid], r[0][tid + off]);
+            r[1][tid] = max(r[1][tid], r[1][tid + off]);
+            r[2][tid] = min(r[2][tid], r[2][tid + off]);
+            r[3][tid] = max(r[3][tid], r[3][tid + off]);
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && r[1][0] >= 0) {
+        atomicMin(&bbox[0], r[0][0]);
+        atomicMax(&bbox[1], r[1][0]);
+        atomicMin(&bbox[2], r[2][0]);
+        atomicMax(&bbox[3], r[3][0]);
+    }
+}
+
 // ------------------------------------------------------------------ generic blend_two_images
 __global__ void col_flags2(const uint8_t *__restrict__ A, int hA, int wA, int ayA, int axA,
                            const uint8_t *__restrict__ B, int hB, int wB, int ayB, int axB,
@@ -330,18 +463,24 @@ extern "C" int pano_plan_composite(const double *shifts, const double *pairs, in
     return PANO_OK;
 }
 
-int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
-                     int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
-                     int H, int W) {
-    if (n < 1 || !frames || !colnz || !canvas || !first_xy || (n > 1 && !steps))
-        return pano_fail(ctx, PANO_E_ARG, "pano_composite: bad arguments");
+// Host check of the parallel-composite condition: frame i never shares a column with a
+// frame j <= i - 2.
+static bool bands_independent(const pano_step *steps, const int32_t *first_xy, int n, int w) {
+    auto fx = [&](int i) { return i == 0 ? first_xy[0] : steps[i - 1].frame_x; };
+    for (int i = 2; i < n; ++i)
+        for (int j = 0; j <= i - 2; ++j)
+            if (!(fx(i) + w <= fx(j) || fx(j) + w <= fx(i))) return false;
+    return true;
+}
+
+static int composite_sequential(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
+                                int h, int w, const pano_step *steps, const int32_t *first_xy,
+                                uint8_t *canvas, int H, int W) {
     int rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, 2 * (size_t)W + 64);
     if (rc) return rc;
     uint8_t *F[2] = {ctx->flags, ctx->flags + W};
     PANO_HIP(ctx, hipMemsetAsync(canvas, 0, (size_t)H * W * 3, ctx->stream));
     PANO_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 2 * (size_t)W, ctx->stream));
-    if (first_xy[0] < 0 || first_xy[1] < 0 || first_xy[0] + w > W || first_xy[1] + h > H)
-        return pano_fail(ctx, PANO_E_ARG, "pano_composite: frame 0 outside canvas");
     dim3 g0((w + 63) / 64, (h + 3) / 4);
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
@@ -352,9 +491,6 @@ int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz,
     int prev_fx = -1;
     for (int i = 1; i < n; ++i) {
         const pano_step &st = steps[i - 1];
-        if (st.frame_x < 0 || st.frame_x + w > W || st.frame_y < 0 || st.frame_y + h > H ||
-            st.canvas_y < 0 || st.canvas_y + st.canvas_h > H)
-            return pano_fail(ctx, PANO_E_ARG, "pano_composite: step outside canvas");
         StepArg s;
         s.fx = st.frame_x;
         s.fy = st.frame_y;
@@ -373,6 +509,91 @@ int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz,
         prev_fx = st.frame_x;
     }
     return PANO_OK;
+}
+
+static int check_geometry(pano_ctx *ctx, int n, int h, int w, const pano_step *steps,
+                          const int32_t *first_xy, int H, int W) {
+    if (first_xy[0] < 0 || first_xy[1] < 0 || first_xy[0] + w > W || first_xy[1] + h > H)
+        return pano_fail(ctx, PANO_E_ARG, "pano_composite: frame 0 outside canvas");
+    for (int i = 1; i < n; ++i) {
+        const pano_step &st = steps[i - 1];
+        if (st.frame_x < 0 || st.frame_x + w > W || st.frame_y < 0 || st.frame_y + h > H ||
+            st.canvas_y < 0 || st.canvas_y + st.canvas_h > H)
+            return pano_fail(ctx, PANO_E_ARG, "pano_composite: step outside canvas");
+    }
+    return PANO_OK;
+}
+
+int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
+                          int h, int w, const pano_step *steps, const int32_t *first_xy,
+                          uint8_t *canvas, int H, int W, int thr, int32_t *bbox) {
+    if (n < 1 || !frames || !colnz || !canvas || !first_xy || (n > 1 && !steps))
+        return pano_fail(ctx, PANO_E_ARG, "pano_composite: bad arguments");
+    int rc = check_geometry(ctx, n, h, w, steps, first_xy, H, W);
+    if (rc) return rc;
+    if (n > kMaxSeq || !bands_independent(steps, first_xy, n, w)) {
+        rc = composite_sequential(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W);
+        if (rc || !bbox) return rc;
+        return launch_gray_bbox(ctx, canvas, H, W, thr, bbox);
+    }
+    SeqArg sa;
+    for (int i = 0; i < n; ++i) {
+        sa.fx[i] = i == 0 ? first_xy[0] : steps[i - 1].frame_x;
+        sa.fy[i] = i == 0 ? first_xy[1] : steps[i - 1].frame_y;
+        sa.is_a[i] = i == 0 ? 0 : (unsigned char)steps[i - 1].frame_is_a;
+        sa.overlap[i] = i == 0 ? 0.0 : steps[i - 1].overlap_range;
+    }
+    const size_t o_mode = 0;
+    const size_t o_w = ((size_t)n * w + 255) & ~size_t(255);
+    const size_t o_own = o_w + (((size_t)n * w * sizeof(float2) + 255) & ~size_t(255));
+    rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, o_own + (size_t)W * sizeof(int32_t));
+    if (rc) return rc;
+    uint8_t *mode = ctx->flags + o_mode;
+    float2 *wgt = (float2 *)(ctx->flags + o_w);
+    int32_t *owner = (int32_t *)(ctx->flags + o_own);
+    if (bbox) {
+        PanoProf prof_(ctx, PK_BBOX);
+        bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
+    }
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_tables<<<n, 256, 0, ctx->stream>>>(colnz, w, sa, mode, wgt);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_tables");
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_owner<<<(W + 255) / 256, 256, 0, ctx->stream>>>(mode, n, w, W, sa, owner);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_owner");
+    dim3 grid((W + 63) / 64, (H + 3) / 4);
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_pixels<<<grid, 256, 0, ctx->stream>>>(frames, h, w, mode, wgt, owner, sa, canvas,
+                                                        H, W, thr, bbox);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_pixels");
+    if (bbox) {
+        PanoProf prof_(ctx, PK_BBOX);
+        bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
+    }
+    return PANO_OK;
+}
+
+int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                     int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
+                     int H, int W) {
+    return launch_composite_bbox(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W, 0,
+                                 nullptr);
+}
+
+int launch_composite_seq(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                         int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
+                         int H, int W) {
+    if (n < 1 || !frames || !colnz || !canvas || !first_xy || (n > 1 && !steps))
+        return pano_fail(ctx, PANO_E_ARG, "pano_composite: bad arguments");
+    int rc = check_geometry(ctx, n, h, w, steps, first_xy, H, W);
+    if (rc) return rc;
+    return composite_sequential(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W);
 }
 
 int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,

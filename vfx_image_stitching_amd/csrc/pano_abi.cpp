@@ -205,6 +205,21 @@ int pano_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, i
     return launch_composite(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W);
 }
 
+int pano_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
+                        int h, int w, const pano_step *steps, const int32_t *first_xy,
+                        uint8_t *canvas, int H, int W, int black_threshold, int32_t *bbox) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_composite_bbox(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W,
+                                 black_threshold, bbox);
+}
+
+int pano_composite_sequential(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
+                              int h, int w, const pano_step *steps, const int32_t *first_xy,
+                              uint8_t *canvas, int H, int W) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_composite_seq(ctx, frames, colnz, n, h, w, steps, first_xy, canvas, H, W);
+}
+
 int pano_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,
                    int wB, const int32_t *geom, double overlap, uint8_t *out) {
     if (!ctx) return PANO_E_ARG;

@@ -36,7 +36,7 @@ struct Cand {
     int32_t octave_field;
     int16_t octave, layer;        // octave index and localised layer
     int32_t frame;
-    uint32_t order;               // scan order: ((octave*8 + layer0) * 2^20 ...) see extrema
+    uint32_t order;               // scan order key (octave*8 + layer0) << 24 | y << 12 | x
 };
 
 // Device-side view of one pyramid level of a frame batch.
@@ -76,7 +76,8 @@ struct pano_ctx {
     RawKp *raw = nullptr;    size_t raw_cap = 0;
     int32_t *counters = nullptr;         // [0]=cands [1]=raw [2..2+n) per-frame raw counts
     size_t counters_n = 0;
-    int32_t *frame_off = nullptr;        // per-frame raw offsets (n+1)
+    int32_t *frame_off = nullptr;        // raw extrema (scan keys) before localisation
+    size_t ext_bytes = 0;
     RawKp *raw_sorted = nullptr;
     double *taps = nullptr;              // device Gaussian taps, per level
     // ---- match / ransac scratch
@@ -155,6 +156,12 @@ int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double th
 int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
                      int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
                      int H, int W);
+int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
+                          int h, int w, const pano_step *steps, const int32_t *first_xy,
+                          uint8_t *canvas, int H, int W, int thr, int32_t *bbox);
+int launch_composite_seq(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                         int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
+                         int H, int W);
 int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,
                      int wB, const int32_t *geom, double overlap, uint8_t *out);
 int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox);

@@ -1,7 +1,8 @@
 // sift_features.hip -- S5..S9 of sift_impl.py on the pyramid built by sift_pyramid.hip.
 //
-//   extrema_localize  find_scale_space_extrema :117-140 + is_pixel_an_extremum :143-163
-//                     + localize_extremum_via_quadratic_fit :169-211 (thread per pixel)
+//   extrema_scan      find_scale_space_extrema :117-140 + is_pixel_an_extremum :143-163
+//                     (LDS-tiled, every octave in one launch)
+//   localize          localize_extremum_via_quadratic_fit :169-211 (thread per candidate)
 //   orientation       compute_keypoints_with_orientations :246-293 (wave per candidate)
 //   sort_dedup        compare_keypoints / remove_duplicate_keypoints :299-327
 //                     + convert_keypoints_to_input_image_size :333-343 (workgroup per frame)
@@ -30,12 +31,6 @@ constexpr double kHistInv = 1.0 / 1099511627776.0;
 constexpr double kDescScale = 1099511627776.0;
 constexpr double kDescInv = 1.0 / 1099511627776.0;
 constexpr int kSortMax = 8192;
-
-struct OctArgs {
-    const float *dog[PANO_MAX_LEVELS];
-    const float *gauss[PANO_MAX_LEVELS];
-    int H, W;
-};
 
 struct PyrArgs {   // all octaves, for the descriptor (level pointers are per frame batch)
     const float *gauss[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
@@ -104,39 +99,90 @@ __device__ void lstsq3_sym(const double A[3][3], const double b[3], double x[3])
     }
 }
 
-__device__ __forceinline__ float dog_at(const OctArgs &a, int lvl, int f, int y, int x) {
-    return a.dog[lvl][((size_t)f * a.H + y) * a.W + x];
+// ------------------------------------------------------------------ S5 + S6
+// S5: one launch covers every octave: workgroup = one 64 x 8 tile of the interior of one
+// octave of one frame; the ni+2 DoG levels of the tile (+1 halo) are staged in LDS and each
+// pixel is checked against its 26 neighbours there (exact f32 comparisons).  Candidates are
+// appended per frame with their scan-order key; S6 runs densely, thread per candidate.
+constexpr int ETX = 64, ETY = 8;
+
+struct DogArgs {
+    const float *dog[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
+    int H[PANO_MAX_OCTAVES], W[PANO_MAX_OCTAVES];
+    int tiles_x[PANO_MAX_OCTAVES];
+    int tile_start[PANO_MAX_OCTAVES + 1];
+    int n_oct;
+};
+
+__device__ __forceinline__ uint32_t scan_key(int o, int layer0, int y, int x) {
+    return ((uint32_t)(o * 8 + layer0) << 24) | ((uint32_t)y << 12) | (uint32_t)x;
 }
 
-// ------------------------------------------------------------------ S5 + S6
 __global__ void __launch_bounds__(256)
-extrema_localize(OctArgs a, LocParams lp, Cand *__restrict__ cands,
-                 int32_t *__restrict__ cand_cnt, int cand_cap) {
-    const int ni = lp.ni, border = lp.border;
-    const int x = border + blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = border + blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int layer0 = 1 + (int)(blockIdx.z % ni);
-    const int f = (int)(blockIdx.z / ni);
-    const int H = a.H, W = a.W;
-    if (x >= W - border || y >= H - border) return;
-    const float v = dog_at(a, layer0, f, y, x);
-    if (!((double)fabsf(v) > lp.thresh)) return;
-    bool ok = true;
-    if (v > 0) {
-        for (int dz = -1; dz <= 1 && ok; ++dz)
-            for (int dy = -1; dy <= 1 && ok; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (!(v >= dog_at(a, layer0 + dz, f, y + dy, x + dx))) { ok = false; break; }
-                }
-    } else {
-        for (int dz = -1; dz <= 1 && ok; ++dz)
-            for (int dy = -1; dy <= 1 && ok; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (!(v <= dog_at(a, layer0 + dz, f, y + dy, x + dx))) { ok = false; break; }
-                }
+extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict__ raw,
+             int32_t *__restrict__ raw_cnt, int raw_cap) {
+    __shared__ float s[PANO_MAX_LEVELS][ETY + 2][ETX + 2];
+    const int f = blockIdx.y;
+    int t = blockIdx.x, o = 0;
+    while (o + 1 < a.n_oct && t >= a.tile_start[o + 1]) ++o;
+    t -= a.tile_start[o];
+    const int H = a.H[o], W = a.W[o];
+    const int x0 = border + (t % a.tiles_x[o]) * ETX;
+    const int y0 = border + (t / a.tiles_x[o]) * ETY;
+    const int tid = threadIdx.x;
+    const int nl = ni + 2;
+    for (int i = tid; i < nl * (ETY + 2) * (ETX + 2); i += 256) {
+        const int l = i / ((ETY + 2) * (ETX + 2));
+        const int rem = i - l * (ETY + 2) * (ETX + 2);
+        const int yy = rem / (ETX + 2), xx = rem - yy * (ETX + 2);
+        const int gy = min(y0 - 1 + yy, H - 1), gx = min(x0 - 1 + xx, W - 1);
+        s[l][yy][xx] = a.dog[o][l][((size_t)f * H + gy) * W + gx];
     }
-    if (!ok) return;
+    __syncthreads();
+    for (int q = tid; q < ETX * ETY; q += 256) {
+        const int px = q % ETX, py = q / ETX;
+        const int x = x0 + px, y = y0 + py;
+        if (x >= W - border || y >= H - border) continue;
+        for (int L = 1; L <= ni; ++L) {
+            const float v = s[L][py + 1][px + 1];
+            if (!((double)fabsf(v) > thresh)) continue;
+            bool ge = true, le = true;
+#pragma unroll
+            for (int dz = -1; dz <= 1; ++dz)
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const float nb = s[L + dz][py + 1 + dy][px + 1 + dx];
+                        ge = ge && (v >= nb);
+                        le = le && (v <= nb);
+                    }
+            if (v > 0 ? ge : le) {
+                const int slot = atomicAdd(&raw_cnt[f], 1);
+                if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = scan_key(o, L, y, x);
+            }
+        }
+    }
+}
 
+__device__ __forceinline__ float dog_at(const DogArgs &a, int o, int lvl, int f, int y, int x) {
+    return a.dog[o][lvl][((size_t)f * a.H[o] + y) * a.W[o] + x];
+}
+
+__global__ void __launch_bounds__(256)
+localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
+         const int32_t *__restrict__ raw_cnt, int raw_cap, Cand *__restrict__ cands,
+         int32_t *__restrict__ cand_cnt, int cand_cap) {
+    const int f = blockIdx.y;
+    const int ci = blockIdx.x * 256 + threadIdx.x;
+    int cnt = raw_cnt[f];
+    cnt = cnt < raw_cap ? cnt : raw_cap;
+    if (ci >= cnt) return;
+    const uint32_t key = raw[(size_t)f * raw_cap + ci];
+    const int o = (int)(key >> 24) / 8, layer0 = (int)(key >> 24) % 8;
+    const int y = (int)((key >> 12) & 4095), x = (int)(key & 4095);
+    const int ni = lp.ni, border = lp.border;
+    const int H = a.H[o], W = a.W[o];
     // ---- quadratic fit (sift_impl.py:169-211), keeping the max_iter quirk
     int xi = x, yi = y, li = layer0;
     float c[3][3][3];
@@ -145,7 +191,7 @@ extrema_localize(OctArgs a, LocParams lp, Cand *__restrict__ cands,
         for (int dz = 0; dz < 3; ++dz)
             for (int dy = 0; dy < 3; ++dy)
                 for (int dx = 0; dx < 3; ++dx)
-                    c[dz][dy][dx] = dog_at(a, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx) / 255.0f;
+                    c[dz][dy][dx] = dog_at(a, o, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx) / 255.0f;
         const float cv = c[1][1][1];
         g[0] = 0.5f * (c[1][1][2] - c[1][1][0]);
         g[1] = 0.5f * (c[1][2][1] - c[1][0][1]);
@@ -183,8 +229,6 @@ extrema_localize(OctArgs a, LocParams lp, Cand *__restrict__ cands,
     const float det = (float)((double)Hs[0][0] * (double)Hs[1][1] -
                               (double)Hs[0][1] * (double)Hs[1][0]);
     if (det <= 0.0f || lp.edge_lhs * (tr * tr) >= lp.edge_rhs * det) return;
-
-    const int o = lp.octave;
     const float so = (float)(1 << o);
     Cand k;
     k.x = ((float)xi + u[0]) * so;
@@ -197,7 +241,7 @@ extrema_localize(OctArgs a, LocParams lp, Cand *__restrict__ cands,
     k.octave = (int16_t)o;
     k.layer = (int16_t)li;
     k.frame = f;
-    k.order = ((uint32_t)(o * 8 + layer0) << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    k.order = key;
     const int slot = atomicAdd(&cand_cnt[f], 1);
     if (slot < cand_cap) cands[(size_t)f * cand_cap + slot] = k;
 }
@@ -543,12 +587,17 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     if (rc) return rc;
     rc = pano_grow(ctx, (void **)&ctx->raw, &ctx->raw_cap, raw_cap * n * sizeof(RawKp));
     if (rc) return rc;
-    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, (2 * (size_t)n + 8) * sizeof(int32_t));
+    const size_t ext_cap = 4 * (size_t)kSortMax;
+    rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint32_t));
+    if (rc) return rc;
+    uint32_t *raw_ext = (uint32_t *)ctx->frame_off;
+    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, (3 * (size_t)n + 8) * sizeof(int32_t));
     if (rc) return rc;
     int32_t *cand_cnt = ctx->counters;
     int32_t *raw_cnt = ctx->counters + n;
     int32_t *err = ctx->counters + 2 * n;
-    PANO_HIP(ctx, hipMemsetAsync(ctx->counters, 0, (2 * (size_t)n + 8) * sizeof(int32_t), ctx->stream));
+    int32_t *ext_cnt = ctx->counters + 2 * n + 8;
+    PANO_HIP(ctx, hipMemsetAsync(ctx->counters, 0, (3 * (size_t)n + 8) * sizeof(int32_t), ctx->stream));
 
     LocParams lp;
     lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);
@@ -559,21 +608,37 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     lp.ni = ni;
     lp.border = p->border;
     lp.max_iter = p->max_iter;
+    lp.octave = 0;
+    DogArgs da{};
+    int tiles = 0;
+    da.n_oct = no;
     for (int o = 0; o < no; ++o) {
-        OctArgs a{};
-        a.H = ctx->oct_h[o];
-        a.W = ctx->oct_w[o];
-        for (int l = 0; l < nl; ++l) a.gauss[l] = ctx->pyr + ctx->gauss_off[o][l];
-        for (int l = 0; l < nl - 1; ++l) a.dog[l] = ctx->dog + ctx->dog_off[o][l];
-        const int iw = a.W - 2 * p->border, ih = a.H - 2 * p->border;
-        if (iw <= 0 || ih <= 0) continue;
-        lp.octave = o;
-        dim3 grid((iw + 63) / 64, (ih + 3) / 4, n * ni);
+        da.H[o] = ctx->oct_h[o];
+        da.W[o] = ctx->oct_w[o];
+        for (int l = 0; l < nl - 1; ++l) da.dog[o][l] = ctx->dog + ctx->dog_off[o][l];
+        const int iw = da.W[o] - 2 * p->border, ih = da.H[o] - 2 * p->border;
+        da.tile_start[o] = tiles;
+        da.tiles_x[o] = iw > 0 ? (iw + ETX - 1) / ETX : 1;
+        if (iw > 0 && ih > 0) tiles += da.tiles_x[o] * ((ih + ETY - 1) / ETY);
+    }
+    da.tile_start[no] = tiles;
+    if (ctx->h * 2 > 4095 || ctx->w * 2 > 4095)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "frames above 2047 px need a wider scan key");
+    if (tiles > 0) {
+        dim3 grid(tiles, n);
         {
             PanoProf prof_(ctx, PK_EXTREMA);
-            extrema_localize<<<grid, 256, 0, ctx->stream>>>(a, lp, ctx->cands, cand_cnt, (int)cand_cap);
+            extrema_scan<<<grid, 256, 0, ctx->stream>>>(da, ni, p->border, lp.thresh, raw_ext,
+                                                        ext_cnt, (int)ext_cap);
         }
-        PANO_LAUNCH_CHECK(ctx, "extrema_localize");
+        PANO_LAUNCH_CHECK(ctx, "extrema_scan");
+        dim3 g2((unsigned)((ext_cap + 255) / 256), n);
+        {
+            PanoProf prof_(ctx, PK_EXTREMA);
+            localize<<<g2, 256, 0, ctx->stream>>>(da, lp, raw_ext, ext_cnt, (int)ext_cap, ctx->cands,
+                                                  cand_cnt, (int)cand_cap);
+        }
+        PANO_LAUNCH_CHECK(ctx, "localize");
     }
     PyrArgs pa{};
     pa.n_oct = no;

@@ -76,47 +76,102 @@ __device__ __forceinline__ float load_px(const LoadArgs &a, int f, int y, int x,
     }
 }
 
-template <int MODE>
+// Register-blocked sliding window: SEG consecutive outputs of one row (or column) from
+// SEG + NT - 1 staged inputs; output j receives taps t = 0..NT-1 in order (the oracle's
+// sequential sum), all index arithmetic compile-time after unrolling.
+template <int NT, int SEG>
+__device__ __forceinline__ void conv_seg(const float *__restrict__ p, int stride,
+                                         const double *__restrict__ k, double (&acc)[SEG]) {
+#pragma unroll
+    for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < SEG + NT - 1; ++i) {
+        const double v = (double)p[i * stride];
+#pragma unroll
+        for (int j = 0; j < SEG; ++j) {
+            const int t = i - j;
+            if (t >= 0 && t < NT) acc[j] = fma(k[t], v, acc[j]);
+        }
+    }
+}
+
+// Runtime tap count fallback (sigma values other than the reference defaults).
+__device__ __forceinline__ double conv_one(const float *__restrict__ p, int stride,
+                                           const double *__restrict__ k, int n) {
+    double acc = 0.0;
+    for (int t = 0; t < n; ++t) acc = fma(k[t], (double)p[t * stride], acc);
+    return acc;
+}
+
+constexpr int SEG = 16;
+
+template <int MODE, int NT>
 __global__ void __launch_bounds__(256)
 blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
            float *__restrict__ in_copy, int H, int W, Taps taps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int r = (taps.n - 1) / 2;
-    const int IW = TX + 2 * r;     // staged input tile width
-    const int IH = TY + 2 * r;
-    float *tin = smem;              // [IH][IW]
-    float *trow = smem + IH * IW;   // [IH][TX]
+    const int n = NT > 0 ? NT : taps.n;
+    const int r = (n - 1) / 2;
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY, f = blockIdx.z;
+    const int tw = min(TX, W - x0), th = min(TY, H - y0);   // valid outputs of this tile
+    const int IW = TX + 2 * r, IH = TY + 2 * r;
+    const int IWP = IW | 1;                                  // odd row pitch: no bank conflicts
+    float *tin = smem;                 // [IH][IWP]
+    float *trow = smem + IH * IWP;     // [IH][TX]
     const int tid = threadIdx.x;
+    const int ih = th + 2 * r, iw = tw + 2 * r;              // staged extent actually needed
 
-    for (int i = tid; i < IH * IW; i += 256) {
-        const int ty = i / IW, tx = i - ty * IW;
+    for (int i = tid; i < ih * iw; i += 256) {
+        const int ty = i / iw, tx = i - ty * iw;
         const int gy = reflect101(y0 - r + ty, H);
         const int gx = reflect101(x0 - r + tx, W);
-        tin[i] = load_px<MODE>(la, f, gy, gx, H, W);
+        tin[ty * IWP + tx] = load_px<MODE>(la, f, gy, gx, H, W);
     }
     __syncthreads();
-    for (int i = tid; i < IH * TX; i += 256) {
-        const int ty = i / TX, tx = i - ty * TX;
-        const float *p = tin + ty * IW + tx;
-        double acc = 0.0;
-        for (int k = 0; k < taps.n; ++k) acc = fma(taps.k[k], (double)p[k], acc);
-        trow[i] = (float)acc;
-    }
-    __syncthreads();
-    for (int i = tid; i < TY * TX; i += 256) {
-        const int ty = i / TX, tx = i - ty * TX;
-        const int gy = y0 + ty, gx = x0 + tx;
-        if (gy >= H || gx >= W) continue;
-        const float *p = trow + ty * TX + tx;
-        double acc = 0.0;
-        for (int k = 0; k < taps.n; ++k) acc = fma(taps.k[k], (double)p[k * TX], acc);
-        const float o = (float)acc;
-        const size_t gi = ((size_t)f * H + gy) * W + gx;
-        out[gi] = o;
-        const float c = tin[(ty + r) * IW + tx + r];
-        if (dog) dog[gi] = o - c;
-        if (in_copy) in_copy[gi] = c;
+    if constexpr (NT > 0) {
+        // row pass: lanes walk consecutive rows (odd pitch), each SEG outputs along x
+        const int nseg = (tw + SEG - 1) / SEG;
+        for (int it = tid; it < ih * nseg; it += 256) {
+            const int row = it % ih, sg = it / ih;
+            double acc[SEG];
+            conv_seg<NT, SEG>(tin + row * IWP + sg * SEG, 1, taps.k, acc);
+#pragma unroll
+            for (int j = 0; j < SEG; ++j) trow[row * TX + sg * SEG + j] = (float)acc[j];
+        }
+        __syncthreads();
+        // column pass: lanes walk consecutive columns, each SEG outputs down y
+        const int nrs = (th + SEG - 1) / SEG;
+        for (int it = tid; it < tw * nrs; it += 256) {
+            const int x = it % tw, rs = it / tw;
+            double acc[SEG];
+            conv_seg<NT, SEG>(trow + rs * SEG * TX + x, TX, taps.k, acc);
+#pragma unroll
+            for (int j = 0; j < SEG; ++j) {
+                const int ty = rs * SEG + j;
+                if (ty >= th) break;
+                const float o = (float)acc[j];
+                const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + x;
+                out[gi] = o;
+                const float c = tin[(ty + r) * IWP + x + r];
+                if (dog) dog[gi] = o - c;
+                if (in_copy) in_copy[gi] = c;
+            }
+        }
+    } else {
+        for (int i = tid; i < ih * tw; i += 256) {
+            const int ty = i / tw, tx = i - ty * tw;
+            trow[ty * TX + tx] = (float)conv_one(tin + ty * IWP + tx, 1, taps.k, n);
+        }
+        __syncthreads();
+        for (int i = tid; i < th * tw; i += 256) {
+            const int ty = i / tw, tx = i - ty * tw;
+            const float o = (float)conv_one(trow + ty * TX + tx, TX, taps.k, n);
+            const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + tx;
+            out[gi] = o;
+            const float c = tin[(ty + r) * IWP + tx + r];
+            if (dog) dog[gi] = o - c;
+            if (in_copy) in_copy[gi] = c;
+        }
     }
 }
 
@@ -142,23 +197,37 @@ Taps make_taps(double sigma) {
 
 size_t smem_bytes(const Taps &t) {
     const int r = (t.n - 1) / 2;
-    return (size_t)((TY + 2 * r) * (TX + 2 * r) + (TY + 2 * r) * TX) * sizeof(float);
+    // trow rows are read up to SEG past the valid extent by the column pass: pad them
+    return (size_t)((TY + 2 * r) * ((TX + 2 * r) | 1) + (TY + 2 * r + SEG) * TX) * sizeof(float);
+}
+
+template <int MODE, int NT>
+int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float *in_copy,
+                   int n, int H, int W, const Taps &t) {
+    dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
+    const size_t sm = smem_bytes(t);
+    if (sm > 65536)
+        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_level<MODE, NT>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+    {
+        PanoProf prof_(ctx, PK_BLUR);
+        blur_level<MODE, NT><<<grid, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+    }
+    PANO_LAUNCH_CHECK(ctx, "blur_level");
+    return PANO_OK;
 }
 
 template <int MODE>
 int launch_blur(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float *in_copy, int n,
                 int H, int W, const Taps &t) {
-    dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
-    const size_t sm = smem_bytes(t);
-    if (sm > 65536)
-        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_level<MODE>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    {
-        PanoProf prof_(ctx, PK_BLUR);
-        blur_level<MODE><<<grid, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+    switch (t.n) {   // the reference's kernel sizes: 11 (base), 11/13/17/21/27 (levels)
+        case 11: return launch_blur_nt<MODE, 11>(ctx, la, out, dog, in_copy, n, H, W, t);
+        case 13: return launch_blur_nt<MODE, 13>(ctx, la, out, dog, in_copy, n, H, W, t);
+        case 17: return launch_blur_nt<MODE, 17>(ctx, la, out, dog, in_copy, n, H, W, t);
+        case 21: return launch_blur_nt<MODE, 21>(ctx, la, out, dog, in_copy, n, H, W, t);
+        case 27: return launch_blur_nt<MODE, 27>(ctx, la, out, dog, in_copy, n, H, W, t);
+        default: return launch_blur_nt<MODE, 0>(ctx, la, out, dog, in_copy, n, H, W, t);
     }
-    PANO_LAUNCH_CHECK(ctx, "blur_level");
-    return PANO_OK;
 }
 
 }  // namespace

@@ -13,8 +13,8 @@ Here every stage runs as libpano kernels over the whole frame batch, on one HIP 
     pano_match         all pairs (fp32 MFMA distance GEMM for SIFT)
     pano_pair_shifts   all pairs (match filter + exhaustive vote RANSAC)
       -- host: 17 records come back (~1 KB); drift correction + composite plan (C) --
-    pano_composite     pre-sized canvas, one launch per step over the new frame's columns
-    pano_gray_bbox     crop box (16 bytes come back)
+    pano_composite_bbox  pre-sized canvas; one parallel pass when no column is covered by
+                       three frames (else the per-step fold), crop box fused (16 B back)
 
 Two small device->host reads are the only synchronisation points.
 """
@@ -134,8 +134,7 @@ class Stitcher:
                                                      ptr(recs)))
         return recs, (best, d1, d2)
 
-    def composite(self, cyl, colnz, shifts_corr, pairs_xy):
-        n, h, w, _ = cyl.shape
+    def plan(self, n, h, w, shifts_corr, pairs_xy):
         sh = np.ascontiguousarray(np.array(shifts_corr, np.float64).reshape(-1, 2))
         pr = np.ascontiguousarray(np.array(pairs_xy, np.float64).reshape(-1, 4))
         steps = (_lib.Step * max(n - 1, 1))()
@@ -145,11 +144,23 @@ class Stitcher:
                                               _lib.i32p(first), _lib.i32p(hw))
         if rc:
             raise PanoError(rc, "pano_plan_composite")
-        H, W = int(hw[0]), int(hw[1])
+        return steps, first, (int(hw[0]), int(hw[1]))
+
+    def composite(self, cyl, colnz, shifts_corr, pairs_xy, bbox=False, sequential=False):
+        """The mosaic loop on a pre-sized canvas; optionally the crop bbox in the same pass."""
+        n, h, w, _ = cyl.shape
+        steps, first, (H, W) = self.plan(n, h, w, shifts_corr, pairs_xy)
         canvas = self._get("canvas", (H, W, 3), self.torch.uint8)
-        self.ctx.check(self.ctx.lib.pano_composite(self.ctx.h, ptr(cyl), ptr(colnz), n, h, w, steps,
-                                                   _lib.i32p(first), ptr(canvas), H, W))
-        return canvas
+        lib, c = self.ctx.lib, self.ctx.h
+        if sequential:
+            self.ctx.check(lib.pano_composite_sequential(c, ptr(cyl), ptr(colnz), n, h, w, steps,
+                                                         _lib.i32p(first), ptr(canvas), H, W))
+            return canvas
+        bb = self._get("bbox", (4,), self.torch.int32) if bbox else None
+        self.ctx.check(lib.pano_composite_bbox(c, ptr(cyl), ptr(colnz), n, h, w, steps,
+                                               _lib.i32p(first), ptr(canvas), H, W, 0,
+                                               ptr(bb) if bbox else None))
+        return (canvas, bb) if bbox else canvas
 
     def bbox(self, img, thr=0):
         H, W, _ = img.shape
@@ -186,8 +197,8 @@ class Stitcher:
                 best_pairs.append(((int(r["xA"]), int(r["yA"])), (int(r["xB"]), int(r["yB"]))))
         corr = drift_correct(shifts)
         pxy = [(a[0], a[1], b[0], b[1]) for a, b in best_pairs]
-        canvas = self.composite(cyl, colnz, corr, pxy)
-        bb = self.bbox(canvas).cpu().numpy()                             # sync point 2
+        canvas, bb_dev = self.composite(cyl, colnz, corr, pxy, bbox=True)
+        bb = bb_dev.cpu().numpy()                                        # sync point 2
         H = canvas.shape[0]
         if bb[1] < 0:
             y0, y1, x0, x1 = 0, H - 1, 0, canvas.shape[1] - 1
