@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=4)
+    ap.add_argument("--match", default=None, choices=["f32", "bf16"])
     return ap.parse_args()
 
 
@@ -115,7 +116,7 @@ def main():
     frames, focals, margin, (h, w), distinct = workload(args.workload, rank, world)
     n_local = len(frames)
     cap = 4096 if args.workload != "synthetic" else 8192
-    st = Stitcher(args.method, cap=cap)
+    st = Stitcher(args.method, cap=cap, match=args.match)
     dev = st.upload(frames)                                   # resident in HBM
     counts = [c for _, c in D.shard_ranges(distinct - 1, world)] if args.workload == "synthetic" \
         else [n_local - 1] * world
@@ -204,7 +205,7 @@ def main():
         "config": {"workload": f"{args.workload} {args.method} end-to-end: {distinct} frames "
                                f"{h}x{w}, {distinct - 1} pairs, {world} rank(s) x {n_local} frames",
                    "frames": distinct, "frame_hw": [h, w], "parallelism": f"pairs sharded x{world}",
-                   "method": args.method},
+                   "method": args.method, "match_gemm": st.match},
         "roofline": roof,
         "cpu_baseline": cpu,
         "kernels_ms_per_step": {k: round(v["total_ms"], 4) for k, v in per_kernel.items()},

@@ -188,51 +188,53 @@ __global__ void composite_owner(const uint8_t *__restrict__ mode, int n, int w, 
     owner[X] = o;
 }
 
+__device__ __forceinline__ void composite_px(const uint8_t *__restrict__ frames, int h, int w,
+                                             const uint8_t *__restrict__ mode,
+                                             const float2 *__restrict__ wgt, int i, const SeqArg &sa,
+                                             int X, int y, uint8_t o[3]) {
+    o[0] = o[1] = o[2] = 0;
+    if (i < 0) return;
+    const int c = X - sa.fx[i];
+    const int fyl = y - sa.fy[i];
+    uint8_t F[3] = {0, 0, 0};
+    if (fyl >= 0 && fyl < h) {
+        const uint8_t *p = frames + (((size_t)i * h + fyl) * w + c) * 3;
+        F[0] = p[0]; F[1] = p[1]; F[2] = p[2];
+    }
+    if (mode[(size_t)i * w + c] != 2) {
+        o[0] = F[0]; o[1] = F[1]; o[2] = F[2];
+        return;
+    }
+    uint8_t M[3] = {0, 0, 0};
+    const int cm = X - sa.fx[i - 1], ym = y - sa.fy[i - 1];
+    if (cm >= 0 && cm < w && ym >= 0 && ym < h) {
+        const uint8_t *q = frames + (((size_t)(i - 1) * h + ym) * w + cm) * 3;
+        M[0] = q[0]; M[1] = q[1]; M[2] = q[2];
+    }
+    const float2 ab = wgt[(size_t)i * w + c];
+    for (int k = 0; k < 3; ++k)
+        o[k] = sa.is_a[i] ? blend_px(ab.x, ab.y, F[k], M[k]) : blend_px(ab.x, ab.y, M[k], F[k]);
+}
+
+// grid-stride over the canvas with a bounded grid: one bbox atomic per workgroup
 __global__ void __launch_bounds__(256)
 composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const uint8_t *__restrict__ mode,
                  const float2 *__restrict__ wgt, const int32_t *__restrict__ owner, SeqArg sa,
                  uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox) {
     __shared__ int r[4][256];
     const int tid = threadIdx.x;
-    const int X = blockIdx.x * 64 + (tid & 63);
-    const int y = blockIdx.y * 4 + (tid >> 6);
     int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
-    if (X < W && y < H) {
-        const int i = owner[X];
-        uint8_t o0 = 0, o1 = 0, o2 = 0;
-        if (i >= 0) {
-            const int c = X - sa.fx[i];
-            const int fyl = y - sa.fy[i];
-            uint8_t F[3] = {0, 0, 0};
-            if (fyl >= 0 && fyl < h) {
-                const uint8_t *p = frames + (((size_t)i * h + fyl) * w + c) * 3;
-                F[0] = p[0]; F[1] = p[1]; F[2] = p[2];
-            }
-            if (mode[(size_t)i * w + c] == 2) {
-                uint8_t M[3] = {0, 0, 0};
-                const int cm = X - sa.fx[i - 1], ym = y - sa.fy[i - 1];
-                if (cm >= 0 && cm < w && ym >= 0 && ym < h) {
-                    const uint8_t *q = frames + (((size_t)(i - 1) * h + ym) * w + cm) * 3;
-                    M[0] = q[0]; M[1] = q[1]; M[2] = q[2];
-                }
-                const float2 ab = wgt[(size_t)i * w + c];
-                if (sa.is_a[i]) {
-                    o0 = blend_px(ab.x, ab.y, F[0], M[0]);
-                    o1 = blend_px(ab.x, ab.y, F[1], M[1]);
-                    o2 = blend_px(ab.x, ab.y, F[2], M[2]);
-                } else {
-                    o0 = blend_px(ab.x, ab.y, M[0], F[0]);
-                    o1 = blend_px(ab.x, ab.y, M[1], F[1]);
-                    o2 = blend_px(ab.x, ab.y, M[2], F[2]);
-                }
-            } else {
-                o0 = F[0]; o1 = F[1]; o2 = F[2];
-            }
+    const size_t total = (size_t)H * W;
+    for (size_t e = (size_t)blockIdx.x * 256 + tid; e < total; e += (size_t)gridDim.x * 256) {
+        const int y = (int)(e / W), X = (int)(e - (size_t)y * W);
+        uint8_t o[3];
+        composite_px(frames, h, w, mode, wgt, owner[X], sa, X, y, o);
+        uint8_t *d = canvas + e * 3;
+        d[0] = o[0]; d[1] = o[1]; d[2] = o[2];
+        if (bbox && gray_u8(o) > thr) {
+            ymin = min(ymin, y); ymax = max(ymax, y);
+            xmin = min(xmin, X); xmax = max(xmax, X);
         }
-        uint8_t *d = canvas + ((size_t)y * W + X) * 3;
-        d[0] = o0; d[1] = o1; d[2] = o2;
-        const uint8_t px[3] = {o0, o1, o2};
-        if (bbox && gray_u8(px) > thr) { ymin = ymax = y; xmin = xmax = X; }
     }
     if (!bbox) return;
     r[0][tid] = ymin; r[1][tid] = ymax; r[2][tid] = xmin; r[3][tid] = xmax;
@@ -565,10 +567,11 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
         composite_owner<<<(W + 255) / 256, 256, 0, ctx->stream>>>(mode, n, w, W, sa, owner);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_owner");
-    dim3 grid((W + 63) / 64, (H + 3) / 4);
+    unsigned nb = (unsigned)(((size_t)H * W + 255) / 256);
+    nb = nb < 1024 ? nb : 1024;
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_pixels<<<grid, 256, 0, ctx->stream>>>(frames, h, w, mode, wgt, owner, sa, canvas,
+        composite_pixels<<<nb, 256, 0, ctx->stream>>>(frames, h, w, mode, wgt, owner, sa, canvas,
                                                         H, W, thr, bbox);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_pixels");

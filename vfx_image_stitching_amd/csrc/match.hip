@@ -53,12 +53,27 @@ struct PairArg {
     int32_t a[256], b[256];
 };
 
+// Operand roles: C[j][i] = sum_k B[j][k] A[i][k], so in the 32 x 32 C layout (col = lane & 31,
+// row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)) a lane owns ONE query row i and 16 candidate
+// rows j: the argmin over j is a register fold, one lane^32 shuffle and one LDS merge of the
+// two j-waves.  ELEM_BF16: the descriptors are staged as bf16 (exact for integers 0..255)
+// and multiplied with v_mfma_f32_32x32x16_bf16 (K = 16 per issue, f32 accumulation exact
+// below 2^24); otherwise v_mfma_f32_32x32x2_f32 in 4 K-chunks of 32.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int KP_BF = PANO_DESC_DIM + 8;   // bf16 row pitch (272 B): conflict-free b128 reads
+
+__device__ __forceinline__ unsigned short f32_to_bf16_exact(float v) {
+    return (unsigned short)(__float_as_uint(v) >> 16);   // exact for integers 0..255
+}
+
+template <bool BF16>
 __global__ void __launch_bounds__(256)
 dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
           const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
           int n_jt) {
-    __shared__ float As[MT * LDA];
-    __shared__ float Bs[MT * LDA];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ float nA[MT], nB[MT];
     __shared__ Part red[2][MT];
     const int p = blockIdx.z;
     const int fa = pairs.a[p], fb = pairs.b[p];
@@ -70,72 +85,103 @@ dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
     const float *dA = desc + (size_t)fa * cap * PANO_DESC_DIM;
     const float *dB = desc + (size_t)fb * cap * PANO_DESC_DIM;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wr = wv >> 1, wc = wv & 1;
-    f32x16 acc[2][2];
+    const int wj = wv >> 1, wi = wv & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    if (tid < MT) nA[tid] = i0 + tid < NA ? norms[(size_t)fa * cap + i0 + tid] : 0.0f;
+    else nB[tid - MT] = j0 + tid - MT < NB ? norms[(size_t)fb * cap + j0 + tid - MT] : 0.0f;
+    f32x16 acc[2][2];   // [j block][i block]
     for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b)
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
-    for (int k0 = 0; k0 < PANO_DESC_DIM; k0 += KC) {
-        // 128 rows x 32 floats per operand = 1024 float4, 4 per thread
-        for (int q = tid; q < MT * KC / 4; q += 256) {
-            const int row = q / (KC / 4), c4 = (q % (KC / 4)) * 4;
+    if constexpr (BF16) {
+        unsigned short *Ab = (unsigned short *)smem;          // [MT][KP_BF]
+        unsigned short *Bb = Ab + MT * KP_BF;                  // [MT][KP_BF]
+        for (int q = tid; q < MT * PANO_DESC_DIM / 4; q += 256) {
+            const int row = q / (PANO_DESC_DIM / 4), c4 = (q % (PANO_DESC_DIM / 4)) * 4;
             float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-            if (i0 + row < NA) va = *(const float4 *)(dA + (size_t)(i0 + row) * PANO_DESC_DIM + k0 + c4);
-            if (j0 + row < NB) vb = *(const float4 *)(dB + (size_t)(j0 + row) * PANO_DESC_DIM + k0 + c4);
-            float *pa = As + row * LDA + c4;
-            float *pb = Bs + row * LDA + c4;
-            pa[0] = va.x; pa[1] = va.y; pa[2] = va.z; pa[3] = va.w;
-            pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
+            if (i0 + row < NA) va = *(const float4 *)(dA + (size_t)(i0 + row) * PANO_DESC_DIM + c4);
+            if (j0 + row < NB) vb = *(const float4 *)(dB + (size_t)(j0 + row) * PANO_DESC_DIM + c4);
+            ushort4 ua = make_ushort4(f32_to_bf16_exact(va.x), f32_to_bf16_exact(va.y),
+                                      f32_to_bf16_exact(va.z), f32_to_bf16_exact(va.w));
+            ushort4 ub = make_ushort4(f32_to_bf16_exact(vb.x), f32_to_bf16_exact(vb.y),
+                                      f32_to_bf16_exact(vb.z), f32_to_bf16_exact(vb.w));
+            *(ushort4 *)(Ab + row * KP_BF + c4) = ua;
+            *(ushort4 *)(Bb + row * KP_BF + c4) = ub;
         }
         __syncthreads();
-        const int lr = lane & 31, lk = lane >> 5;
-#pragma unroll 4
-        for (int kk = 0; kk < KC; kk += 2) {
-            float av[2], bv[2];
-            for (int m = 0; m < 2; ++m) av[m] = As[(wr * 64 + m * 32 + lr) * LDA + kk + lk];
-            for (int m = 0; m < 2; ++m) bv[m] = Bs[(wc * 64 + m * 32 + lr) * LDA + kk + lk];
+#pragma unroll
+        for (int kk = 0; kk < PANO_DESC_DIM; kk += 16) {
+            bf16x8 fj[2], fi[2];
+            for (int m = 0; m < 2; ++m) {
+                fj[m] = *(const bf16x8 *)(Bb + (wj * 64 + m * 32 + lr) * KP_BF + kk + 8 * lh);
+                fi[m] = *(const bf16x8 *)(Ab + (wi * 64 + m * 32 + lr) * KP_BF + kk + 8 * lh);
+            }
             for (int a = 0; a < 2; ++a)
                 for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a], fi[b], acc[a][b], 0, 0, 0);
         }
-        __syncthreads();
+    } else {
+        float *As = (float *)smem;          // [MT][LDA]
+        float *Bs = As + MT * LDA;          // [MT][LDA]
+        for (int k0 = 0; k0 < PANO_DESC_DIM; k0 += KC) {
+            for (int q = tid; q < MT * KC / 4; q += 256) {
+                const int row = q / (KC / 4), c4 = (q % (KC / 4)) * 4;
+                float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+                if (i0 + row < NA) va = *(const float4 *)(dA + (size_t)(i0 + row) * PANO_DESC_DIM + k0 + c4);
+                if (j0 + row < NB) vb = *(const float4 *)(dB + (size_t)(j0 + row) * PANO_DESC_DIM + k0 + c4);
+                float *pa = As + row * LDA + c4;
+                float *pb = Bs + row * LDA + c4;
+                pa[0] = va.x; pa[1] = va.y; pa[2] = va.z; pa[3] = va.w;
+                pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int kk = 0; kk < KC; kk += 2) {
+                float fj[2], fi[2];
+                for (int m = 0; m < 2; ++m) {
+                    fj[m] = Bs[(wj * 64 + m * 32 + lr) * LDA + kk + lh];
+                    fi[m] = As[(wi * 64 + m * 32 + lr) * LDA + kk + lh];
+                }
+                for (int a = 0; a < 2; ++a)
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fj[a], fi[b], acc[a][b], 0, 0, 0);
+            }
+            __syncthreads();
+        }
     }
-    // epilogue: lane holds rows (reg&3) + 8*(reg>>2) + 4*(lane>>5), column lane&31
-    const int hcol = lane & 31, hrow = 4 * (lane >> 5);
-    for (int a = 0; a < 2; ++a) {
-        for (int r = 0; r < 16; ++r) {
-            const int row = wr * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + hrow;
-            const int gi = i0 + row;
-            const float na = gi < NA ? norms[(size_t)fa * cap + gi] : 0.0f;
-            float best = INFINITY, second = INFINITY;
-            int bj = 0x7fffffff;
-            for (int b = 0; b < 2; ++b) {
-                const int gj = j0 + wc * 64 + b * 32 + hcol;
-                if (gj < NB) {
-                    const float d = (na + norms[(size_t)fb * cap + gj]) - 2.0f * acc[a][b][r];
-                    merge(best, bj, second, d, gj, INFINITY);
+    __syncthreads();
+    // epilogue: per i (= lane & 31 of i block b), fold the wave's 64 j values
+    for (int b = 0; b < 2; ++b) {
+        const int il = wi * 64 + b * 32 + lr;          // tile-local i
+        const float na = nA[il];
+        float best = INFINITY, second = INFINITY;
+        int bj = 0x7fffffff;
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int jl = wj * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (j0 + jl < NB) {
+                    const float d = (na + nB[jl]) - 2.0f * acc[a][b][r];
+                    merge(best, bj, second, d, j0 + jl, INFINITY);
                 }
             }
-            // butterfly over the 32 lanes that share this row
-            for (int off = 1; off < 32; off <<= 1) {
-                const float ob = __shfl_xor(best, off);
-                const int oj = __shfl_xor(bj, off);
-                const float os = __shfl_xor(second, off);
-                merge(best, bj, second, ob, oj, os);
-            }
-            if (hcol == 0) red[wc][row] = Part{best, bj, second};
         }
+        const float ob = __shfl_xor(best, 32);
+        const int oj = __shfl_xor(bj, 32);
+        const float os = __shfl_xor(second, 32);
+        merge(best, bj, second, ob, oj, os);
+        if (lh == 0) red[wj][il] = Part{best, bj, second};
     }
     __syncthreads();
     if (tid < MT) {
         Part x = red[0][tid];
         const Part y = red[1][tid];
-        float b = x.best, s = x.second;
-        int j = x.idx;
-        merge(b, j, s, y.best, y.idx, y.second);
+        float bb = x.best, ss = x.second;
+        int jj = x.idx;
+        merge(bb, jj, ss, y.best, y.idx, y.second);
         const int gi = i0 + tid;
-        if (gi < NA) parts[((size_t)p * n_jt + blockIdx.x) * cap + gi] = Part{b, j, s};
+        if (gi < NA) parts[((size_t)p * n_jt + blockIdx.x) * cap + gi] = Part{bb, jj, ss};
     }
 }
 
@@ -234,6 +280,13 @@ dist_direct(const float *__restrict__ desc, const int32_t *__restrict__ counts, 
 
 }  // namespace
 
+int match_set_attributes(pano_ctx *ctx) {
+    const int sm = 2 * MT * KP_BF * (int)sizeof(unsigned short);
+    PANO_HIP(ctx, hipFuncSetAttribute((const void *)dist_mfma<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, sm));
+    return PANO_OK;
+}
+
 int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
                  const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
                  float *d2) {
@@ -273,9 +326,14 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
         }
         PANO_LAUNCH_CHECK(ctx, "row_norms");
         dim3 grid(n_t, n_t, np);
-        {
+        if (exact_int == 2) {
+            const size_t sm = 2 * (size_t)MT * KP_BF * sizeof(unsigned short);
             PanoProf prof_(ctx, PK_DIST_MFMA);
-            dist_mfma<<<grid, 256, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+            dist_mfma<true><<<grid, 256, sm, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+        } else {
+            const size_t sm = 2 * (size_t)MT * LDA * sizeof(float);
+            PanoProf prof_(ctx, PK_DIST_MFMA);
+            dist_mfma<false><<<grid, 256, sm, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
         }
         PANO_LAUNCH_CHECK(ctx, "dist_mfma");
         dim3 g2((cap + 255) / 256, np);

@@ -12,6 +12,7 @@ int sift_plan(const pano_sift_params *p, int h, int w, int *n_oct, int *n_lvl, d
               double *sig_lvl);
 int sift_set_attributes(pano_ctx *ctx);
 int harris_set_attributes(pano_ctx *ctx);
+int match_set_attributes(pano_ctx *ctx);
 
 int pano_fail(pano_ctx *ctx, int code, const std::string &msg) {
     if (ctx) ctx->err = msg;
@@ -79,6 +80,7 @@ int pano_ctx_create(int device, void *stream, pano_ctx **out) {
     ctx->stream = (hipStream_t)stream;
     int rc = sift_set_attributes(ctx);
     if (!rc) rc = harris_set_attributes(ctx);
+    if (!rc) rc = match_set_attributes(ctx);
     if (rc) {
         delete ctx;
         return rc;

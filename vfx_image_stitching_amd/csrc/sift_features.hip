@@ -104,7 +104,7 @@ __device__ void lstsq3_sym(const double A[3][3], const double b[3], double x[3])
 // octave of one frame; the ni+2 DoG levels of the tile (+1 halo) are staged in LDS and each
 // pixel is checked against its 26 neighbours there (exact f32 comparisons).  Candidates are
 // appended per frame with their scan-order key; S6 runs densely, thread per candidate.
-constexpr int ETX = 64, ETY = 8;
+constexpr int ETX = 64, ETY = 16;
 
 struct DogArgs {
     const float *dog[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t scan_key(int o, int layer0, int y, int x) {
 __global__ void __launch_bounds__(256)
 extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict__ raw,
              int32_t *__restrict__ raw_cnt, int raw_cap) {
-    __shared__ float s[PANO_MAX_LEVELS][ETY + 2][ETX + 2];
+    __shared__ float s[PANO_MAX_LEVELS - 1][ETY + 2][ETX + 2];
     const int f = blockIdx.y;
     int t = blockIdx.x, o = 0;
     while (o + 1 < a.n_oct && t >= a.tile_start[o + 1]) ++o;
@@ -131,12 +131,28 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
     const int y0 = border + (t / a.tiles_x[o]) * ETY;
     const int tid = threadIdx.x;
     const int nl = ni + 2;
-    for (int i = tid; i < nl * (ETY + 2) * (ETX + 2); i += 256) {
-        const int l = i / ((ETY + 2) * (ETX + 2));
-        const int rem = i - l * (ETY + 2) * (ETX + 2);
-        const int yy = rem / (ETX + 2), xx = rem - yy * (ETX + 2);
-        const int gy = min(y0 - 1 + yy, H - 1), gx = min(x0 - 1 + xx, W - 1);
-        s[l][yy][xx] = a.dog[o][l][((size_t)f * H + gy) * W + gx];
+    // stage the ni+2 DoG levels of the tile (+1 halo); 4 independent loads per round
+    constexpr int TE = (ETY + 2) * (ETX + 2);
+    const int total = nl * TE;
+    for (int i0 = tid; i0 < total; i0 += 4 * 256) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * 256;
+            v[u] = 0.0f;
+            if (i < total) {
+                const int l = i / TE;
+                const int rem = i - l * TE;
+                const int yy = rem / (ETX + 2), xx = rem - yy * (ETX + 2);
+                const int gy = min(y0 - 1 + yy, H - 1), gx = min(x0 - 1 + xx, W - 1);
+                v[u] = a.dog[o][l][((size_t)f * H + gy) * W + gx];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * 256;
+            if (i < total) (&s[0][0][0])[(i / TE) * TE + (i % TE)] = v[u];
+        }
     }
     __syncthreads();
     for (int q = tid; q < ETX * ETY; q += 256) {
@@ -154,8 +170,8 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
 #pragma unroll
                     for (int dx = -1; dx <= 1; ++dx) {
                         const float nb = s[L + dz][py + 1 + dy][px + 1 + dx];
-                        ge = ge && (v >= nb);
-                        le = le && (v <= nb);
+                        ge &= (v >= nb);
+                        le &= (v <= nb);
                     }
             if (v > 0 ? ge : le) {
                 const int slot = atomicAdd(&raw_cnt[f], 1);
@@ -281,16 +297,17 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         const int side = 2 * radius + 1;
         const int S = side * side;
         for (int s = lane; s < S; s += 64) {
-            const int dy = s / side - radius;
-            const int dx = s - (s / side) * side - radius;
+            // column-major walk: neighbouring lanes take neighbouring ROWS, which spread over
+            // more histogram bins than a row run (fewer same-address LDS atomics)
+            const int dx = s / side - radius;
+            const int dy = s - (s / side) * side - radius;
             const int yy = cy + dy, xx = cx + dx;
             if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
             const float gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
             const float gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
             const float mag = sqrtf(gx * gx + gy * gy);
-            const float ang =
-                np_remainder_f((float)atan2((double)gy, (double)gx) * kRad2DegF32, 360.0f);
-            const float w = (float)exp((double)(wfac * (float)(dx * dx + dy * dy)));
+            const float ang = np_remainder_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+            const float w = expf(wfac * (float)(dx * dx + dy * dy));
             const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
             const double val = (double)(w * mag);
             atomicAdd(&hist[wv][bin], (unsigned long long)llrint(val * kHistScale));
@@ -516,8 +533,8 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     const float bins_per_deg = (float)(8.0 / 360.0);
     __syncthreads();
     for (int s = tid; s < S; s += 256) {
-        const int ys = s / side - half;
-        const int xs = s - (s / side) * side - half;
+        const int xs = s / side - half;                   // column-major: see orientation
+        const int ys = s - (s / side) * side - half;
         const int rr = py + ys, cc = px + xs;
         if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
         const double rrot = (double)xs * sin_a + (double)ys * cos_a;
@@ -529,8 +546,7 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
         const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
         const float mag = sqrtf(gx * gx + gy * gy);
-        const float ori =
-            np_remainder_f((float)atan2((double)gy, (double)gx) * kRad2DegF32, 360.0f);
+        const float ori = np_remainder_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
         const double w = exp(-0.125 * (rq * rq + cq * cq));
         const double wm = w * (double)mag;
         const float ob = np_remainder_f((ori - angle_f) * bins_per_deg, 8.0f);

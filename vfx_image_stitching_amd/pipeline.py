@@ -56,7 +56,8 @@ class Stitcher:
 
     def __init__(self, method: str = "sift", device: int | None = None, cap: int = 4096,
                  max_points: int = 200, ransac_thr: float = 3.0, desc_thresh: float | None = None,
-                 sift_params: dict | None = None):
+                 sift_params: dict | None = None, match: str | None = None):
+        import os
         import torch
         self.torch = torch
         self.method = method
@@ -68,6 +69,8 @@ class Stitcher:
         self.desc_thresh = float(desc_thresh if desc_thresh is not None
                                  else (25000 if method == "sift" else 1.0))
         self.params = _lib.default_sift_params(**(sift_params or {}))
+        # SIFT distance GEMM: "bf16" (exact for integer descriptors, 16x MFMA rate) or "f32"
+        self.match = match or os.environ.get("PANO_MATCH", "f32")
         self._buf = {}
 
     # ------------------------------------------------------------------ buffers
@@ -122,7 +125,7 @@ class Stitcher:
         best = self._get("best", (P, cap), T.int32)
         d1 = self._get("d1", (P, cap), T.float32)
         d2 = self._get("d2", (P, cap), T.float32)
-        exact = 1 if self.method == "sift" else 0
+        exact = (2 if self.match == "bf16" else 1) if self.method == "sift" else 0
         self.ctx.check(self.ctx.lib.pano_match(self.ctx.h, ptr(desc), ptr(counts), cap,
                                                _lib.i32p(hp), P, exact, ptr(best), ptr(d1), ptr(d2)))
         recs = self._get("recs", (P, 64), T.uint8)
