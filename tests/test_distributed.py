@@ -1,0 +1,161 @@
+"""Multi-GPU host logic on the CPU: pair shards, the record all_gather,
+band ownership and the crop-box all_reduce -- world_size 2 over gloo.
+
+The band compositing itself is checked on the GPU (test_gpu_parity.py::test_bands_*).
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from vfx_image_stitching_amd import _lib
+from vfx_image_stitching_amd import distributed as D
+from vfx_image_stitching_amd.pipeline import drift_correct
+
+
+def _plan(gold, h=512, w=384):
+    shifts = [tuple(s["move"]) for s in gold["shifts"]]
+    pairs = [tuple(tuple(p) for p in s["pair"]) for s in gold["shifts"]]
+    steps, first, (H, W) = D.global_plan(drift_correct(shifts), pairs, len(shifts) + 1, h, w)
+    return steps, first, H, W
+
+
+@pytest.mark.parametrize("n_pairs,world", [(17, 1), (17, 2), (17, 8), (143, 8), (5, 8), (0, 3)])
+def test_shard_ranges_balanced_and_contiguous(n_pairs, world):
+    r = D.shard_ranges(n_pairs, world)
+    assert len(r) == world
+    assert sum(c for _, c in r) == n_pairs
+    assert max(c for _, c in r) - min(c for _, c in r) <= 1
+    pos = 0
+    for s, c in r:
+        assert s == pos
+        pos += c
+    if (n_pairs, world) == (17, 8):                     # 3,2,2,2,2,2,2,2
+        assert [c for _, c in r] == [3, 2, 2, 2, 2, 2, 2, 2]
+
+
+def _last_frame_per_column(steps, first, w, n, W):
+    last = np.full(W, -1)
+    for i in range(n):
+        x = D.frame_xy(steps, first, i)[0]
+        last[x:x + w] = i
+    return last
+
+
+@pytest.mark.parametrize("name", ["sift_parrington.json", "sift_grail.json",
+                                  "harris_parrington.json", "harris_grail.json"])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_band_ownership_tiles_canvas(gold_json, name, world):
+    """Owned column ranges partition [0, W) and each owned column's last covering frame
+    and its predecessor are both inside the owning band."""
+    gold = gold_json(name)
+    steps, first, H, W = _plan(gold)
+    n = len(steps) + 1
+    w = 384
+    D.check_bands(steps, first, w)
+    last = _last_frame_per_column(steps, first, w, n, W)
+    assert (last >= 0).all()
+    covered = np.zeros(W, np.int32)
+    for s, c in D.shard_ranges(n - 1, world):
+        loc, first_loc, x0, bw, (lo, hi) = D.band_plan(steps, first, w, H, s, c, n)
+        assert x0 <= lo <= hi <= x0 + bw
+        covered[lo:hi] += 1
+        seg = last[lo:hi]
+        assert ((seg > s) | ((seg == 0) & (s == 0))).all()
+        assert (seg <= s + c).all()
+        # local plan = global plan shifted by the band origin
+        for k in range(c):
+            assert loc[k].frame_x + x0 == steps[s + k].frame_x
+            assert loc[k].frame_y == steps[s + k].frame_y
+    assert (covered == 1).all()
+
+
+def test_check_bands_refuses_triple_coverage():
+    """Small |dx| (< w/2): frames i and i-2 overlap -> band compositing is refused."""
+    shifts = [(-100.0, 0.0)] * 4
+    pairs = [((10.0, 10.0), (110.0, 10.0))] * 4
+    steps, first, _ = D.global_plan(drift_correct(shifts), pairs, 5, 64, 384)
+    with pytest.raises(D.BandError):
+        D.check_bands(steps, first, 384)
+
+
+# ---------------------------------------------------------------- gloo world_size 2
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rec(dx, dy, n):
+    r = np.zeros(1, _lib.PAIR_NP)
+    r["dx"], r["dy"] = dx, dy
+    r["xA"], r["yA"], r["xB"], r["yB"] = 10.0, 20.0, 10.0 - dx, 20.0 - dy
+    r["n_matches"], r["votes"], r["status"] = n, n, _lib.PANO_OK
+    return r
+
+
+def _worker(rank, world, port, gold, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shifts = [tuple(s["move"]) for s in gold["shifts"]]
+        pairs = [s["pair"] for s in gold["shifts"]]
+        shards = D.shard_ranges(len(shifts), world)
+        s0, c = shards[rank]
+        # 1. this rank's records (as pano_pair_shifts would write them) -> one all_gather
+        local = np.concatenate([_rec(shifts[s0 + k][0], shifts[s0 + k][1], 100 + s0 + k)
+                                for k in range(c)])
+        for k in range(c):
+            (xa, ya), (xb, yb) = pairs[s0 + k]
+            local[k]["xA"], local[k]["yA"], local[k]["xB"], local[k]["yB"] = xa, ya, xb, yb
+        t = torch.from_numpy(local.view(np.uint8).reshape(c, 64).copy())
+        recs = D.gather_records(t, [cc for _, cc in shards])
+        # 2. every rank replays the same global plan and derives its band
+        got_shifts, got_pairs = D.records_to_shifts(recs)
+        steps, first, (H, W) = D.global_plan(drift_correct(got_shifts), got_pairs,
+                                             len(got_shifts) + 1, 512, 384)
+        D.check_bands(steps, first, 384)
+        _, _, _, _, (lo, hi) = D.band_plan(steps, first, 384, H, s0, c, len(steps) + 1)
+        spans = [None] * world
+        dist.all_gather_object(spans, (lo, hi))
+        # 3. crop box: rank 1 pretends its band is empty
+        box = torch.tensor([5 + rank, 400 - rank, lo, hi - 1] if rank == 0 else list(D.NO_BOX),
+                           dtype=torch.int64)
+        g = D.global_bbox(box)
+        q.put((rank, [(float(r["dx"]), float(r["dy"]), int(r["n_matches"])) for r in recs],
+               spans, (H, W), g))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_plan_bands_bbox(gold_json):
+    import torch.multiprocessing as mp
+    gold = gold_json("sift_parrington.json")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, gold, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    shifts = [tuple(s["move"]) for s in gold["shifts"]]
+    for rank, recs, spans, (H, W), g in out:
+        assert [(a, b) for a, b, _ in recs] == [tuple(map(float, s)) for s in shifts]
+        assert [n for _, _, n in recs] == list(range(100, 100 + len(shifts)))
+        # the two bands tile the canvas exactly
+        (l0, h0), (l1, h1) = spans
+        assert sorted([l0, h0, l1, h1])[0] == 0 and max(h0, h1) == W
+        assert min(h0, h1) == max(l0, l1)
+        assert g == (5, 400, spans[0][0], spans[0][1] - 1)
+    assert out[0][1:] == out[1][1:]                      # identical replay on every rank

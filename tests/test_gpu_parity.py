@@ -359,3 +359,29 @@ def test_synthetic_sequence_recovers_known_shift(gpu):
     for i, (dx, dy) in enumerate(res.shifts):
         assert abs(dx + 300) <= 1.5, (i, dx)
         assert abs(dy - (jit[i + 1] - jit[i])) <= 1.5, (i, dy)
+
+
+# ------------------------------------------------------------------ multi-GPU bands (8e)
+@pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("harris", "grail")])
+def test_bands_assemble_to_single_gpu_canvas(gpu, method, setname):
+    """Each shard's records equal the single-GPU ones; owned bands composited from the shard's
+    own frames tile the single-GPU canvas byte for byte (world 2, 3 and 8 simulated in one
+    process -- the exchange itself is tested with gloo in test_distributed.py)."""
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd import distributed as D
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = data.load_set(setname)
+    st = Stitcher(method)
+    dev = st.upload(frames)
+    full = st.run(dev, focals, margin=margin)
+    canvas = full.canvas.cpu().numpy()
+    for world in (2, 3, 8):
+        got = np.full_like(canvas, 7)
+        for s, c in D.shard_ranges(len(frames) - 1, world):
+            recs_dev, cyl, colnz = D.local_records(st, dev[s:s + c + 1], focals[s:s + c + 1])
+            local = recs_dev.cpu().numpy().view(np.uint8)
+            assert np.array_equal(local, full.records.view(np.uint8).reshape(-1, 64)[s:s + c])
+            owned, lo, (H, W) = D.composite_band(st, cyl, colnz, full.records, s)
+            assert (H, W) == canvas.shape[:2]
+            got[:, lo:lo + owned.shape[1]] = owned.cpu().numpy()
+        assert np.array_equal(got, canvas), world

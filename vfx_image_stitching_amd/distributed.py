@@ -99,15 +99,57 @@ def check_bands(steps, first, w):
             raise BandError(f"frames {i} and {i - 2} overlap: bands are not independent")
 
 
-def band_plan(steps, first, w, H, f0, count):
+def last_cover(steps, first, w, i, n_frames):
+    """Columns whose final value is written by frame i: its span minus frame i+1's span.
+
+    With no column covered by three frames (check_bands), only frame i+1 can overwrite
+    frame i, so a canvas column's final value is fixed by its LAST covering frame i and
+    that frame's predecessor i-1.  Returns a list of disjoint [lo, hi) intervals.
+    """
+    lo, hi = frame_xy(steps, first, i)[0], frame_xy(steps, first, i)[0] + w
+    if i + 1 >= n_frames:
+        return [(lo, hi)]
+    nlo = frame_xy(steps, first, i + 1)[0]
+    nhi = nlo + w
+    out = []
+    if lo < min(hi, nlo):
+        out.append((lo, min(hi, nlo)))
+    if max(lo, nhi) < hi:
+        out.append((max(lo, nhi), hi))
+    return out
+
+
+def owned_columns(steps, first, w, f0, count, n_frames):
+    """Canvas columns a band of frames f0 .. f0+count composites to their final value.
+
+    The band holds frames f0 .. f0+count and applies steps f0+1 .. f0+count, so it owns the
+    columns whose last covering frame is in (f0, f0+count] -- plus frame 0's for the first
+    band.  Returns one [lo, hi) interval (BandError if the union is not contiguous).
+    """
+    iv = []
+    for i in range(f0 if f0 == 0 else f0 + 1, f0 + count + 1):
+        iv.extend(last_cover(steps, first, w, i, n_frames))
+    if not iv:
+        return (0, 0)
+    iv.sort()
+    lo, hi = iv[0]
+    for a, b in iv[1:]:
+        if a > hi:
+            raise BandError(f"band {f0}..{f0 + count} owns non-contiguous columns")
+        hi = max(hi, b)
+    return lo, hi
+
+
+def band_plan(steps, first, w, H, f0, count, n_frames=None):
     """Local composite plan for frames f0 .. f0+count (rank's range incl. boundary frame).
 
     Returns (local_steps, local_first_xy, x_offset, band_width, owned (x0, x1)).
     The band starts from frame f0 as it stands before step f0+1 (its raw pixels in the
-    columns the next frame can reach) and applies global steps f0+1 .. f0+count.
-    Owned columns: everything the band's frames cover, minus frame f0's overlap with the
-    previous rank's frames (that rank blended those columns).
+    columns the next frame can reach: frame f0+1 never meets frame f0-1) and applies
+    global steps f0+1 .. f0+count.  Owned columns: see owned_columns.
     """
+    if n_frames is None:
+        n_frames = len(steps) + 1
     xs = [frame_xy(steps, first, f0 + k)[0] for k in range(count + 1)]
     x_lo, x_hi = min(xs), max(xs) + w
     loc = (_lib.Step * max(count, 1))()
@@ -120,14 +162,57 @@ def band_plan(steps, first, w, H, f0, count):
         s.canvas_x = g.canvas_x - x_lo
     fx, fy = frame_xy(steps, first, f0)
     first_loc = np.array([fx - x_lo, fy], np.int32)
-    own_lo, own_hi = x_lo, x_hi
-    if f0 > 0:
-        px = frame_xy(steps, first, f0 - 1)[0]
-        if px > fx:                        # previous frame to the right (dx < 0 sequences)
-            own_hi = min(own_hi, px)
-        else:
-            own_lo = max(own_lo, px + w)
+    own_lo, own_hi = owned_columns(steps, first, w, f0, count, n_frames)
+    assert x_lo <= own_lo and own_hi <= x_hi
     return loc, first_loc, x_lo, x_hi - x_lo, (own_lo, own_hi)
+
+
+def local_records(stitcher, frames_dev, focals):
+    """Cylindrical projection, features, matching and RANSAC of one rank's frames."""
+    n_local = frames_dev.shape[0]
+    cyl, colnz = stitcher.cylindrical(frames_dev, focals)
+    feats = stitcher.features(cyl)
+    recs_dev, _ = stitcher.pair_records(feats, [(i, i + 1) for i in range(n_local - 1)])
+    return recs_dev, cyl, colnz
+
+
+def composite_band(stitcher, cyl, colnz, recs, pair_start, check=True):
+    """Drift + global plan from ALL records, then this rank's band of the canvas.
+
+    Returns (owned band view [H, own_hi-own_lo, 3] on device, own_lo, (H, W)).
+    """
+    import torch
+    n_local, h, w = cyl.shape[0], cyl.shape[1], cyl.shape[2]
+    from .pipeline import drift_correct
+    shifts, pairs = records_to_shifts(recs, integer=stitcher.method != "sift")
+    n_frames = len(shifts) + 1
+    steps, first, (H, W) = global_plan(drift_correct(shifts), pairs, n_frames, h, w)
+    if check:
+        check_bands(steps, first, w)
+    loc, first_loc, x0, bw, (own_lo, own_hi) = band_plan(steps, first, w, H, pair_start,
+                                                         n_local - 1, n_frames)
+    band = stitcher._get("band", (H, bw, 3), torch.uint8)
+    ctx = stitcher.ctx
+    ctx.check(ctx.lib.pano_composite(ctx.h, _lib.ptr(cyl), _lib.ptr(colnz), n_local, h, w, loc,
+                                     _lib.i32p(first_loc), _lib.ptr(band), H, bw))
+    return band[:, own_lo - x0:own_hi - x0], own_lo, (H, W)
+
+
+NO_BOX = (1 << 30, -1, 1 << 30, -1)
+
+
+def global_bbox(local_bbox, group=None):
+    """rectangle_crop's box over all bands: elementwise min/max of [ymin ymax xmin xmax]
+    (int64 tensor; a band with no pixel contributes NO_BOX).  One 4-int all_reduce."""
+    import torch
+    import torch.distributed as dist
+    b = local_bbox.to(torch.int64).clone()
+    # (-ymin, ymax, -xmin, xmax) under one MAX reduction
+    v = torch.stack([-b[0], b[1], -b[2], b[3]])
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    v = v.cpu().numpy()
+    return int(-v[0]), int(v[1]), int(-v[2]), int(v[3])
 
 
 def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15):
@@ -138,41 +223,21 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
     """
     import torch
     import torch.distributed as dist
-    n_local = frames_dev.shape[0]
-    h, w = frames_dev.shape[1], frames_dev.shape[2]
-    cyl, colnz = stitcher.cylindrical(frames_dev, focals)
-    feats = stitcher.features(cyl)
-    recs_dev, _ = stitcher.pair_records(feats, [(i, i + 1) for i in range(n_local - 1)])
+    recs_dev, cyl, colnz = local_records(stitcher, frames_dev, focals)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world > 1:
         recs = gather_records(recs_dev, pair_counts, group)
     else:
         recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)
-    from .pipeline import drift_correct
-    shifts, pairs = records_to_shifts(recs, integer=stitcher.method != "sift")
-    steps, first, (H, W) = global_plan(drift_correct(shifts), pairs, len(shifts) + 1, h, w)
-    if world > 1:
-        check_bands(steps, first, w)
-    loc, first_loc, x0, bw, (own_lo, own_hi) = band_plan(steps, first, w, H, pair_start,
-                                                         n_local - 1)
-    band = stitcher._get("band", (H, bw, 3), torch.uint8)
-    ctx = stitcher.ctx
-    ctx.check(ctx.lib.pano_composite(ctx.h, _lib.ptr(cyl), _lib.ptr(colnz), n_local, h, w, loc,
-                                     _lib.i32p(first_loc), _lib.ptr(band), H, bw))
-    owned = band[:, own_lo - x0:own_hi - x0].contiguous()
-    bb = stitcher.bbox(owned).to(torch.int64)
-    lo = torch.where(bb[1] >= 0, bb, torch.tensor([1 << 30, -1, 1 << 30, -1], device=bb.device))
-    lo[2] += own_lo
-    lo[3] = torch.where(lo[3] >= 0, lo[3] + own_lo, lo[3])
-    if world > 1:
-        mins = torch.stack([lo[0], lo[2]])
-        maxs = torch.stack([lo[1], lo[3]])
-        dist.all_reduce(mins, op=dist.ReduceOp.MIN, group=group)
-        dist.all_reduce(maxs, op=dist.ReduceOp.MAX, group=group)
-        g = (int(mins[0]), int(maxs[0]), int(mins[1]), int(maxs[1]))
+    owned, own_lo, (H, W) = composite_band(stitcher, cyl, colnz, recs, pair_start,
+                                           check=world > 1)
+    if owned.shape[1] > 0:
+        bb = stitcher.bbox(owned.contiguous()).to(torch.int64)
+        lo = torch.where(bb[1] >= 0, bb, torch.tensor(NO_BOX, device=bb.device))
+        lo[2:] = torch.where(lo[3] >= 0, lo[2:] + own_lo, lo[2:])
     else:
-        v = lo.cpu().numpy()
-        g = (int(v[0]), int(v[1]), int(v[2]), int(v[3]))
+        lo = torch.tensor(NO_BOX, dtype=torch.int64, device=owned.device)
+    g = global_bbox(lo, group)
     if g[1] >= 0:
         y0, y1 = max(0, g[0] + margin), min(H - 1, g[1] - margin)
     else:
