@@ -93,7 +93,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (!ctx) return PANO_OK;
     (void)hipStreamSynchronize(ctx->stream);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
-                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch};
+                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
@@ -120,7 +120,7 @@ int pano_sync(pano_ctx *ctx) {
     if (e != hipSuccess) return pano_hip_check(ctx, e, "pano_sync");
     if (ctx->counters && ctx->n > 0) {
         int32_t err = 0;
-        e = hipMemcpy(&err, ctx->counters + 2 * ctx->n, sizeof err, hipMemcpyDeviceToHost);
+        e = hipMemcpy(&err, ctx->counters, sizeof err, hipMemcpyDeviceToHost);
         if (e == hipSuccess && err) return pano_fail(ctx, PANO_E_OVERFLOW, "keypoint capacity exceeded");
     }
     return PANO_OK;

@@ -17,6 +17,9 @@
 #define PANO_MAX_OCTAVES 16
 #define PANO_MAX_LEVELS 8      // num_intervals + 3 <= 8  -> num_intervals <= 5
 #define PANO_MAX_TAPS 64
+// SIFT per-frame counters: one 128-byte line each (no false sharing between frames).
+// Layout of pano_ctx::counters: [err] [cand f=0..n) [raw f] [ext f], kCntStride ints apiece.
+constexpr int kCntStride = 32;
 #define PANO_ORI_BINS 36
 
 // Raw keypoint produced by the orientation kernel (before sort/dedup/convert), in base
@@ -79,7 +82,10 @@ struct pano_ctx {
     int32_t *frame_off = nullptr;        // raw extrema (scan keys) before localisation
     size_t ext_bytes = 0;
     RawKp *raw_sorted = nullptr;
-    double *taps = nullptr;              // device Gaussian taps, per level
+    double *taps = nullptr;              // device Gaussian taps, per level [L][PANO_MAX_TAPS]
+    double taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // what *taps holds
+    bool taps_valid = false;
+    uint8_t *gray = nullptr; size_t gray_bytes = 0;   // u8 gray frames (base blur input)
     // ---- match / ransac scratch
     void *mscratch = nullptr; size_t mscratch_bytes = 0;
     // ---- composite scratch
@@ -194,6 +200,12 @@ __device__ __forceinline__ float np_remainder_f(float a, float b) {
         m = copysignf(0.0f, b);
     }
     return m;
+}
+// np_remainder_f for b > 0 with the common |a| < b case first: fmod(a, b) == a exactly
+// there, so the result is a, a + b (a < 0, rounded as numpy rounds it) or +0.
+__device__ __forceinline__ float np_remainder_pos_f(float a, float b) {
+    if (fabsf(a) < b) return a < 0.0f ? a + b : (a == 0.0f ? 0.0f : a);
+    return np_remainder_f(a, b);
 }
 __device__ __forceinline__ double np_remainder(double a, double b) {
     double m = fmod(a, b);

@@ -57,9 +57,12 @@ __device__ void lstsq3_sym(const double A[3][3], const double b[3], double x[3])
             a[i][j] = A[i][j];
             v[i][j] = (i == j) ? 1.0 : 0.0;
         }
+    // Cyclic Jacobi converges quadratically: stop once the off-diagonal mass is below
+    // 1e-20 of the diagonal -- later rotations would move x by ~1e-20 relative, far under
+    // the f32 rounding of the result (the solve only has to reproduce dgelsd -> float32).
     for (int sweep = 0; sweep < 16; ++sweep) {
         const double off = fabs(a[0][1]) + fabs(a[0][2]) + fabs(a[1][2]);
-        if (off == 0.0) break;
+        if (off <= 1e-20 * (fabs(a[0][0]) + fabs(a[1][1]) + fabs(a[2][2]))) break;
         for (int pq = 0; pq < 3; ++pq) {
             const int p = pq == 2 ? 1 : 0;
             const int q = pq == 0 ? 1 : 2;
@@ -122,6 +125,7 @@ __global__ void __launch_bounds__(256)
 extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict__ raw,
              int32_t *__restrict__ raw_cnt, int raw_cap) {
     __shared__ float s[PANO_MAX_LEVELS - 1][ETY + 2][ETX + 2];
+    __shared__ int wtot[4], wbase;
     const int f = blockIdx.y;
     int t = blockIdx.x, o = 0;
     while (o + 1 < a.n_oct && t >= a.tile_start[o + 1]) ++o;
@@ -131,53 +135,106 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
     const int y0 = border + (t / a.tiles_x[o]) * ETY;
     const int tid = threadIdx.x;
     const int nl = ni + 2;
-    // stage the ni+2 DoG levels of the tile (+1 halo); 4 independent loads per round
-    constexpr int TE = (ETY + 2) * (ETX + 2);
-    const int total = nl * TE;
-    for (int i0 = tid; i0 < total; i0 += 4 * 256) {
-        float v[4];
+    // stage the ni+2 DoG levels of the tile (+1 halo): wave w stages rows w, w+4, ... of the
+    // (level, row) list, lane = column (lanes 0,1 also take the two right-halo columns);
+    // level / row are wave-uniform and 8 rows are in flight per lane.
+    const int lane = tid & 63, wv = tid >> 6;
+    const int nrows = nl * (ETY + 2);
+    const int gxa = min(x0 - 1 + lane, W - 1);
+    const int gxb = min(x0 - 1 + 64 + lane, W - 1);
+    for (int r0 = wv; r0 < nrows; r0 += 4 * 8) {
+        float va[8], vb[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * 256;
-            v[u] = 0.0f;
-            if (i < total) {
-                const int l = i / TE;
-                const int rem = i - l * TE;
-                const int yy = rem / (ETX + 2), xx = rem - yy * (ETX + 2);
-                const int gy = min(y0 - 1 + yy, H - 1), gx = min(x0 - 1 + xx, W - 1);
-                v[u] = a.dog[o][l][((size_t)f * H + gy) * W + gx];
+        for (int u = 0; u < 8; ++u) {
+            const int rr = r0 + 4 * u;
+            va[u] = vb[u] = 0.0f;
+            if (rr < nrows) {
+                const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
+                const int gy = min(y0 - 1 + yy, H - 1);
+                const float *row = a.dog[o][l] + ((size_t)f * H + gy) * W;
+                va[u] = row[gxa];
+                if (lane < ETX + 2 - 64) vb[u] = row[gxb];
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * 256;
-            if (i < total) (&s[0][0][0])[(i / TE) * TE + (i % TE)] = v[u];
+        for (int u = 0; u < 8; ++u) {
+            const int rr = r0 + 4 * u;
+            if (rr < nrows) {
+                const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
+                s[l][yy][lane] = va[u];
+                if (lane < ETX + 2 - 64) s[l][yy][64 + lane] = vb[u];
+            }
         }
     }
     __syncthreads();
-    for (int q = tid; q < ETX * ETY; q += 256) {
-        const int px = q % ETX, py = q / ETX;
-        const int x = x0 + px, y = y0 + py;
-        if (x >= W - border || y >= H - border) continue;
-        for (int L = 1; L <= ni; ++L) {
-            const float v = s[L][py + 1][px + 1];
-            if (!((double)fabsf(v) > thresh)) continue;
-            bool ge = true, le = true;
+    // is_pixel_an_extremum: v >= all 26 neighbours  <=>  v == max of the 3x3x3 cube (v is
+    // in it), likewise <= / min.  The cube max/min is separable: lane = column, 3-wide
+    // horizontal then 3-tall vertical max/min per level in registers (4 output rows per
+    // thread), then the 3-level max/min per layer.  Exact: only f32 max/min/compare.
+    constexpr int RPT = ETY / 4;                  // output rows per thread
+    static_assert(ETX == 64 && ETY % 4 == 0, "lane = column, 4 row groups");
+    const int py0 = wv * RPT;
+    float vmx[PANO_MAX_LEVELS - 1][RPT], vmn[PANO_MAX_LEVELS - 1][RPT];
 #pragma unroll
-            for (int dz = -1; dz <= 1; ++dz)
+    for (int l = 0; l < PANO_MAX_LEVELS - 1; ++l) {
+        if (l >= nl) break;
+        float hmx[RPT + 2], hmn[RPT + 2];
 #pragma unroll
-                for (int dy = -1; dy <= 1; ++dy)
+        for (int r = 0; r < RPT + 2; ++r) {
+            const float *row = &s[l][py0 + r][lane];
+            const float a0 = row[0], a1 = row[1], a2 = row[2];
+            hmx[r] = fmaxf(fmaxf(a0, a1), a2);
+            hmn[r] = fminf(fminf(a0, a1), a2);
+        }
 #pragma unroll
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const float nb = s[L + dz][py + 1 + dy][px + 1 + dx];
-                        ge &= (v >= nb);
-                        le &= (v <= nb);
-                    }
-            if (v > 0 ? ge : le) {
-                const int slot = atomicAdd(&raw_cnt[f], 1);
-                if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = scan_key(o, L, y, x);
+        for (int i = 0; i < RPT; ++i) {
+            vmx[l][i] = fmaxf(fmaxf(hmx[i], hmx[i + 1]), hmx[i + 2]);
+            vmn[l][i] = fminf(fminf(hmn[i], hmn[i + 1]), hmn[i + 2]);
+        }
+    }
+    const int x = x0 + lane;
+    uint32_t hits = 0;                            // bit i * 8 + L: extremum at row i, layer L
+    if (x < W - border) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int py = py0 + i, y = y0 + py;
+            if (y >= H - border) break;
+#pragma unroll
+            for (int L = 1; L < PANO_MAX_LEVELS - 2; ++L) {
+                if (L > ni) break;
+                const float v = s[L][py + 1][lane + 1];
+                if (!((double)fabsf(v) > thresh)) continue;
+                const bool ext = v > 0
+                    ? v >= fmaxf(fmaxf(vmx[L - 1][i], vmx[L][i]), vmx[L + 1][i])
+                    : v <= fminf(fminf(vmn[L - 1][i], vmn[L][i]), vmn[L + 1][i]);
+                if (ext) hits |= 1u << (i * 8 + L);
             }
         }
+    }
+    // one global atomic per workgroup: wave prefix sums of the per-lane hit counts, wave
+    // totals through LDS, then each lane writes its keys (key order is restored downstream)
+    const int mine = __popc(hits);
+    int incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        const int tot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        wbase = tot ? atomicAdd(&raw_cnt[f * kCntStride], tot) : 0;
+    }
+    __syncthreads();
+    int slot = wbase + incl - mine;
+    for (int w = 0; w < wv; ++w) slot += wtot[w];
+    while (hits) {
+        const int b = __ffs(hits) - 1;
+        hits &= hits - 1;
+        if (slot < raw_cap)
+            raw[(size_t)f * raw_cap + slot] = scan_key(o, b & 7, y0 + py0 + (b >> 3), x);
+        ++slot;
     }
 }
 
@@ -185,16 +242,8 @@ __device__ __forceinline__ float dog_at(const DogArgs &a, int o, int lvl, int f,
     return a.dog[o][lvl][((size_t)f * a.H[o] + y) * a.W[o] + x];
 }
 
-__global__ void __launch_bounds__(256)
-localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
-         const int32_t *__restrict__ raw_cnt, int raw_cap, Cand *__restrict__ cands,
-         int32_t *__restrict__ cand_cnt, int cand_cap) {
-    const int f = blockIdx.y;
-    const int ci = blockIdx.x * 256 + threadIdx.x;
-    int cnt = raw_cnt[f];
-    cnt = cnt < raw_cap ? cnt : raw_cap;
-    if (ci >= cnt) return;
-    const uint32_t key = raw[(size_t)f * raw_cap + ci];
+// One extremum through the quadratic fit and the contrast / edge tests.
+__device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint32_t key, int f, Cand &k) {
     const int o = (int)(key >> 24) / 8, layer0 = (int)(key >> 24) % 8;
     const int y = (int)((key >> 12) & 4095), x = (int)(key & 4095);
     const int ni = lp.ni, border = lp.border;
@@ -235,18 +284,17 @@ localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
         li += (int)rintf(u[2]);
         if (yi < border || yi >= H - border || xi < border || xi >= W - border || li < 1 ||
             li > ni)
-            return;
+            return false;
     }
     double dacc = 0.0;
     for (int i = 0; i < 3; ++i) dacc += (double)(g[i] * u[i]);
     const float val = c[1][1][1] + 0.5f * (float)dacc;
-    if (fabsf(val) * (float)ni < lp.contrast) return;
+    if (fabsf(val) * (float)ni < lp.contrast) return false;
     const float tr = Hs[0][0] + Hs[1][1];
     const float det = (float)((double)Hs[0][0] * (double)Hs[1][1] -
                               (double)Hs[0][1] * (double)Hs[1][0]);
-    if (det <= 0.0f || lp.edge_lhs * (tr * tr) >= lp.edge_rhs * det) return;
+    if (det <= 0.0f || lp.edge_lhs * (tr * tr) >= lp.edge_rhs * det) return false;
     const float so = (float)(1 << o);
-    Cand k;
     k.x = ((float)xi + u[0]) * so;
     k.y = ((float)yi + u[1]) * so;
     k.octave_field = o + li * 256 + (int)rintf((u[2] + 0.5f) * 255.0f) * 65536;
@@ -258,11 +306,34 @@ localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
     k.layer = (int16_t)li;
     k.frame = f;
     k.order = key;
-    const int slot = atomicAdd(&cand_cnt[f], 1);
-    if (slot < cand_cap) cands[(size_t)f * cand_cap + slot] = k;
+    return true;
 }
 
+__global__ void __launch_bounds__(256)
+localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
+         const int32_t *__restrict__ raw_cnt, int raw_cap, Cand *__restrict__ cands,
+         int32_t *__restrict__ cand_cnt, int cand_cap) {
+    const int f = blockIdx.y;
+    const int ci = blockIdx.x * 256 + threadIdx.x;
+    int cnt = raw_cnt[f * kCntStride];
+    cnt = cnt < raw_cap ? cnt : raw_cap;
+    if ((int)blockIdx.x * 256 >= cnt) return;   // uniform
+    bool keep = false;
+    Cand k;
+    if (ci < cnt) keep = localize_one(a, lp, raw[(size_t)f * raw_cap + ci], f, k);
+    const unsigned long long m = __ballot(keep);
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&cand_cnt[f * kCntStride], __popcll(m));
+    base = __shfl(base, 0);
+    const int slot = base + __popcll(m & ((1ull << lane) - 1));
+    if (keep && slot < cand_cap) cands[(size_t)f * cand_cap + slot] = k;
+}
+
+
 // ------------------------------------------------------------------ S7
+constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
+
 struct OriParams {
     double scale_factor, radius_factor, peak_ratio;
 };
@@ -274,10 +345,11 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     __shared__ unsigned long long hist[4][PANO_ORI_BINS];
     __shared__ double hd[4][PANO_ORI_BINS];
     __shared__ double sm[4][PANO_ORI_BINS];
+    __shared__ float patch[4][kOriPatch * kOriPatch];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int ci = blockIdx.x * 4 + wv;
-    int cnt = cand_cnt[f];
+    int cnt = cand_cnt[f * kCntStride];
     cnt = cnt < cand_cap ? cnt : cand_cap;
     if ((int)blockIdx.x * 4 >= cnt) return;   // uniform: no wave of this block is active
     const bool active = ci < cnt;
@@ -296,17 +368,43 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         const int cx = (int)rintf(k.x / (float)(1 << o));
         const int side = 2 * radius + 1;
         const int S = side * side;
-        for (int s = lane; s < S; s += 64) {
-            // column-major walk: neighbouring lanes take neighbouring ROWS, which spread over
-            // more histogram bins than a row run (fewer same-address LDS atomics)
-            const int dx = s / side - radius;
-            const int dy = s - (s / side) * side - radius;
+        // stage the (side+2)^2 neighbourhood (clamped; out-of-image samples are skipped
+        // below) so each sample's four gradient taps are LDS reads
+        const int P = side + 2;
+        const bool staged = P <= kOriPatch;
+        float *pt = patch[wv];
+        if (staged) {
+            const int by = cy - radius - 1, bx = cx - radius - 1;
+            for (int e = lane; e < P * P; e += 64) {
+                const int r = e / P, c = e - (e / P) * P;
+                const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
+                pt[r * kOriPatch + c] = img[(size_t)yy * W + xx];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // lane l walks its own run of Q consecutive column-major samples (neighbouring lanes
+        // are Q samples apart: different bins, fewer same-address LDS atomics)
+        const int Q = (S + 63) / 64;
+        const int j0 = lane * Q;
+        int xi = j0 / side, yi = j0 - (j0 / side) * side;
+        const int jend = min(j0 + Q, S);
+        for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
+            const int dx = xi - radius, dy = yi - radius;
             const int yy = cy + dy, xx = cx + dx;
             if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
-            const float gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
-            const float gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+            float gx, gy;
+            if (staged) {
+                const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
+                gx = q[1] - q[-1];
+                gy = q[-kOriPatch] - q[kOriPatch];
+            } else {
+                gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
+                gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+            }
             const float mag = sqrtf(gx * gx + gy * gy);
-            const float ang = np_remainder_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+            const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
             const float w = expf(wfac * (float)(dx * dx + dy * dy));
             const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
             const double val = (double)(w * mag);
@@ -324,18 +422,30 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         sm[wv][b] = sm[wv][b] / 16.0;
     }
     __syncthreads();
-    if (!active || lane >= PANO_ORI_BINS) return;
+    // peaks -> keypoints; one (wave-aggregated) append per candidate
     const int nb = PANO_ORI_BINS;
-    const double *s = sm[wv];
-    double mx = s[0];
-    for (int b = 1; b < nb; ++b) mx = fmax(mx, s[b]);
     const int p = lane;
-    const double l = s[(p + nb - 1) % nb], r = s[(p + 1) % nb];
-    if (!(s[p] > l && s[p] > r)) return;
-    if (!(s[p] >= op.peak_ratio * mx)) return;
-    const double interp = np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * s[p]) + r), (double)nb);
-    double angle = 360.0 - interp * 360.0 / nb;
-    if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
+    bool emit = false;
+    double angle = 0.0;
+    if (active && lane < nb) {
+        const double *s = sm[wv];
+        double mx = s[0];
+        for (int b = 1; b < nb; ++b) mx = fmax(mx, s[b]);
+        const double l = s[(p + nb - 1) % nb], r = s[(p + 1) % nb];
+        if (s[p] > l && s[p] > r && s[p] >= op.peak_ratio * mx) {
+            const double interp =
+                np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * s[p]) + r), (double)nb);
+            angle = 360.0 - interp * 360.0 / nb;
+            if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
+            emit = true;
+        }
+    }
+    const unsigned long long m = __ballot(emit);
+    if (!m) return;
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&raw_cnt[f * kCntStride], __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (!emit) return;
     RawKp q;
     q.x = k.x;
     q.y = k.y;
@@ -345,7 +455,7 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     q.octave = k.octave_field;
     q.frame = f;
     q.order = ((uint64_t)k.order << 6) | (uint64_t)p;
-    const int slot = atomicAdd(&raw_cnt[f], 1);
+    const int slot = base + __popcll(m & ((1ull << lane) - 1));
     if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = q;
 }
 
@@ -376,7 +486,7 @@ sort_dedup(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, i
     __shared__ int32_t scan[1024];
     const int f = blockIdx.x, tid = threadIdx.x;
     const RawKp *rec = raw + (size_t)f * raw_cap;
-    int cnt = raw_cnt[f];
+    int cnt = raw_cnt[f * kCntStride];
     if (cnt > raw_cap || cnt > kSortMax) {
         if (tid == 0) { err[0] = PANO_E_OVERFLOW; counts[f] = -1; }
         return;
@@ -498,17 +608,21 @@ struct DescParams {
     float max_value;   // f32(descriptor_max_value)
 };
 
+constexpr int kDescWin = 4096;
+
 __global__ void __launch_bounds__(256)
 descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
            const int32_t *__restrict__ counts, int cap, float *__restrict__ desc) {
-    __shared__ unsigned long long acc[128];
+    __shared__ unsigned long long acc[4][128];   // one histogram per wave
+    __shared__ uint32_t list[kDescWin];          // compacted candidate samples (xi << 16 | yi)
+    __shared__ int list_n;
     __shared__ float vec[128];
     __shared__ float sh_norm;
     const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
     int cnt = counts[f];
     cnt = cnt < cap ? cnt : cap;
     if (k >= cnt) return;
-    if (tid < 128) acc[tid] = 0ull;
+    for (int i = tid; i < 4 * 128; i += 256) (&acc[0][0])[i] = 0ull;
     const pano_kp kp = kps[(size_t)f * cap + k];
     int oct = kp.octave & 255;
     if (oct >= 128) oct |= -128;
@@ -528,48 +642,88 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     const int diag = (int)sqrt((double)(rows * rows + cols * cols));
     half = half < diag ? half : diag;
     const int side = 2 * half + 1;
-    const int S = side * side;
     const float angle_f = (float)angle;
     const float bins_per_deg = (float)(8.0 / 360.0);
     __syncthreads();
-    for (int s = tid; s < S; s += 256) {
-        const int xs = s / side - half;                   // column-major: see orientation
-        const int ys = s - (s / side) * side - half;
-        const int rr = py + ys, cc = px + xs;
-        if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
-        const double rrot = (double)xs * sin_a + (double)ys * cos_a;
-        const double crot = (double)xs * cos_a - (double)ys * sin_a;
-        const double rq = rrot / hwd, cq = crot / hwd;
-        const double rbin = (rq + 2.0) - 0.5;
-        const double cbin = (cq + 2.0) - 0.5;
-        if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) continue;
-        const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
-        const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
-        const float mag = sqrtf(gx * gx + gy * gy);
-        const float ori = np_remainder_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
-        const double w = exp(-0.125 * (rq * rq + cq * cq));
-        const double wm = w * (double)mag;
-        const float ob = np_remainder_f((ori - angle_f) * bins_per_deg, 8.0f);
-        const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
-        const int o0 = ((int)floorf(ob)) % 8;
-        const double rf = rbin - r0, cf = cbin - c0;
-        const double of = (double)ob - (double)o0;
-        const double c1 = wm * rf;
-        const double c0w = wm - c1;
-        const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rb = r0 + 1 + (q >> 1), cb = c0 + 1 + (q & 1);
-            if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
-            const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
-            const double v0 = part[q] * (1 - of);
-            const double v1 = part[q] * of;
-            atomicAdd(&acc[base + o0], (unsigned long long)llrint(v0 * kDescScale));
-            atomicAdd(&acc[base + (o0 + 1) % 8], (unsigned long long)llrint(v1 * kDescScale));
+    // Two phases per window of kDescWin samples: (A) a cheap, conservative test of the
+    // rotated-bin range (no divisions) compacts the candidate samples into an LDS list with
+    // one ballot per wave; (B) the threads process the list densely -- exact bin test, then
+    // the gradient / exp / atan2 / trilinear work -- so about half the square patch (outside
+    // the 4 x 4 bins) costs almost nothing and the heavy path runs without divergence.
+    // The fixed-point histogram sums are integers, hence independent of this order.
+    const int S = side * side;
+    const int lane = tid & 63, wv = tid >> 6;
+    unsigned long long *wacc = acc[wv];
+    const float inv_side = 1.0f / (float)side;
+    const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hwd < 2.5 with slack
+    for (int win = 0; win < S; win += kDescWin) {
+        if (tid == 0) list_n = 0;
+        __syncthreads();
+        const int wend = min(win + kDescWin, S);
+        for (int j = win + tid; j < wend + ((256 - (wend - win) % 256) % 256); j += 256) {
+            bool ok = false;
+            int xi = 0, yi = 0;
+            if (j < wend) {
+                // column-major j -> (xi, yi); the f32 quotient is exact for side < 2048
+                xi = side < 2048 ? (int)(((float)j + 0.5f) * inv_side) : j / side;
+                yi = j - xi * side;
+                const int xs = xi - half, ys = yi - half;
+                const int rr = py + ys, cc = px + xs;
+                const double rrot = (double)xs * sin_a + (double)ys * cos_a;
+                const double crot = (double)xs * cos_a - (double)ys * sin_a;
+                ok = rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1 && fabs(rrot) < lim &&
+                     fabs(crot) < lim;
+            }
+            const unsigned long long m = __ballot(ok);
+            int off = 0;
+            if (lane == 0 && m) off = atomicAdd(&list_n, __popcll(m));
+            off = __shfl(off, 0);
+            if (ok) list[off + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)(xi << 16 | yi);
         }
+        __syncthreads();
+        const int nl = list_n;
+        for (int t = tid; t < nl; t += 256) {
+            const int xi = (int)(list[t] >> 16), yi = (int)(list[t] & 0xffff);
+            const int xs = xi - half, ys = yi - half;
+            const int rr = py + ys, cc = px + xs;
+            const double rrot = (double)xs * sin_a + (double)ys * cos_a;
+            const double crot = (double)xs * cos_a - (double)ys * sin_a;
+            const double rq = rrot / hwd, cq = crot / hwd;
+            const double rbin = (rq + 2.0) - 0.5;
+            const double cbin = (cq + 2.0) - 0.5;
+            if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) continue;
+            const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
+            const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
+            const float mag = sqrtf(gx * gx + gy * gy);
+            const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+            const double w = exp(-0.125 * (rq * rq + cq * cq));
+            const double wm = w * (double)mag;
+            const float ob = np_remainder_pos_f((ori - angle_f) * bins_per_deg, 8.0f);
+            const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
+            const int o0 = ((int)floorf(ob)) % 8;
+            const double rf = rbin - r0, cf = cbin - c0;
+            const double of = (double)ob - (double)o0;
+            const double c1 = wm * rf;
+            const double c0w = wm - c1;
+            const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rb = r0 + 1 + (q >> 1), cb = c0 + 1 + (q & 1);
+                if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
+                const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
+                const double v0 = part[q] * (1 - of);
+                const double v1 = part[q] * of;
+                atomicAdd(&wacc[base + o0], (unsigned long long)llrint(v0 * kDescScale));
+                atomicAdd(&wacc[base + (o0 + 1) % 8], (unsigned long long)llrint(v1 * kDescScale));
+            }
+        }
+        __syncthreads();
     }
     __syncthreads();
-    if (tid < 128) vec[tid] = (float)((double)(long long)acc[tid] * kDescInv);
+    if (tid < 128) {
+        const unsigned long long t = acc[0][tid] + acc[1][tid] + acc[2][tid] + acc[3][tid];
+        vec[tid] = (float)((double)(long long)t * kDescInv);
+    }
     __syncthreads();
     if (tid == 0) sh_norm = sqrtf(sdot_skx(vec, 128)) * dp.max_value;
     __syncthreads();
@@ -607,13 +761,14 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint32_t));
     if (rc) return rc;
     uint32_t *raw_ext = (uint32_t *)ctx->frame_off;
-    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, (3 * (size_t)n + 8) * sizeof(int32_t));
+    const size_t cnt_ints = (3 * (size_t)n + 1) * kCntStride;
+    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, cnt_ints * sizeof(int32_t));
     if (rc) return rc;
-    int32_t *cand_cnt = ctx->counters;
-    int32_t *raw_cnt = ctx->counters + n;
-    int32_t *err = ctx->counters + 2 * n;
-    int32_t *ext_cnt = ctx->counters + 2 * n + 8;
-    PANO_HIP(ctx, hipMemsetAsync(ctx->counters, 0, (3 * (size_t)n + 8) * sizeof(int32_t), ctx->stream));
+    int32_t *err = ctx->counters;
+    int32_t *cand_cnt = err + kCntStride;
+    int32_t *raw_cnt = cand_cnt + (size_t)n * kCntStride;
+    int32_t *ext_cnt = raw_cnt + (size_t)n * kCntStride;
+    PANO_HIP(ctx, hipMemsetAsync(ctx->counters, 0, cnt_ints * sizeof(int32_t), ctx->stream));
 
     LocParams lp;
     lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);

@@ -17,10 +17,14 @@
 // per pass reproduces it exactly.  The x2 bilinear upsample of integer gray levels is exact.
 #include "pano_internal.h"
 
+#include <algorithm>
+#include <cstring>
+
 namespace {
 
 constexpr int TX = 64;
 constexpr int TY = 64;
+constexpr int TXP = TX + 1;   // odd trow pitch: row-pass stores are conflict-free
 
 struct Taps {
     double k[PANO_MAX_TAPS];
@@ -30,7 +34,7 @@ struct Taps {
 enum Mode { MODE_BASE = 0, MODE_LEVEL = 1, MODE_DOWN = 2 };
 
 struct LoadArgs {
-    const uint8_t *bgr;   // MODE_BASE: [n][sh][sw][3]
+    const uint8_t *gray;  // MODE_BASE: [n][sh][sw] u8 gray (cvtColor BGR2GRAY)
     const float *src;     // MODE_LEVEL: [n][H][W]; MODE_DOWN: [n][sh][sw]
     int sh, sw;           // source size (BASE: gray size; DOWN: previous octave size)
     double ifx, ify;      // DOWN: 1 / (dst / src), OpenCV resizeNN
@@ -48,31 +52,87 @@ __device__ __forceinline__ void lin_map(int d, int src_n, int &s0, int &s1, floa
     w1 = (float)fx;
 }
 
-template <int MODE>
-__device__ __forceinline__ float load_px(const LoadArgs &a, int f, int y, int x, int H, int W) {
-    if constexpr (MODE == MODE_LEVEL) {
-        return a.src[((size_t)f * H + y) * W + x];
-    } else if constexpr (MODE == MODE_DOWN) {
-        int sy = (int)floor(y * a.ify);
-        int sx = (int)floor(x * a.ifx);
-        sy = sy < a.sh - 1 ? sy : a.sh - 1;
-        sx = sx < a.sw - 1 ? sx : a.sw - 1;
-        return a.src[((size_t)f * a.sh + sy) * a.sw + sx];
-    } else {
-        // gray at (gy, gx) of the source frame, then x2 bilinear (exact for integers)
-        int y0, y1, x0, x1;
-        float wy, wx;
-        lin_map(y, a.sh, y0, y1, wy);
-        lin_map(x, a.sw, x0, x1, wx);
-        const uint8_t *fr = a.bgr + (size_t)f * a.sh * a.sw * 3;
-        const float g00 = gray_u8(fr + ((size_t)y0 * a.sw + x0) * 3);
-        const float g01 = gray_u8(fr + ((size_t)y0 * a.sw + x1) * 3);
-        const float g10 = gray_u8(fr + ((size_t)y1 * a.sw + x0) * 3);
-        const float g11 = gray_u8(fr + ((size_t)y1 * a.sw + x1) * 3);
-        const float wx0 = 1.0f - wx, wy0 = 1.0f - wy;
+// BORDER_REFLECT_101 with the in-range case first (interior tiles never take the slow path).
+__device__ __forceinline__ int reflect_fast(int i, int n) {
+    return (unsigned)i < (unsigned)n ? i : reflect101(i, n);
+}
+
+// Tile staging split into a per-lane column part (computed once per lane) and a per-row
+// part (wave-uniform), so the inner staging loop is one or a few loads per element.
+template <int MODE> struct Stager;
+
+template <> struct Stager<MODE_LEVEL> {
+    const float *src;
+    int W;
+    __device__ Stager(const LoadArgs &a, int f, int H, int W_, int x)
+        : src(a.src + (size_t)f * H * W_ + x), W(W_) {}
+    __device__ __forceinline__ float get(int gy) const { return src[(size_t)gy * W]; }
+};
+
+template <> struct Stager<MODE_DOWN> {   // OpenCV INTER_NEAREST 1/2 of the previous octave
+    const float *src;
+    int sx, sw, sh;
+    double ify;
+    __device__ Stager(const LoadArgs &a, int f, int H, int W, int x) {
+        (void)H;
+        (void)W;
+        src = a.src + (size_t)f * a.sh * a.sw;
+        sw = a.sw;
+        sh = a.sh;
+        ify = a.ify;
+        const int t = (int)floor(x * a.ifx);
+        sx = t < a.sw - 1 ? t : a.sw - 1;
+    }
+    __device__ __forceinline__ float get(int gy) const {
+        int sy = (int)floor(gy * ify);
+        sy = sy < sh - 1 ? sy : sh - 1;
+        return src[(size_t)sy * sw + sx];
+    }
+};
+
+template <> struct Stager<MODE_BASE> {   // gray (u8) -> x2 INTER_LINEAR, exact
+    const uint8_t *fr;
+    int c0, c1, sh, sw;
+    float wx, wx0;
+    __device__ Stager(const LoadArgs &a, int f, int H, int W, int x) {
+        (void)H;
+        (void)W;
+        sh = a.sh;
+        sw = a.sw;
+        fr = a.gray + (size_t)f * a.sh * a.sw;
+        lin_map(x, a.sw, c0, c1, wx);
+        wx0 = 1.0f - wx;
+    }
+    __device__ __forceinline__ float get(int gy) const {
+        int y0, y1;
+        float wy;
+        lin_map(gy, sh, y0, y1, wy);
+        const float g00 = fr[(size_t)y0 * sw + c0], g01 = fr[(size_t)y0 * sw + c1];
+        const float g10 = fr[(size_t)y1 * sw + c0], g11 = fr[(size_t)y1 * sw + c1];
         const float h0 = g00 * wx0 + g01 * wx;
         const float h1 = g10 * wx0 + g11 * wx;
-        return h0 * wy0 + h1 * wy;
+        return h0 * (1.0f - wy) + h1 * wy;
+    }
+};
+
+// cvtColor(BGR2GRAY) of every frame, 4 pixels per thread (sift_impl.py:27-28).
+__global__ void __launch_bounds__(256)
+gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t npx) {
+    const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 + 4 <= npx) {
+        const uint32_t *p = (const uint32_t *)(bgr + i0 * 3);   // 12 bytes, 4-aligned
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
+        uint8_t b[12];
+        for (int k = 0; k < 4; ++k) {
+            b[k] = (uint8_t)(w0 >> (8 * k));
+            b[4 + k] = (uint8_t)(w1 >> (8 * k));
+            b[8 + k] = (uint8_t)(w2 >> (8 * k));
+        }
+        uint32_t out = 0;
+        for (int k = 0; k < 4; ++k) out |= (uint32_t)gray_u8(b + 3 * k) << (8 * k);
+        *(uint32_t *)(gray + i0) = out;
+    } else {
+        for (size_t i = i0; i < npx; ++i) gray[i] = gray_u8(bgr + i * 3);
     }
 }
 
@@ -117,15 +177,19 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     const int IW = TX + 2 * r, IH = TY + 2 * r;
     const int IWP = IW | 1;                                  // odd row pitch: no bank conflicts
     float *tin = smem;                 // [IH][IWP]
-    float *trow = smem + IH * IWP;     // [IH][TX]
+    float *trow = smem + IH * IWP;     // [IH][TXP]
     const int tid = threadIdx.x;
     const int ih = th + 2 * r, iw = tw + 2 * r;              // staged extent actually needed
 
-    for (int i = tid; i < ih * iw; i += 256) {
-        const int ty = i / iw, tx = i - ty * iw;
-        const int gy = reflect101(y0 - r + ty, H);
-        const int gx = reflect101(x0 - r + tx, W);
-        tin[ty * IWP + tx] = load_px<MODE>(la, f, gy, gx, H, W);
+    {
+        // lane -> staged column tid % 128 (iw <= 64 + 62 < 128), rows step 2 per half-block
+        const int cx = tid & 127;
+        if (cx < iw) {
+            const Stager<MODE> sg(la, f, H, W, reflect_fast(x0 - r + cx, W));
+#pragma unroll 4
+            for (int ty = tid >> 7; ty < ih; ty += 2)
+                tin[ty * IWP + cx] = sg.get(reflect_fast(y0 - r + ty, H));
+        }
     }
     __syncthreads();
     if constexpr (NT > 0) {
@@ -136,7 +200,7 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
             double acc[SEG];
             conv_seg<NT, SEG>(tin + row * IWP + sg * SEG, 1, taps.k, acc);
 #pragma unroll
-            for (int j = 0; j < SEG; ++j) trow[row * TX + sg * SEG + j] = (float)acc[j];
+            for (int j = 0; j < SEG; ++j) trow[row * TXP + sg * SEG + j] = (float)acc[j];
         }
         __syncthreads();
         // column pass: lanes walk consecutive columns, each SEG outputs down y
@@ -144,7 +208,7 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         for (int it = tid; it < tw * nrs; it += 256) {
             const int x = it % tw, rs = it / tw;
             double acc[SEG];
-            conv_seg<NT, SEG>(trow + rs * SEG * TX + x, TX, taps.k, acc);
+            conv_seg<NT, SEG>(trow + rs * SEG * TXP + x, TXP, taps.k, acc);
 #pragma unroll
             for (int j = 0; j < SEG; ++j) {
                 const int ty = rs * SEG + j;
@@ -160,12 +224,12 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     } else {
         for (int i = tid; i < ih * tw; i += 256) {
             const int ty = i / tw, tx = i - ty * tw;
-            trow[ty * TX + tx] = (float)conv_one(tin + ty * IWP + tx, 1, taps.k, n);
+            trow[ty * TXP + tx] = (float)conv_one(tin + ty * IWP + tx, 1, taps.k, n);
         }
         __syncthreads();
         for (int i = tid; i < th * tw; i += 256) {
             const int ty = i / tw, tx = i - ty * tw;
-            const float o = (float)conv_one(trow + ty * TX + tx, TX, taps.k, n);
+            const float o = (float)conv_one(trow + ty * TXP + tx, TXP, taps.k, n);
             const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + tx;
             out[gi] = o;
             const float c = tin[(ty + r) * IWP + tx + r];
@@ -173,6 +237,110 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
             if (in_copy) in_copy[gi] = c;
         }
     }
+}
+
+// ------------------------------------------------------------------ small-octave tail
+// Octaves whose levels fit one 64 x 64 tile are latency-bound as separate launches (one
+// tiny workgroup per frame, ~7 us each, 5 per octave).  blur_tail runs them all in ONE
+// launch: a 1024-thread workgroup per frame keeps the current level in LDS and cascades
+// level by level, octave by octave (nearest 1/2 of level n_lvl-3 seeds the next octave),
+// writing every Gaussian level and DoG to HBM.  Per output it is the same arithmetic as
+// blur_level (sequential fma in tap order, one f32 rounding per pass), hence bit-identical.
+constexpr int kTailDim = 64;
+constexpr int kTailOct = 8;
+
+struct TailArgs {
+    const float *prev;                          // G[o_tail-1][n_lvl-3], frame stride ph*pw
+    int ph, pw;
+    float *G[kTailOct][PANO_MAX_LEVELS];        // level planes (frame 0)
+    float *D[kTailOct][PANO_MAX_LEVELS];        // DoG planes (frame 0)
+    int H[kTailOct], W[kTailOct];
+    int n_oct, n_lvl, rmax;
+    const double *taps;                         // [n_lvl][PANO_MAX_TAPS], level 0 unused
+    int ntap[PANO_MAX_LEVELS];
+};
+
+__device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_NEAREST
+    return (int)floor(d * inv);
+}
+
+__global__ void __launch_bounds__(1024)
+blur_tail(TailArgs ta) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    constexpr int NT = 1024, P = kTailDim;
+    const int HD = kTailDim + 2 * ta.rmax;        // halo tile side
+    const int HPP = HD | 1;
+    float *halo = smem + 3 * P * P;               // [HD][HPP]
+    float *rowt = halo + HD * HPP;                // [HD][P + 1]
+    double *tp = (double *)(((uintptr_t)(rowt + HD * (P + 1)) + 7) & ~(uintptr_t)7);
+    int cur = 0, keep = -1;
+    for (int oi = 0; oi < ta.n_oct; ++oi) {
+        const int H = ta.H[oi], W = ta.W[oi];
+        // ---- level 0: nearest 1/2 of the previous octave's level n_lvl-3
+        {
+            const int sh = oi == 0 ? ta.ph : ta.H[oi - 1];
+            const int sw = oi == 0 ? ta.pw : ta.W[oi - 1];
+            const double ifx = 1.0 / ((double)W / sw), ify = 1.0 / ((double)H / sh);
+            int dst = 0;
+            while (dst == keep) ++dst;
+            float *o0 = smem + dst * P * P;
+            float *g0 = ta.G[oi][0] + (size_t)f * H * W;
+            for (int i = tid; i < H * W; i += NT) {
+                const int y = i / W, x = i - (i / W) * W;
+                const int sy = min(tail_src(y, ify), sh - 1), sx = min(tail_src(x, ifx), sw - 1);
+                const float v = oi == 0 ? ta.prev[(size_t)f * sh * sw + (size_t)sy * sw + sx]
+                                        : smem[keep * P * P + sy * P + sx];
+                o0[y * P + x] = v;
+                g0[i] = v;
+            }
+            cur = dst;
+            keep = -1;
+            __syncthreads();
+        }
+        for (int l = 1; l < ta.n_lvl; ++l) {
+            const int n = ta.ntap[l], r = (n - 1) / 2;
+            const float *in = smem + cur * P * P;
+            int out = 0;
+            while (out == cur || out == keep) ++out;
+            if (tid < n) tp[tid] = ta.taps[l * PANO_MAX_TAPS + tid];
+            const int hh = H + 2 * r, hw = W + 2 * r;
+            for (int i = tid; i < hh * hw; i += NT) {
+                const int y = i / hw, x = i - (i / hw) * hw;
+                halo[y * HPP + x] = in[reflect101(y - r, H) * P + reflect101(x - r, W)];
+            }
+            __syncthreads();
+            for (int i = tid; i < hh * W; i += NT) {       // row pass
+                const int y = i / W, x = i - (i / W) * W;
+                const float *q = halo + y * HPP + x;
+                double acc = 0.0;
+                for (int t = 0; t < n; ++t) acc = fma(tp[t], (double)q[t], acc);
+                rowt[y * (P + 1) + x] = (float)acc;
+            }
+            __syncthreads();
+            float *g = ta.G[oi][l] + (size_t)f * H * W;
+            float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
+            for (int i = tid; i < H * W; i += NT) {        // column pass + DoG
+                const int y = i / W, x = i - (i / W) * W;
+                const float *q = rowt + y * (P + 1) + x;
+                double acc = 0.0;
+                for (int t = 0; t < n; ++t) acc = fma(tp[t], (double)q[t * (P + 1)], acc);
+                const float o = (float)acc;
+                smem[out * P * P + y * P + x] = o;
+                g[i] = o;
+                d[i] = o - in[y * P + x];
+            }
+            __syncthreads();
+            cur = out;
+            if (l == ta.n_lvl - 3) keep = cur;
+        }
+    }
+}
+
+size_t tail_smem_bytes(int rmax) {
+    const int HD = kTailDim + 2 * rmax;
+    return (size_t)(3 * kTailDim * kTailDim + HD * (HD | 1) + HD * (kTailDim + 1)) * sizeof(float) +
+           8 + PANO_MAX_TAPS * sizeof(double);
 }
 
 // getGaussianKernel(ksize, sigma, CV_32F) (cv2_compat.getGaussianKernel): f32 taps widened.
@@ -198,7 +366,7 @@ Taps make_taps(double sigma) {
 size_t smem_bytes(const Taps &t) {
     const int r = (t.n - 1) / 2;
     // trow rows are read up to SEG past the valid extent by the column pass: pad them
-    return (size_t)((TY + 2 * r) * ((TX + 2 * r) | 1) + (TY + 2 * r + SEG) * TX) * sizeof(float);
+    return (size_t)((TY + 2 * r) * ((TX + 2 * r) | 1) + (TY + 2 * r + SEG) * TXP) * sizeof(float);
 }
 
 template <int MODE, int NT>
@@ -321,17 +489,34 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     for (int l = 1; l < nl; ++l)
         if (tl[l].n < 0) return pano_fail(ctx, PANO_E_UNSUPPORTED, "Gaussian kernel too wide");
     float *G = ctx->pyr, *D = ctx->dog;
+    // gray frames (u8) for the base image
+    {
+        const size_t npx = (size_t)n * h * w;
+        rc = pano_grow(ctx, (void **)&ctx->gray, &ctx->gray_bytes, npx + 16);
+        if (rc) return rc;
+        const unsigned blocks = (unsigned)((npx + 1023) / 1024);
+        {
+            PanoProf prof_(ctx, PK_BLUR);
+            gray_frames<<<blocks, 256, 0, ctx->stream>>>(bgr, ctx->gray, npx);
+        }
+        PANO_LAUNCH_CHECK(ctx, "gray_frames");
+    }
+    // first octave of the fused small-octave tail (every level fits one 64 x 64 tile)
+    int o_tail = no;
+    for (int o = 1; o < no; ++o)
+        if (ctx->oct_h[o] <= kTailDim && ctx->oct_w[o] <= kTailDim) { o_tail = o; break; }
+    if (no - o_tail > kTailOct) o_tail = no - kTailOct;
     // octave 0, level 0: base image
     {
         LoadArgs la{};
-        la.bgr = bgr;
+        la.gray = ctx->gray;
         la.sh = h;
         la.sw = w;
         rc = launch_blur<MODE_BASE>(ctx, la, G + ctx->gauss_off[0][0], nullptr, nullptr, n,
                                     ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
     }
-    for (int o = 0; o < no; ++o) {
+    for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
         for (int l = 1; l < nl; ++l) {
             float *out = G + ctx->gauss_off[o][l];
@@ -353,6 +538,48 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
             }
             if (rc) return rc;
         }
+    }
+    if (o_tail < no) {
+        // device copy of the level taps (uploaded only when they change)
+        double th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
+        TailArgs ta{};
+        int rmax = 0;
+        for (int l = 1; l < nl; ++l) {
+            for (int t = 0; t < tl[l].n; ++t) th[l * PANO_MAX_TAPS + t] = tl[l].k[t];
+            ta.ntap[l] = tl[l].n;
+            rmax = std::max(rmax, (tl[l].n - 1) / 2);
+        }
+        if (!ctx->taps) {
+            PANO_HIP(ctx, hipMalloc((void **)&ctx->taps, sizeof(th)));
+            ctx->taps_valid = false;
+        }
+        if (!ctx->taps_valid || memcmp(th, ctx->taps_host, sizeof(th)) != 0) {
+            memcpy(ctx->taps_host, th, sizeof(th));
+            PANO_HIP(ctx, hipMemcpy(ctx->taps, ctx->taps_host, sizeof(th), hipMemcpyHostToDevice));
+            ctx->taps_valid = true;
+        }
+        ta.taps = ctx->taps;
+        ta.rmax = rmax;
+        ta.prev = G + ctx->gauss_off[o_tail - 1][nl - 3];
+        ta.ph = ctx->oct_h[o_tail - 1];
+        ta.pw = ctx->oct_w[o_tail - 1];
+        ta.n_oct = no - o_tail;
+        ta.n_lvl = nl;
+        for (int oi = 0; oi < ta.n_oct; ++oi) {
+            const int o = o_tail + oi;
+            ta.H[oi] = ctx->oct_h[o];
+            ta.W[oi] = ctx->oct_w[o];
+            for (int l = 0; l < nl; ++l) ta.G[oi][l] = G + ctx->gauss_off[o][l];
+            for (int l = 0; l + 1 < nl; ++l) ta.D[oi][l] = D + ctx->dog_off[o][l];
+        }
+        const size_t sm = tail_smem_bytes(rmax);
+        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_tail,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        {
+            PanoProf prof_(ctx, PK_BLUR);
+            blur_tail<<<n, 1024, sm, ctx->stream>>>(ta);
+        }
+        PANO_LAUNCH_CHECK(ctx, "blur_tail");
     }
     return PANO_OK;
 }
