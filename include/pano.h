@@ -133,11 +133,13 @@ int pano_harris(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w, int ma
  * Brute-force L2 nearest neighbour of every row of A among rows of B
  * (image_stitching_sift.py:63-79, image_stitching_harris.py:219-240).
  * exact_int == 1: descriptors are integers in [0,255] (SIFT): fp32 MFMA distance GEMM
- *   (v_mfma_f32_32x32x2_f32), distances exact.
- * exact_int == 2: same inputs, staged as bf16 and multiplied with v_mfma_f32_32x32x16_bf16:
- *   bit-identical results (integers <= 255 are exact in bf16; every product and partial
- *   sum is an integer < 2^24, exact in the f32 accumulator), 16x the MFMA rate.  exact_int == 0 (Harris): direct fp32 differences summed in the
- *   OpenBLAS sdot order numpy uses.
+ *   (v_mfma_f32_32x32x2_f32, LDS-staged), distances exact.
+ * exact_int == 2 (the Stitcher default): same inputs, packed once to bf16 rows + norms and
+ *   multiplied with v_mfma_f32_32x32x16_bf16 from register-loaded fragments: bit-identical
+ *   results (integers <= 255 are exact in bf16; every product and partial sum is an integer
+ *   < 2^24, exact in the f32 accumulator).
+ * exact_int == 0 (Harris): direct fp32 differences summed in the OpenBLAS sdot order numpy
+ *   uses.
  * Batched over pairs: pair p matches frame h_pairs[2p] (A) against h_pairs[2p+1] (B) of a
  * [frames][cap][128] descriptor array with d_counts[frames].
  * Outputs per pair p, row i (< cap): d_best[p][i] (first minimum, -1 if B empty),

@@ -3,16 +3,20 @@
 //   SIFT  (image_stitching_sift.py:63-79): for each i, argmin_j ||dA_i - dB_j||^2 with a
 //         strict '<' scan (first j wins ties).  Descriptors are integers in [0, 255], so
 //         ||a||^2 + ||b||^2 - 2 a.b is an exact integer < 2^24 in f32 whatever the order:
-//         the distance matrix is an fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32, exact f32
-//         fma chains) with the argmin / second-min fused into the epilogue.
+//         the distance matrix is an MFMA GEMM with the argmin / second-min fused into the
+//         epilogue.  Two exact variants:
+//           bf16 (default, exact_int = 2): pack_rows -> bf16 rows + norms once per frame;
+//                dist_bf16 loads MFMA fragments straight into registers (no LDS staging)
+//                and runs v_mfma_f32_32x32x16_bf16 (integers 0..255 are exact in bf16);
+//           f32  (exact_int = 1): dist_mfma, LDS-staged K chunks, v_mfma_f32_32x32x2_f32.
 //   Harris (image_stitching_harris.py:219-240): float descriptors; numpy's np.dot(diff,
 //         diff) is OpenBLAS sdot, whose summation order is reproduced exactly
 //         (oracle/numerics.py::sdot_skx), one distance per thread.
 //
 // Workgroup tile: 128 (rows of A) x 128 (rows of B), 4 waves as 2 x 2, each wave 64 x 64 =
-// 2 x 2 MFMA blocks of 32 x 32; K = 128 streamed through LDS in 4 chunks of 32.
-// Per (row, column tile) the workgroup writes (best, index, second) partials; a reduce
-// kernel folds the column tiles in index order.  Roofline unit M1 = 2*N*M*128 flop/pair.
+// 2 x 2 MFMA blocks of 32 x 32.  Per (row, column tile) the workgroup writes (best, index,
+// second) partials; reduce_parts folds the column tiles in index order.
+// Roofline unit M1 = 2*N*M*128 flop/pair.
 #include "pano_internal.h"
 
 namespace {
@@ -61,13 +65,11 @@ struct PairArg {
 // below 2^24); otherwise v_mfma_f32_32x32x2_f32 in 4 K-chunks of 32.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int KP_BF = PANO_DESC_DIM + 8;   // bf16 row pitch (272 B): conflict-free b128 reads
 
 __device__ __forceinline__ unsigned short f32_to_bf16_exact(float v) {
     return (unsigned short)(__float_as_uint(v) >> 16);   // exact for integers 0..255
 }
 
-template <bool BF16>
 __global__ void __launch_bounds__(256)
 dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
           const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
@@ -94,34 +96,7 @@ dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
         for (int b = 0; b < 2; ++b)
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
-    if constexpr (BF16) {
-        unsigned short *Ab = (unsigned short *)smem;          // [MT][KP_BF]
-        unsigned short *Bb = Ab + MT * KP_BF;                  // [MT][KP_BF]
-        for (int q = tid; q < MT * PANO_DESC_DIM / 4; q += 256) {
-            const int row = q / (PANO_DESC_DIM / 4), c4 = (q % (PANO_DESC_DIM / 4)) * 4;
-            float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-            if (i0 + row < NA) va = *(const float4 *)(dA + (size_t)(i0 + row) * PANO_DESC_DIM + c4);
-            if (j0 + row < NB) vb = *(const float4 *)(dB + (size_t)(j0 + row) * PANO_DESC_DIM + c4);
-            ushort4 ua = make_ushort4(f32_to_bf16_exact(va.x), f32_to_bf16_exact(va.y),
-                                      f32_to_bf16_exact(va.z), f32_to_bf16_exact(va.w));
-            ushort4 ub = make_ushort4(f32_to_bf16_exact(vb.x), f32_to_bf16_exact(vb.y),
-                                      f32_to_bf16_exact(vb.z), f32_to_bf16_exact(vb.w));
-            *(ushort4 *)(Ab + row * KP_BF + c4) = ua;
-            *(ushort4 *)(Bb + row * KP_BF + c4) = ub;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int kk = 0; kk < PANO_DESC_DIM; kk += 16) {
-            bf16x8 fj[2], fi[2];
-            for (int m = 0; m < 2; ++m) {
-                fj[m] = *(const bf16x8 *)(Bb + (wj * 64 + m * 32 + lr) * KP_BF + kk + 8 * lh);
-                fi[m] = *(const bf16x8 *)(Ab + (wi * 64 + m * 32 + lr) * KP_BF + kk + 8 * lh);
-            }
-            for (int a = 0; a < 2; ++a)
-                for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a], fi[b], acc[a][b], 0, 0, 0);
-        }
-    } else {
+    {
         float *As = (float *)smem;          // [MT][LDA]
         float *Bs = As + MT * LDA;          // [MT][LDA]
         for (int k0 = 0; k0 < PANO_DESC_DIM; k0 += KC) {
@@ -167,6 +142,129 @@ dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
                 }
             }
         }
+        const float ob = __shfl_xor(best, 32);
+        const int oj = __shfl_xor(bj, 32);
+        const float os = __shfl_xor(second, 32);
+        merge(best, bj, second, ob, oj, os);
+        if (lh == 0) red[wj][il] = Part{best, bj, second};
+    }
+    __syncthreads();
+    if (tid < MT) {
+        Part x = red[0][tid];
+        const Part y = red[1][tid];
+        float bb = x.best, ss = x.second;
+        int jj = x.idx;
+        merge(bb, jj, ss, y.best, y.idx, y.second);
+        const int gi = i0 + tid;
+        if (gi < NA) parts[((size_t)p * n_jt + blockIdx.x) * cap + gi] = Part{bb, jj, ss};
+    }
+}
+
+// ---------------------------------------------------------------- bf16 path (default)
+// pack_rows: one pass over the live descriptor rows -> bf16 rows (exact: integers 0..255)
+// + exact f32 norms.  16 threads per row, 8 elements each; the norm partials are integers
+// < 2^24, so the shuffle reduction is exact in any order.
+__global__ void __launch_bounds__(256)
+pack_rows(const float *__restrict__ desc, const int32_t *__restrict__ counts, int cap,
+          int n_frames, unsigned short *__restrict__ pk, float *__restrict__ norms) {
+    const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t row = gid >> 4;
+    const int part = (int)(gid & 15);
+    if (row >= (size_t)n_frames * cap) return;
+    const int f = (int)(row / cap), r = (int)(row % cap);
+    int cnt = counts[f];
+    cnt = cnt < cap ? cnt : cap;
+    const bool live = r < cnt;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (live) {
+        const float4 *src = (const float4 *)(desc + row * PANO_DESC_DIM + part * 8);
+        a = src[0];
+        b = src[1];
+    }
+    float s = a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z +
+              b.w * b.w;
+    for (int d = 8; d > 0; d >>= 1) s += __shfl_xor(s, d, 16);
+    if (!live) return;
+    ushort4 u0 = make_ushort4(f32_to_bf16_exact(a.x), f32_to_bf16_exact(a.y),
+                              f32_to_bf16_exact(a.z), f32_to_bf16_exact(a.w));
+    ushort4 u1 = make_ushort4(f32_to_bf16_exact(b.x), f32_to_bf16_exact(b.y),
+                              f32_to_bf16_exact(b.z), f32_to_bf16_exact(b.w));
+    ushort4 *dst = (ushort4 *)(pk + row * PANO_DESC_DIM + part * 8);
+    dst[0] = u0;
+    dst[1] = u1;
+    if (part == 0) norms[row] = s;
+}
+
+// dist_bf16: 128 x 128 tile per workgroup, 4 waves as 2 (j) x 2 (i), each 64 x 64 = 2 x 2
+// v_mfma_f32_32x32x16_bf16 blocks.  Every wave loads its A / B fragments for the whole
+// K = 128 straight from the packed rows into registers (32 independent 16-byte loads: one
+// memory round trip), then issues 32 MFMAs and folds argmin / second-min in registers.
+// Rows past the live count are clamped to a live row and masked in the epilogue.
+__global__ void __launch_bounds__(256)
+dist_bf16(const unsigned short *__restrict__ pk, const float *__restrict__ norms,
+          const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
+          int n_jt) {
+    __shared__ float nB[MT];
+    __shared__ Part red[2][MT];
+    const int p = blockIdx.z;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    int NA = counts[fa], NB = counts[fb];
+    NA = NA < cap ? NA : cap;
+    NB = NB < cap ? NB : cap;
+    const int i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
+    if (i0 >= NA || j0 >= NB) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wj = wv >> 1, wi = wv & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    const unsigned short *rA = pk + (size_t)fa * cap * PANO_DESC_DIM;
+    const unsigned short *rB = pk + (size_t)fb * cap * PANO_DESC_DIM;
+    if (tid < MT) nB[tid] = j0 + tid < NB ? norms[(size_t)fb * cap + j0 + tid] : 0.0f;
+    bf16x8 fj[2][8], fi[2][8];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int jr = min(j0 + wj * 64 + m * 32 + lr, NB - 1);
+        const int ir = min(i0 + wi * 64 + m * 32 + lr, NA - 1);
+        const bf16x8 *qj = (const bf16x8 *)(rB + (size_t)jr * PANO_DESC_DIM + 8 * lh);
+        const bf16x8 *qi = (const bf16x8 *)(rA + (size_t)ir * PANO_DESC_DIM + 8 * lh);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            fj[m][k] = qj[2 * k];
+            fi[m][k] = qi[2 * k];
+        }
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a][k], fi[b][k], acc[a][b], 0, 0, 0);
+    __syncthreads();                                    // nB
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int il = wi * 64 + b * 32 + lr;
+        const float na = i0 + il < NA ? norms[(size_t)fa * cap + i0 + il] : 0.0f;
+        float best = INFINITY, second = INFINITY;
+        int bj = 0x7fffffff;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {       // j increasing within the lane: strict <
+                const int jl = wj * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const float d = (na + nB[jl]) - 2.0f * acc[a][b][r];
+                const bool ok = j0 + jl < NB;
+                const bool lt = ok && d < best;
+                second = lt ? best : (ok ? fminf(second, d) : second);
+                bj = lt ? j0 + jl : bj;
+                best = lt ? d : best;
+            }
         const float ob = __shfl_xor(best, 32);
         const int oj = __shfl_xor(bj, 32);
         const float os = __shfl_xor(second, 32);
@@ -280,12 +378,7 @@ dist_direct(const float *__restrict__ desc, const int32_t *__restrict__ counts, 
 
 }  // namespace
 
-int match_set_attributes(pano_ctx *ctx) {
-    const int sm = 2 * MT * KP_BF * (int)sizeof(unsigned short);
-    PANO_HIP(ctx, hipFuncSetAttribute((const void *)dist_mfma<true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    return PANO_OK;
-}
+int match_set_attributes(pano_ctx *) { return PANO_OK; }
 
 int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
                  const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
@@ -320,20 +413,33 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
         float *norms = (float *)ctx->mscratch;
         Part *parts = (Part *)((char *)ctx->mscratch + norm_bytes);
         const size_t rows = (size_t)n_frames * cap;
-        {
-            PanoProf prof_(ctx, PK_NORMS);
-            row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
-        }
-        PANO_LAUNCH_CHECK(ctx, "row_norms");
         dim3 grid(n_t, n_t, np);
         if (exact_int == 2) {
-            const size_t sm = 2 * (size_t)MT * KP_BF * sizeof(unsigned short);
+            // packed bf16 rows live after the partials
+            const size_t pk_off = (norm_bytes + part_bytes + 255) & ~size_t(255);
+            rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes,
+                           pk_off + rows * PANO_DESC_DIM * sizeof(unsigned short));
+            if (rc) return rc;
+            norms = (float *)ctx->mscratch;
+            parts = (Part *)((char *)ctx->mscratch + norm_bytes);
+            unsigned short *pk = (unsigned short *)((char *)ctx->mscratch + pk_off);
+            {
+                PanoProf prof_(ctx, PK_NORMS);
+                pack_rows<<<(unsigned)((rows * 16 + 255) / 256), 256, 0, ctx->stream>>>(
+                    desc, counts, cap, n_frames, pk, norms);
+            }
+            PANO_LAUNCH_CHECK(ctx, "pack_rows");
             PanoProf prof_(ctx, PK_DIST_MFMA);
-            dist_mfma<true><<<grid, 256, sm, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+            dist_bf16<<<grid, 256, 0, ctx->stream>>>(pk, norms, counts, cap, pa, parts, n_t);
         } else {
+            {
+                PanoProf prof_(ctx, PK_NORMS);
+                row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
+            }
+            PANO_LAUNCH_CHECK(ctx, "row_norms");
             const size_t sm = 2 * (size_t)MT * LDA * sizeof(float);
             PanoProf prof_(ctx, PK_DIST_MFMA);
-            dist_mfma<false><<<grid, 256, sm, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
+            dist_mfma<<<grid, 256, sm, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
         }
         PANO_LAUNCH_CHECK(ctx, "dist_mfma");
         dim3 g2((cap + 255) / 256, np);

@@ -29,6 +29,14 @@ constexpr float kRad2DegF32 = 180.0f / 3.14159265358979323846f;   // numpy f32 r
 constexpr double kHistScale = 1099511627776.0;                    // 2^40 fixed point
 constexpr double kHistInv = 1.0 / 1099511627776.0;
 constexpr double kDescScale = 1099511627776.0;
+
+// llrint for |x| < 2^51 in two instructions: adding 1.5 * 2^52 rounds to an integer (ties to
+// even, as llrint in the default mode) and leaves it in the low mantissa bits.  Histogram
+// contributions are < 2^9 * 2^40, far inside the range.
+__device__ __forceinline__ unsigned long long rint_fix(double x) {
+    const double magic = 6755399441055744.0;
+    return (unsigned long long)(__double_as_longlong(x + magic) - __double_as_longlong(magic));
+}
 constexpr double kDescInv = 1.0 / 1099511627776.0;
 constexpr int kSortMax = 8192;
 
@@ -408,7 +416,7 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             const float w = expf(wfac * (float)(dx * dx + dy * dy));
             const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
             const double val = (double)(w * mag);
-            atomicAdd(&hist[wv][bin], (unsigned long long)llrint(val * kHistScale));
+            atomicAdd(&hist[wv][bin], rint_fix(val * kHistScale));
         }
     }
     __syncthreads();
@@ -713,8 +721,8 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
                 const double v0 = part[q] * (1 - of);
                 const double v1 = part[q] * of;
-                atomicAdd(&wacc[base + o0], (unsigned long long)llrint(v0 * kDescScale));
-                atomicAdd(&wacc[base + (o0 + 1) % 8], (unsigned long long)llrint(v1 * kDescScale));
+                atomicAdd(&wacc[base + o0], rint_fix(v0 * kDescScale));
+                atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1 * kDescScale));
             }
         }
         __syncthreads();

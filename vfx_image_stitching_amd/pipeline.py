@@ -70,7 +70,7 @@ class Stitcher:
                                  else (25000 if method == "sift" else 1.0))
         self.params = _lib.default_sift_params(**(sift_params or {}))
         # SIFT distance GEMM: "bf16" (exact for integer descriptors, 16x MFMA rate) or "f32"
-        self.match = match or os.environ.get("PANO_MATCH", "f32")
+        self.match = match or os.environ.get("PANO_MATCH", "bf16")
         self._buf = {}
 
     # ------------------------------------------------------------------ buffers
