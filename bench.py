@@ -190,6 +190,11 @@ def main():
                     "launches_per_step": launches_per_step,
                     "kernel_ms_per_step": round(per_step_ms, 4)}
 
+    # correctness of what was timed: the single-GPU panorama against the reference's digest
+    parity = None
+    if world == 1 and args.workload != "synthetic":
+        parity = check_parity(st, dev, focals, margin, args.workload, args.method)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "synthetic":
         cpu = cpu_baseline(frames, focals, args.cpu_frames, args.method, h, w)
@@ -208,12 +213,29 @@ def main():
                    "method": args.method, "match_gemm": st.match},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "parity": parity,
         "kernels_ms_per_step": {k: round(v["total_ms"], 4) for k, v in per_kernel.items()},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def check_parity(st, dev, focals, margin, workload, method):
+    """Panorama of the benchmarked sequence vs the reference's (tests/golden digest)."""
+    import hashlib
+    path = os.path.join(ROOT, "tests", "golden", f"{method}_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    gold = json.load(open(path))
+    pano = np.ascontiguousarray(st.run(dev, focals, margin=margin).panorama.cpu().numpy())
+    h = hashlib.sha256()
+    h.update(f"{pano.dtype.str}{pano.shape}".encode())
+    h.update(pano.tobytes())
+    ok = h.hexdigest() == gold["pano_digest"]
+    return {"panorama_bit_exact_vs_reference": ok, "shape": list(pano.shape),
+            "psnr_db": "inf" if ok else None}
 
 
 def cpu_baseline(frames, focals, n, method, h, w):

@@ -91,9 +91,14 @@ int pano_ctx_create(int device, void *stream, pano_ctx **out) {
 
 int pano_ctx_destroy(pano_ctx *ctx) {
     if (!ctx) return PANO_OK;
+    sift_join_tail(ctx);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
-                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray};
+                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
@@ -103,6 +108,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
 
 int pano_ctx_set_stream(pano_ctx *ctx, void *stream) {
     if (!ctx) return PANO_E_ARG;
+    sift_join_tail(ctx);
     ctx->stream = (hipStream_t)stream;
     return PANO_OK;
 }
@@ -148,9 +154,10 @@ int pano_sift(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     if (!ctx) return PANO_E_ARG;
     pano_sift_params p;
     if (params) p = *params; else pano_sift_default_params(&p);
-    int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p);
-    if (rc) return rc;
-    return launch_sift_keypoints(ctx, &p, kps, desc, cap, counts);
+    int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true);
+    if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, desc, cap, counts);
+    sift_join_tail(ctx);                  // no-op unless an error left the tail unjoined
+    return rc;
 }
 
 int pano_sift_level_shape(pano_ctx *ctx, int octave, int *h_out, int *w_out, int *n_octaves) {

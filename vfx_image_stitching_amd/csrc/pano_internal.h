@@ -82,6 +82,7 @@ struct pano_ctx {
     int32_t *frame_off = nullptr;        // raw extrema (scan keys) before localisation
     size_t ext_bytes = 0;
     RawKp *raw_sorted = nullptr;
+    uint32_t *sorted = nullptr; size_t sorted_bytes = 0;   // per-frame sorted raw indices
     double *taps = nullptr;              // device Gaussian taps, per level [L][PANO_MAX_TAPS]
     double taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // what *taps holds
     bool taps_valid = false;
@@ -94,16 +95,30 @@ struct pano_ctx {
     void *hscratch = nullptr; size_t hscratch_bytes = 0;
     // ---- blend scratch
     void *bscratch = nullptr; size_t bscratch_bytes = 0;
+    // ---- side stream: the small-octave blur tail runs there, overlapped with the extrema
+    // scan of the large octaves (fork / join by events; see launch_sift_pyramid)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool tail_pending = false;           // blur_tail enqueued on `side`, not yet joined
+    int o_tail = 0;                      // first octave of the tail
     // ---- live profiler
     ProfState prof;
 };
+
+// Make ctx->stream wait for a pending blur tail (no-op otherwise).
+inline void sift_join_tail(pano_ctx *ctx) {
+    if (!ctx->tail_pending) return;
+    (void)hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0);
+    ctx->tail_pending = false;
+}
 
 // RAII: records a start/stop hipEvent pair on the context's stream around one launch
 // when the profiler is enabled for this kernel class.
 struct PanoProf {
     pano_ctx *ctx;
+    hipStream_t st;
     bool on;
-    PanoProf(pano_ctx *c, int kid) : ctx(c), on(false) {
+    PanoProf(pano_ctx *c, int kid, hipStream_t s = nullptr) : ctx(c), st(s ? s : c->stream), on(false) {
         ProfState &p = c->prof;
         if (p.kernel != kid && p.kernel != PK_COUNT) return;
         if (p.used + 2 > p.ev.size()) {
@@ -115,12 +130,12 @@ struct PanoProf {
         }
         p.kid.resize(p.ev.size() / 2);
         p.kid[p.used / 2] = kid;
-        on = hipEventRecord(p.ev[p.used], c->stream) == hipSuccess;
+        on = hipEventRecord(p.ev[p.used], st) == hipSuccess;
     }
     ~PanoProf() {
         if (!on) return;
         ProfState &p = ctx->prof;
-        (void)hipEventRecord(p.ev[p.used + 1], ctx->stream);
+        (void)hipEventRecord(p.ev[p.used + 1], st);
         p.used += 2;
     }
 };
@@ -145,7 +160,7 @@ int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need);
 int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
                        const double *h_focal, uint8_t *colnz);
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
-                        const pano_sift_params *p);
+                        const pano_sift_params *p, bool defer_tail = false);
 int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
                           int cap, int32_t *counts);
 int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int max_points,

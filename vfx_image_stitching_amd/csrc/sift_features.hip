@@ -4,16 +4,18 @@
 //                     (LDS-tiled, every octave in one launch)
 //   localize          localize_extremum_via_quadratic_fit :169-211 (thread per candidate)
 //   orientation       compute_keypoints_with_orientations :246-293 (wave per candidate)
-//   sort_dedup        compare_keypoints / remove_duplicate_keypoints :299-327
-//                     + convert_keypoints_to_input_image_size :333-343 (workgroup per frame)
+//   rank_keys         compare_keypoints :299-316 (rank = sorted slot, whole-GPU all-pairs)
+//   emit_keypoints    remove_duplicate_keypoints :319-327 + convert_keypoints_to_input_image_size
+//                     :333-343 (workgroup per frame)
 //   descriptor        unpack_octave :349-358 + generate_descriptors :361-526
 //                     (workgroup per keypoint)
 //
 // Parity notes (DESIGN.md "Parity"):
 //  * extrema decisions are exact f32 comparisons; the cube / gradient / Hessian are the
 //    reference's f32 expressions in its evaluation order (no contraction);
-//  * lstsq (numpy: LAPACK dgelsd in double, result cast to f32) is a Jacobi
-//    pseudo-inverse in double with numpy's rcond = 3 * DBL_EPSILON cut;
+//  * lstsq (numpy: LAPACK dgelsd in double, result cast to f32) is an LU solve with partial
+//    pivoting in double, falling back to a Jacobi pseudo-inverse with numpy's
+//    rcond = 3 * DBL_EPSILON cut when the Hessian is near-singular;
 //  * np.dot of two 3-vectors = f32 products summed in double (OpenBLAS tail loop);
 //  * histograms accumulate in 64-bit fixed point (order independent => deterministic, and
 //    more accurate than the reference's sequential sums);
@@ -29,6 +31,15 @@ constexpr float kRad2DegF32 = 180.0f / 3.14159265358979323846f;   // numpy f32 r
 constexpr double kHistScale = 1099511627776.0;                    // 2^40 fixed point
 constexpr double kHistInv = 1.0 / 1099511627776.0;
 constexpr double kDescScale = 1099511627776.0;
+
+// a / b correctly rounded from y = RN(1 / b) (Markstein): q = RN(a y) is within one ulp, the
+// remainder a - b q is exact under fma, and RN(q + r y) is the correctly rounded quotient
+// (no under/overflow here: |a| < 2^12, b > 2^-4).  Same value as the hardware divide.
+__device__ __forceinline__ double div_rn(double a, double b, double y) {
+    const double q = a * y;
+    const double r = fma(-q, b, a);
+    return fma(r, y, q);
+}
 
 // llrint for |x| < 2^51 in two instructions: adding 1.5 * 2^52 rounds to an integer (ties to
 // even, as llrint in the default mode) and leaves it in the low mantissa bits.  Histogram
@@ -110,6 +121,39 @@ __device__ void lstsq3_sym(const double A[3][3], const double b[3], double x[3])
     }
 }
 
+// Well-conditioned fast path for the same solve: LU with partial pivoting in double.
+// dgelsd and LU both land within ~cond * 1e-16 of the exact solution, far below the f32
+// rounding the result goes through; near-singular Hessians (a pivot under 1e-6 of the
+// largest entry, i.e. cond >~ 1e6) take the Jacobi pseudo-inverse, which reproduces
+// dgelsd's rank cut.  Returns false when the fallback is needed.
+__device__ __forceinline__ bool solve3_lu(const double A[3][3], const double b[3], double x[3]) {
+    double a0[3] = {A[0][0], A[0][1], A[0][2]}, a1[3] = {A[1][0], A[1][1], A[1][2]},
+           a2[3] = {A[2][0], A[2][1], A[2][2]};
+    double r0 = b[0], r1 = b[1], r2 = b[2];
+    double amax = 0.0;
+    for (int j = 0; j < 3; ++j) amax = fmax(amax, fmax(fabs(a0[j]), fmax(fabs(a1[j]), fabs(a2[j]))));
+    const double tol = 1e-6 * amax;
+    auto swp = [](double (&u)[3], double (&v)[3], double &ru, double &rv) {
+        for (int j = 0; j < 3; ++j) { const double t = u[j]; u[j] = v[j]; v[j] = t; }
+        const double t = ru; ru = rv; rv = t;
+    };
+    if (fabs(a1[0]) > fabs(a0[0]) && fabs(a1[0]) >= fabs(a2[0])) swp(a0, a1, r0, r1);
+    else if (fabs(a2[0]) > fabs(a0[0])) swp(a0, a2, r0, r2);
+    if (!(fabs(a0[0]) > tol)) return false;
+    const double l1 = a1[0] / a0[0], l2 = a2[0] / a0[0];
+    a1[1] -= l1 * a0[1]; a1[2] -= l1 * a0[2]; r1 -= l1 * r0;
+    a2[1] -= l2 * a0[1]; a2[2] -= l2 * a0[2]; r2 -= l2 * r0;
+    if (fabs(a2[1]) > fabs(a1[1])) swp(a1, a2, r1, r2);
+    if (!(fabs(a1[1]) > tol)) return false;
+    const double l = a2[1] / a1[1];
+    a2[2] -= l * a1[2]; r2 -= l * r1;
+    if (!(fabs(a2[2]) > tol)) return false;
+    x[2] = r2 / a2[2];
+    x[1] = (r1 - a1[2] * x[2]) / a1[1];
+    x[0] = (r0 - a0[1] * x[1] - a0[2] * x[2]) / a0[0];
+    return true;
+}
+
 // ------------------------------------------------------------------ S5 + S6
 // S5: one launch covers every octave: workgroup = one 64 x 8 tile of the interior of one
 // octave of one frame; the ni+2 DoG levels of the tile (+1 halo) are staged in LDS and each
@@ -131,11 +175,11 @@ __device__ __forceinline__ uint32_t scan_key(int o, int layer0, int y, int x) {
 
 __global__ void __launch_bounds__(256)
 extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict__ raw,
-             int32_t *__restrict__ raw_cnt, int raw_cap) {
+             int32_t *__restrict__ raw_cnt, int raw_cap, int tile_base) {
     __shared__ float s[PANO_MAX_LEVELS - 1][ETY + 2][ETX + 2];
     __shared__ int wtot[4], wbase;
     const int f = blockIdx.y;
-    int t = blockIdx.x, o = 0;
+    int t = blockIdx.x + tile_base, o = 0;
     while (o + 1 < a.n_oct && t >= a.tile_start[o + 1]) ++o;
     t -= a.tile_start[o];
     const int H = a.H[o], W = a.W[o];
@@ -144,34 +188,44 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
     const int tid = threadIdx.x;
     const int nl = ni + 2;
     // stage the ni+2 DoG levels of the tile (+1 halo): wave w stages rows w, w+4, ... of the
-    // (level, row) list, lane = column (lanes 0,1 also take the two right-halo columns);
-    // level / row are wave-uniform and 8 rows are in flight per lane.
+    // (level, row) list with lane = column; the two right-halo columns of every row are one
+    // extra load per thread.  Level / row are wave-uniform and all of a thread's loads are
+    // issued before the first LDS store (one memory round trip for ni <= 3).
     const int lane = tid & 63, wv = tid >> 6;
     const int nrows = nl * (ETY + 2);
     const int gxa = min(x0 - 1 + lane, W - 1);
-    const int gxb = min(x0 - 1 + 64 + lane, W - 1);
-    for (int r0 = wv; r0 < nrows; r0 += 4 * 8) {
-        float va[8], vb[8];
+    constexpr int RB = 24;                       // rows per wave per batch (90 rows at ni = 3)
+    for (int r0 = wv; r0 < nrows; r0 += 4 * RB) {
+        float va[RB];
+        float vh = 0.0f;
+        const int hr = r0 - wv + (tid >> 1);       // right-halo: (row, column 64 + (tid & 1))
+        const bool hv = (tid >> 1) < 4 * RB && hr < nrows;
+        if (hv) {
+            const int l = hr / (ETY + 2), yy = hr - l * (ETY + 2);
+            const int gy = min(y0 - 1 + yy, H - 1);
+            vh = a.dog[o][l][((size_t)f * H + gy) * W + min(x0 + 63 + (tid & 1), W - 1)];
+        }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < RB; ++u) {
             const int rr = r0 + 4 * u;
-            va[u] = vb[u] = 0.0f;
+            va[u] = 0.0f;
             if (rr < nrows) {
                 const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
                 const int gy = min(y0 - 1 + yy, H - 1);
-                const float *row = a.dog[o][l] + ((size_t)f * H + gy) * W;
-                va[u] = row[gxa];
-                if (lane < ETX + 2 - 64) vb[u] = row[gxb];
+                va[u] = a.dog[o][l][((size_t)f * H + gy) * W + gxa];
             }
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < RB; ++u) {
             const int rr = r0 + 4 * u;
             if (rr < nrows) {
                 const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
                 s[l][yy][lane] = va[u];
-                if (lane < ETX + 2 - 64) s[l][yy][64 + lane] = vb[u];
             }
+        }
+        if (hv) {
+            const int l = hr / (ETY + 2), yy = hr - l * (ETY + 2);
+            s[l][yy][64 + (tid & 1)] = vh;
         }
     }
     __syncthreads();
@@ -284,7 +338,7 @@ __device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint32_t key
             b[i] = g[i];
             for (int j = 0; j < 3; ++j) A[i][j] = Hs[i][j];
         }
-        lstsq3_sym(A, b, sol);
+        if (!solve3_lu(A, b, sol)) lstsq3_sym(A, b, sol);
         for (int i = 0; i < 3; ++i) u[i] = -(float)sol[i];
         if (fabsf(u[0]) < 0.5f && fabsf(u[1]) < 0.5f && fabsf(u[2]) < 0.5f) break;
         xi += (int)rintf(u[0]);
@@ -484,55 +538,95 @@ __device__ __forceinline__ bool rec_before(const RawKp &a, const RawKp &b) {
     return a.order < b.order;
 }
 
+// The reference's sort (compare_keypoints, stable) is a strict total order once scan order
+// breaks ties, so each keypoint's sorted position is its RANK: rank_keys counts, for every
+// raw keypoint, how many keys of its frame precede it -- ~count^2 compares per frame spread
+// over the whole GPU, keys staged through LDS in chunks -- and scatters its index to that
+// slot.  emit_keypoints then de-duplicates neighbours and converts (one workgroup per frame).
+constexpr int kRankChunk = 2048;
+
+// Block = 64 keypoints x 4 waves: wave q counts, for its lane's keypoint, the keys of
+// quarter q of each LDS chunk that sort before it (8 keys per step, one pass; the full
+// comparator only on a step holding an equal (x, y) key); the 4 partial ranks are summed.
+__global__ void __launch_bounds__(256)
+rank_keys(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
+          uint32_t *__restrict__ sorted) {
+    __shared__ unsigned long long ks[kRankChunk];
+    __shared__ int part[4][64];
+    const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+    const int cnt = raw_cnt[f * kCntStride];
+    if (cnt > raw_cap || (int)blockIdx.x * 64 >= cnt) return;
+    const RawKp *rec = raw + (size_t)f * raw_cap;
+    const int i = blockIdx.x * 64 + lane;
+    const bool live = i < cnt;
+    unsigned long long ki = ~0ull;
+    if (live) ki = ((unsigned long long)sortable(rec[i].x) << 32) | sortable(rec[i].y);
+    int rank = 0;
+    for (int c0 = 0; c0 < cnt; c0 += kRankChunk) {
+        const int m = min(kRankChunk, cnt - c0);
+        const int m32 = (m + 31) & ~31;                 // pad: ~0 keys never sort before
+        __syncthreads();
+        for (int t = tid; t < m32; t += 256) {
+            unsigned long long k = ~0ull;
+            if (t < m) {
+                const RawKp &r = rec[c0 + t];
+                k = ((unsigned long long)sortable(r.x) << 32) | sortable(r.y);
+            }
+            ks[t] = k;
+        }
+        __syncthreads();
+        if (!live) continue;
+        const int qs = (m32 >> 2) * q, qe = qs + (m32 >> 2);
+        for (int t = qs; t < qe; t += 8) {
+            unsigned long long k8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) k8[u] = ks[t + u];
+            bool anyeq = false;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                rank += k8[u] < ki;
+                anyeq |= k8[u] == ki;
+            }
+            if (anyeq) {                                // ties on (x, y): full comparator
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int j = c0 + t + u;
+                    if (k8[u] == ki && j != i && rec_before(rec[j], rec[i])) ++rank;
+                }
+            }
+        }
+    }
+    part[q][lane] = rank;
+    __syncthreads();
+    if (q == 0 && live) {
+        const int r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+        if (r < cnt) sorted[(size_t)f * raw_cap + r] = (uint32_t)i;
+        else atomicExch(&sorted[(size_t)f * raw_cap], 0xFFFFFFFFu);   // order broken: flag
+    }
+}
+
 __global__ void __launch_bounds__(1024)
-sort_dedup(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
-           pano_kp *__restrict__ out, int cap, int32_t *__restrict__ counts,
-           int32_t *__restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    unsigned long long *key = (unsigned long long *)smem_raw;      // [kSortMax]
-    uint32_t *idx = (uint32_t *)(key + kSortMax);                  // [kSortMax]
+emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
+               const uint32_t *__restrict__ sorted, pano_kp *__restrict__ out, int cap,
+               int32_t *__restrict__ counts, int32_t *__restrict__ err) {
     __shared__ int32_t scan[1024];
     const int f = blockIdx.x, tid = threadIdx.x;
     const RawKp *rec = raw + (size_t)f * raw_cap;
-    int cnt = raw_cnt[f * kCntStride];
-    if (cnt > raw_cap || cnt > kSortMax) {
+    const uint32_t *idx = sorted + (size_t)f * raw_cap;
+    const int cnt = raw_cnt[f * kCntStride];
+    if (cnt > raw_cap) {
         if (tid == 0) { err[0] = PANO_E_OVERFLOW; counts[f] = -1; }
         return;
     }
-    int n2 = 1;
-    while (n2 < cnt) n2 <<= 1;
-    for (int i = tid; i < n2; i += 1024) {
-        if (i < cnt) {
-            key[i] = ((unsigned long long)sortable(rec[i].x) << 32) | sortable(rec[i].y);
-            idx[i] = (uint32_t)i;
-        } else {
-            key[i] = ~0ull;
-            idx[i] = 0xFFFFFFFFu;
-        }
-    }
-    __syncthreads();
-    for (int kk = 2; kk <= n2; kk <<= 1) {
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < n2; i += 1024) {
-                const int l = i ^ j;
-                if (l <= i) continue;
-                const bool asc = (i & kk) == 0;
-                bool lt;   // element l strictly before element i
-                const unsigned long long ki = key[i], kl = key[l];
-                const uint32_t ii = idx[i], il = idx[l];
-                if (ki != kl) lt = kl < ki;
-                else if (ii == 0xFFFFFFFFu || il == 0xFFFFFFFFu) lt = ii == 0xFFFFFFFFu && il != 0xFFFFFFFFu;
-                else lt = rec_before(rec[il], rec[ii]);
-                if (asc == lt) {
-                    key[i] = kl; key[l] = ki;
-                    idx[i] = il; idx[l] = ii;
-                }
-            }
-            __syncthreads();
-        }
+    // every slot must hold a live index (rank_keys is a permutation of 0..cnt-1)
+    int bad = 0;
+    for (int i = tid; i < cnt; i += 1024) bad |= idx[i] >= (uint32_t)cnt;
+    if (__syncthreads_or(bad)) {
+        if (tid == 0) { err[0] = PANO_E_OVERFLOW; err[1] = 0x5017; counts[f] = -1; }
+        return;
     }
     // de-duplicate consecutive equal (pt, size, angle), then block-wide exclusive scan
-    const int per = (n2 + 1023) / 1024;
+    const int per = (cnt + 1023) / 1024;
     const int beg = tid * per;
     int mine = 0;
     for (int t = 0; t < per; ++t) {
@@ -663,6 +757,7 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     const int lane = tid & 63, wv = tid >> 6;
     unsigned long long *wacc = acc[wv];
     const float inv_side = 1.0f / (float)side;
+    const double inv_hwd = 1.0 / hwd;
     const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hwd < 2.5 with slack
     for (int win = 0; win < S; win += kDescWin) {
         if (tid == 0) list_n = 0;
@@ -696,7 +791,7 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const int rr = py + ys, cc = px + xs;
             const double rrot = (double)xs * sin_a + (double)ys * cos_a;
             const double crot = (double)xs * cos_a - (double)ys * sin_a;
-            const double rq = rrot / hwd, cq = crot / hwd;
+            const double rq = div_rn(rrot, hwd, inv_hwd), cq = div_rn(crot, hwd, inv_hwd);
             const double rbin = (rq + 2.0) - 0.5;
             const double cbin = (cq + 2.0) - 0.5;
             if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) continue;
@@ -705,7 +800,7 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const float mag = sqrtf(gx * gx + gy * gy);
             const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
             const double w = exp(-0.125 * (rq * rq + cq * cq));
-            const double wm = w * (double)mag;
+            const double wm = (w * (double)mag) * kDescScale;   // 2^40 fixed point, exact scaling
             const float ob = np_remainder_pos_f((ori - angle_f) * bins_per_deg, 8.0f);
             const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
             const int o0 = ((int)floorf(ob)) % 8;
@@ -721,8 +816,8 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
                 const double v0 = part[q] * (1 - of);
                 const double v1 = part[q] * of;
-                atomicAdd(&wacc[base + o0], rint_fix(v0 * kDescScale));
-                atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1 * kDescScale));
+                atomicAdd(&wacc[base + o0], rint_fix(v0));
+                atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1));
             }
         }
         __syncthreads();
@@ -804,13 +899,21 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     if (ctx->h * 2 > 4095 || ctx->w * 2 > 4095)
         return pano_fail(ctx, PANO_E_UNSUPPORTED, "frames above 2047 px need a wider scan key");
     if (tiles > 0) {
-        dim3 grid(tiles, n);
-        {
-            PanoProf prof_(ctx, PK_EXTREMA);
-            extrema_scan<<<grid, 256, 0, ctx->stream>>>(da, ni, p->border, lp.thresh, raw_ext,
-                                                        ext_cnt, (int)ext_cap);
+        // large octaves first (overlapping a pending blur tail on the side stream), then
+        // join and scan the tail octaves
+        const int split = ctx->tail_pending ? da.tile_start[ctx->o_tail] : tiles;
+        for (int part = 0; part < 2; ++part) {
+            const int t0 = part == 0 ? 0 : split, t1 = part == 0 ? split : tiles;
+            if (part == 1) sift_join_tail(ctx);
+            if (t1 <= t0) continue;
+            dim3 grid(t1 - t0, n);
+            {
+                PanoProf prof_(ctx, PK_EXTREMA);
+                extrema_scan<<<grid, 256, 0, ctx->stream>>>(da, ni, p->border, lp.thresh, raw_ext,
+                                                            ext_cnt, (int)ext_cap, t0);
+            }
+            PANO_LAUNCH_CHECK(ctx, "extrema_scan");
         }
-        PANO_LAUNCH_CHECK(ctx, "extrema_scan");
         dim3 g2((unsigned)((ext_cap + 255) / 256), n);
         {
             PanoProf prof_(ctx, PK_EXTREMA);
@@ -819,6 +922,7 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         }
         PANO_LAUNCH_CHECK(ctx, "localize");
     }
+    sift_join_tail(ctx);                  // orientation / descriptors read every octave
     PyrArgs pa{};
     pa.n_oct = no;
     for (int o = 0; o < no; ++o) {
@@ -837,12 +941,20 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
     {
-        const size_t sm = kSortMax * (sizeof(unsigned long long) + sizeof(uint32_t));
+        rc = pano_grow(ctx, (void **)&ctx->sorted, &ctx->sorted_bytes, raw_cap * n * sizeof(uint32_t));
+        if (rc) return rc;
+        dim3 grid((unsigned)((raw_cap + 63) / 64), n);
         {
             PanoProf prof_(ctx, PK_SORT);
-            sort_dedup<<<n, 1024, sm, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, kps, cap, counts, err);
+            rank_keys<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted);
         }
-        PANO_LAUNCH_CHECK(ctx, "sort_dedup");
+        PANO_LAUNCH_CHECK(ctx, "rank_keys");
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            emit_keypoints<<<n, 1024, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted,
+                                                        kps, cap, counts, err);
+        }
+        PANO_LAUNCH_CHECK(ctx, "emit_keypoints");
     }
     {
         DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
@@ -856,9 +968,4 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     return PANO_OK;
 }
 
-int sift_set_attributes(pano_ctx *ctx) {
-    const int sm = kSortMax * (sizeof(unsigned long long) + sizeof(uint32_t));
-    PANO_HIP(ctx, hipFuncSetAttribute((const void *)sort_dedup,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    return PANO_OK;
-}
+int sift_set_attributes(pano_ctx *) { return PANO_OK; }

@@ -239,6 +239,86 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     }
 }
 
+// The reference's kernel sizes (compile-time NT): 512-thread workgroups, ONE LDS tile.
+// Stage the (64+2r)^2 input tile; the column-pass threads keep their DoG centres in
+// registers; the row pass runs in place (each thread loads its SR + NT - 1 inputs, barrier,
+// writes its SR outputs over them); the column pass (SC outputs per thread, all 512 threads
+// busy) writes level, DoG and level-0 copy.  Half the LDS of a two-tile design, twice the
+// waves per CU; per output the arithmetic is blur_level's (sequential fma in tap order).
+template <int MODE, int NT>
+__global__ void __launch_bounds__(512)
+blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
+          float *__restrict__ in_copy, int H, int W, Taps taps) {
+    constexpr int R = (NT - 1) / 2;
+    constexpr int IWP = (TX + 2 * R) | 1;
+    constexpr int SR = 16, SC = 8;
+    constexpr bool CENTER = MODE != MODE_BASE;
+    static_assert((TY + 2 * R) * (TX / SR) <= 512 && TX * (TY / SC) <= 512, "one item per thread");
+    extern __shared__ __attribute__((aligned(16))) float tin[];   // [TY + 2R][IWP]
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY, f = blockIdx.z;
+    const int tw = min(TX, W - x0), th = min(TY, H - y0);
+    const int tid = threadIdx.x;
+    const int ih = th + 2 * R, iw = tw + 2 * R;
+    {
+        const int cx = tid & 127;
+        if (cx < iw) {
+            const Stager<MODE> sg(la, f, H, W, reflect_fast(x0 - R + cx, W));
+#pragma unroll 4
+            for (int ty = tid >> 7; ty < ih; ty += 4)
+                tin[ty * IWP + cx] = sg.get(reflect_fast(y0 - R + ty, H));
+        }
+    }
+    __syncthreads();
+    // column-pass item of this thread and its centres (before the row pass overwrites them)
+    const int nrs = (th + SC - 1) / SC;
+    const bool colw = tid < tw * nrs;
+    const int cxp = colw ? tid % tw : 0, crs = colw ? tid / tw : 0;
+    float cen[SC];
+#pragma unroll
+    for (int j = 0; j < SC; ++j)
+        cen[j] = (CENTER && colw) ? tin[(crs * SC + j + R) * IWP + cxp + R] : 0.0f;
+    // row pass, in place
+    const int nseg = (tw + SR - 1) / SR;
+    const bool roww = tid < ih * nseg;
+    const int row = roww ? tid % ih : 0, sg = roww ? tid / ih : 0;
+    float v[SR + NT - 1];
+#pragma unroll
+    for (int i = 0; i < SR + NT - 1; ++i) v[i] = roww ? tin[row * IWP + sg * SR + i] : 0.0f;
+    __syncthreads();
+    if (roww) {
+        double acc[SR];
+#pragma unroll
+        for (int j = 0; j < SR; ++j) acc[j] = 0.0;
+#pragma unroll
+        for (int i = 0; i < SR + NT - 1; ++i) {
+            const double x = (double)v[i];
+#pragma unroll
+            for (int j = 0; j < SR; ++j) {
+                const int t = i - j;
+                if (t >= 0 && t < NT) acc[j] = fma(taps.k[t], x, acc[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SR; ++j) tin[row * IWP + sg * SR + j] = (float)acc[j];
+    }
+    __syncthreads();
+    if (!colw) return;
+    double acc[SC];
+    conv_seg<NT, SC>(tin + crs * SC * IWP + cxp, IWP, taps.k, acc);
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+        const int ty = crs * SC + j;
+        if (ty >= th) break;
+        const float o = (float)acc[j];
+        const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + cxp;
+        out[gi] = o;
+        if constexpr (CENTER) {
+            if (dog) dog[gi] = o - cen[j];
+            if (in_copy) in_copy[gi] = cen[j];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ small-octave tail
 // Octaves whose levels fit one 64 x 64 tile are latency-bound as separate launches (one
 // tiny workgroup per frame, ~7 us each, 5 per octave).  blur_tail runs them all in ONE
@@ -262,6 +342,54 @@ struct TailArgs {
 
 __device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_NEAREST
     return (int)floor(d * inv);
+}
+
+// One tail level for a compile-time tap count: halo staging with the in-range reflect
+// first, register-blocked row pass (8 outputs per thread) into rowt, register-blocked column
+// pass (8 outputs per thread) writing the LDS level, the Gaussian level and the DoG.
+// Taps are uniform loads kept in registers.  Caller synchronises after it.
+template <int NT>
+__device__ __forceinline__ void tail_level(const float *in, float *outb, float *halo, float *rowt,
+                                           int HPP, int H, int W,
+                                           const double *__restrict__ taps_g, float *g, float *d,
+                                           int tid) {
+    constexpr int R = (NT - 1) / 2, SG = 8, P = kTailDim;
+    const int hh = H + 2 * R, hw = W + 2 * R;
+    {
+        const int cx = tid & 127;                  // hw <= 64 + 2 * 13 < 128
+        if (cx < hw) {
+            const int sx = reflect_fast(cx - R, W);
+            for (int y = tid >> 7; y < hh; y += 8) halo[y * HPP + cx] = in[reflect_fast(y - R, H) * P + sx];
+        }
+    }
+    double k[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) k[t] = taps_g[t];
+    __syncthreads();
+    const int nseg = (W + SG - 1) / SG;
+    if (tid < hh * nseg) {
+        const int y = tid % hh, sg = tid / hh;
+        double acc[SG];
+        conv_seg<NT, SG>(halo + y * HPP + sg * SG, 1, k, acc);
+#pragma unroll
+        for (int j = 0; j < SG; ++j) rowt[y * (P + 1) + sg * SG + j] = (float)acc[j];
+    }
+    __syncthreads();
+    const int nrs = (H + SG - 1) / SG;
+    if (tid < W * nrs) {
+        const int x = tid % W, rs = tid / W;
+        double acc[SG];
+        conv_seg<NT, SG>(rowt + rs * SG * (P + 1) + x, P + 1, k, acc);
+#pragma unroll
+        for (int j = 0; j < SG; ++j) {
+            const int y = rs * SG + j;
+            if (y >= H) break;
+            const float o = (float)acc[j];
+            outb[y * P + x] = o;
+            g[y * W + x] = o;
+            d[y * W + x] = o - in[y * P + x];
+        }
+    }
 }
 
 __global__ void __launch_bounds__(1024)
@@ -303,6 +431,24 @@ blur_tail(TailArgs ta) {
             const float *in = smem + cur * P * P;
             int out = 0;
             while (out == cur || out == keep) ++out;
+            float *g = ta.G[oi][l] + (size_t)f * H * W;
+            float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
+            const double *tg = ta.taps + l * PANO_MAX_TAPS;
+            bool done = true;
+            switch (n) {   // the reference's kernel sizes; others take the generic loop below
+                case 11: tail_level<11>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
+                case 13: tail_level<13>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
+                case 17: tail_level<17>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
+                case 21: tail_level<21>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
+                case 27: tail_level<27>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
+                default: done = false;
+            }
+            if (done) {
+                __syncthreads();
+                cur = out;
+                if (l == ta.n_lvl - 3) keep = cur;
+                continue;
+            }
             if (tid < n) tp[tid] = ta.taps[l * PANO_MAX_TAPS + tid];
             const int hh = H + 2 * r, hw = W + 2 * r;
             for (int i = tid; i < hh * hw; i += NT) {
@@ -318,8 +464,6 @@ blur_tail(TailArgs ta) {
                 rowt[y * (P + 1) + x] = (float)acc;
             }
             __syncthreads();
-            float *g = ta.G[oi][l] + (size_t)f * H * W;
-            float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
             for (int i = tid; i < H * W; i += NT) {        // column pass + DoG
                 const int y = i / W, x = i - (i / W) * W;
                 const float *q = rowt + y * (P + 1) + x;
@@ -373,15 +517,25 @@ template <int MODE, int NT>
 int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float *in_copy,
                    int n, int H, int W, const Taps &t) {
     dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
-    const size_t sm = smem_bytes(t);
-    if (sm > 65536)
-        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_level<MODE, NT>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    {
-        PanoProf prof_(ctx, PK_BLUR);
-        blur_level<MODE, NT><<<grid, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+    if constexpr (NT > 0) {
+        constexpr int R = (NT - 1) / 2;
+        const size_t sm = (size_t)(TY + 2 * R) * ((TX + 2 * R) | 1) * sizeof(float);
+        {
+            PanoProf prof_(ctx, PK_BLUR);
+            blur_fast<MODE, NT><<<grid, 512, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+        }
+        PANO_LAUNCH_CHECK(ctx, "blur_fast");
+    } else {
+        const size_t sm = smem_bytes(t);
+        if (sm > 65536)
+            PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_level<MODE, 0>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        {
+            PanoProf prof_(ctx, PK_BLUR);
+            blur_level<MODE, 0><<<grid, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+        }
+        PANO_LAUNCH_CHECK(ctx, "blur_level");
     }
-    PANO_LAUNCH_CHECK(ctx, "blur_level");
     return PANO_OK;
 }
 
@@ -474,7 +628,8 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
 }
 
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
-                        const pano_sift_params *p) {
+                        const pano_sift_params *p, bool defer_tail) {
+    sift_join_tail(ctx);                  // a previous call's tail must finish first
     int no, nl;
     double sb, sl[PANO_MAX_LEVELS];
     int rc = sift_plan(p, h, w, &no, &nl, &sb, sl);
@@ -516,30 +671,10 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                                     ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
     }
-    for (int o = 0; o < o_tail; ++o) {
-        const int H = ctx->oct_h[o], W = ctx->oct_w[o];
-        for (int l = 1; l < nl; ++l) {
-            float *out = G + ctx->gauss_off[o][l];
-            float *dg = D + ctx->dog_off[o][l - 1];
-            LoadArgs la{};
-            if (l == 1 && o > 0) {
-                // next-octave base = INTER_NEAREST (w//2, h//2) of level nl-3 of octave o-1,
-                // materialised as G[o][0] by the same launch
-                la.src = G + ctx->gauss_off[o - 1][nl - 3];
-                la.sh = ctx->oct_h[o - 1];
-                la.sw = ctx->oct_w[o - 1];
-                la.ifx = 1.0 / ((double)W / la.sw);
-                la.ify = 1.0 / ((double)H / la.sh);
-                rc = launch_blur<MODE_DOWN>(ctx, la, out, dg, G + ctx->gauss_off[o][0], n, H, W,
-                                            tl[l]);
-            } else {
-                la.src = G + ctx->gauss_off[o][l - 1];
-                rc = launch_blur<MODE_LEVEL>(ctx, la, out, dg, nullptr, n, H, W, tl[l]);
-            }
-            if (rc) return rc;
-        }
-    }
-    if (o_tail < no) {
+    // fork the small-octave tail onto the side stream as soon as its input exists
+    // (G[o_tail-1][nl-3]); only the last small blurs of that octave are then in flight, so
+    // its n workgroups get CUs before the extrema scan fills the GPU
+    auto fork_tail = [&]() -> int {
         // device copy of the level taps (uploaded only when they change)
         double th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
         TailArgs ta{};
@@ -575,11 +710,50 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         const size_t sm = tail_smem_bytes(rmax);
         PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_tail,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        if (!ctx->side) {
+            PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+        }
+        PANO_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+        PANO_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
         {
-            PanoProf prof_(ctx, PK_BLUR);
-            blur_tail<<<n, 1024, sm, ctx->stream>>>(ta);
+            PanoProf prof_(ctx, PK_BLUR, ctx->side);
+            blur_tail<<<n, 1024, sm, ctx->side>>>(ta);
         }
         PANO_LAUNCH_CHECK(ctx, "blur_tail");
+        PANO_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
+        ctx->tail_pending = true;
+        ctx->o_tail = o_tail;
+        return PANO_OK;
+    };
+    for (int o = 0; o < o_tail; ++o) {
+        const int H = ctx->oct_h[o], W = ctx->oct_w[o];
+        for (int l = 1; l < nl; ++l) {
+            float *out = G + ctx->gauss_off[o][l];
+            float *dg = D + ctx->dog_off[o][l - 1];
+            LoadArgs la{};
+            if (l == 1 && o > 0) {
+                // next-octave base = INTER_NEAREST (w//2, h//2) of level nl-3 of octave o-1,
+                // materialised as G[o][0] by the same launch
+                la.src = G + ctx->gauss_off[o - 1][nl - 3];
+                la.sh = ctx->oct_h[o - 1];
+                la.sw = ctx->oct_w[o - 1];
+                la.ifx = 1.0 / ((double)W / la.sw);
+                la.ify = 1.0 / ((double)H / la.sh);
+                rc = launch_blur<MODE_DOWN>(ctx, la, out, dg, G + ctx->gauss_off[o][0], n, H, W,
+                                            tl[l]);
+            } else {
+                la.src = G + ctx->gauss_off[o][l - 1];
+                rc = launch_blur<MODE_LEVEL>(ctx, la, out, dg, nullptr, n, H, W, tl[l]);
+            }
+            if (rc) return rc;
+            if (o == o_tail - 1 && l == nl - 3 && o_tail < no) {
+                rc = fork_tail();
+                if (rc) return rc;
+            }
+        }
     }
+    if (o_tail < no && !defer_tail) sift_join_tail(ctx);
     return PANO_OK;
 }
