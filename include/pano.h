@@ -235,6 +235,22 @@ int pano_prof_enable(pano_ctx *ctx, int kernel_class);
 int pano_prof_read(pano_ctx *ctx, int kernel_class, int *launches, double *total_ms,
                    double *min_ms, double *max_ms);
 
+/* ---------------------------------------------------------------- hipGraph capture
+ * Launch-bound sequences (e.g. a whole stitch) can be captured once and replayed:
+ * pano_graph_begin(ctx) starts capturing ctx's stream (call the sequence once eagerly first
+ * so every scratch buffer has its final size: growth inside a capture fails with
+ * PANO_E_UNSUPPORTED); pano_graph_end instantiates it.  pano_graph_launch replays it on
+ * ctx's stream with the same device pointers and kernel arguments as captured.  Profiler
+ * event pairs recorded during capture (pano_prof_enable) belong to the graph and are
+ * re-recorded by every replay: pano_graph_prof reads the last replay (stream synchronised
+ * by the caller). */
+typedef struct pano_graph pano_graph;
+int pano_graph_begin(pano_ctx *ctx);
+int pano_graph_end(pano_ctx *ctx, pano_graph **out);
+int pano_graph_launch(pano_ctx *ctx, pano_graph *g);
+int pano_graph_prof(pano_graph *g, int kernel_class, int *launches, double *total_ms);
+int pano_graph_destroy(pano_graph *g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -385,3 +385,24 @@ def test_bands_assemble_to_single_gpu_canvas(gpu, method, setname):
             assert (H, W) == canvas.shape[:2]
             got[:, lo:lo + owned.shape[1]] = owned.cpu().numpy()
         assert np.array_equal(got, canvas), world
+
+
+# ------------------------------------------------------------------ hipGraph replay
+@pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("harris", "grail")])
+def test_graph_replay_matches_eager(gpu, method, setname, gold_json):
+    """Captured + replayed launch sequences give the same bytes as eager launches, and the
+    replayed panorama is the reference's."""
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = data.load_set(setname)
+    st = Stitcher(method)
+    dev = st.upload(frames)
+    eager = st.run(dev, focals, margin=margin)
+    e_recs = eager.records.copy()
+    e_pano = eager.panorama.cpu().numpy()
+    for _ in range(3):                                  # capture, then replays
+        res = st.run(dev, focals, margin=margin, graph=True)
+        assert np.array_equal(res.records.view(np.uint8), e_recs.view(np.uint8))
+        assert np.array_equal(res.panorama.cpu().numpy(), e_pano)
+    assert digest(e_pano) == gold_json(f"{method}_{setname}.json")["pano_digest"]
+    st.release_graphs()

@@ -110,6 +110,11 @@ SIGNATURES = {
     "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),
     "pano_prof_enable": (_I, [_P, _I]),
     "pano_prof_read": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int), _PD, _PD, _PD]),
+    "pano_graph_begin": (_I, [_P]),
+    "pano_graph_end": (_I, [_P, ctypes.POINTER(_P)]),
+    "pano_graph_launch": (_I, [_P, _P]),
+    "pano_graph_prof": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int), _PD]),
+    "pano_graph_destroy": (_I, [_P]),
 }
 
 # kernel classes of pano_prof_enable (include/pano.h PANO_K_*)
@@ -180,6 +185,30 @@ class Context:
     def prof_enable(self, kernel):
         k = kernel if isinstance(kernel, int) else (K_ALL if kernel == "all" else KERNELS.index(kernel))
         self.check(self.lib.pano_prof_enable(self.h, k))
+
+    # ---- hipGraph capture / replay of launch sequences (include/pano.h)
+    def graph_begin(self):
+        self.check(self.lib.pano_graph_begin(self.h))
+
+    def graph_end(self):
+        g = _P()
+        self.check(self.lib.pano_graph_end(self.h, ctypes.byref(g)))
+        return g
+
+    def graph_launch(self, g):
+        self.check(self.lib.pano_graph_launch(self.h, g))
+
+    def graph_prof(self, g, kernel):
+        k = kernel if isinstance(kernel, int) else (K_ALL if kernel == "all" else KERNELS.index(kernel))
+        n, tot = ctypes.c_int(), ctypes.c_double()
+        rc = self.lib.pano_graph_prof(g, k, ctypes.byref(n), ctypes.byref(tot))
+        if rc:
+            hip = (PANO_E_HIP - rc) // 100 if rc < PANO_E_HIP else None
+            raise PanoError(rc, f"pano_graph_prof: hipEventElapsedTime failed (hipError {hip})")
+        return {"launches": n.value, "total_ms": tot.value}
+
+    def graph_destroy(self, g):
+        self.lib.pano_graph_destroy(g)
 
     def prof_read(self, kernel):
         k = kernel if isinstance(kernel, int) else (K_ALL if kernel == "all" else KERNELS.index(kernel))

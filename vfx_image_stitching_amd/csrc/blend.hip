@@ -481,8 +481,10 @@ static int composite_sequential(pano_ctx *ctx, const uint8_t *frames, const uint
     int rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, 2 * (size_t)W + 64);
     if (rc) return rc;
     uint8_t *F[2] = {ctx->flags, ctx->flags + W};
-    PANO_HIP(ctx, hipMemsetAsync(canvas, 0, (size_t)H * W * 3, ctx->stream));
-    PANO_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 2 * (size_t)W, ctx->stream));
+    rc = launch_fill(ctx, canvas, 0, (size_t)H * W * 3);
+    if (rc) return rc;
+    rc = launch_fill(ctx, ctx->flags, 0, 2 * (size_t)W);
+    if (rc) return rc;
     dim3 g0((w + 63) / 64, (h + 3) / 4);
     {
         PanoProf prof_(ctx, PK_COMPOSITE);

@@ -47,7 +47,7 @@ cyl_gather(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
     const size_t plane = (size_t)h * w;
     const int32_t s = win[f * plane + (size_t)y * w + x];
     uint8_t b = 0, g = 0, r = 0;
-    if (s >= 0) {
+    if (s >= 0 && (size_t)s < plane) {
         const uint8_t *p = src + (f * plane + s) * 3;
         b = p[0];
         g = p[1];
@@ -72,8 +72,9 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
     int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, need);
     if (rc) return rc;
     int32_t *win = (int32_t *)ctx->bscratch;
-    PANO_HIP(ctx, hipMemsetAsync(win, 0xFF, plane * n * sizeof(int32_t), ctx->stream));
-    if (colnz) PANO_HIP(ctx, hipMemsetAsync(colnz, 0, (size_t)n * w, ctx->stream));
+    rc = launch_fill(ctx, win, 0xFF, plane * n * sizeof(int32_t));
+    if (rc) return rc;
+    if (colnz && (rc = launch_fill(ctx, colnz, 0, (size_t)n * w))) return rc;
     for (int f0 = 0; f0 < n; f0 += kFocalChunk) {
         const int nf = n - f0 < kFocalChunk ? n - f0 : kFocalChunk;
         FocalArg fa;

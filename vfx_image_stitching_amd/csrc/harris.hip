@@ -225,14 +225,14 @@ harris_desc(const uint8_t *__restrict__ gray, int h, int w, Taps9 t9,
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int k = blockIdx.x * 4 + wv;
-    const int cnt = counts[f];
+    const int cnt = min(counts[f], max_points);
     if ((int)blockIdx.x * 4 >= cnt) return;
     const bool active = k < cnt;
     const uint8_t *g = gray + (size_t)f * h * w;
     int cx = 0, cy = 0;
     if (active) {
-        cx = xy[((size_t)f * max_points + k) * 2];
-        cy = xy[((size_t)f * max_points + k) * 2 + 1];
+        cx = min(max(xy[((size_t)f * max_points + k) * 2], 0), w - 1);
+        cy = min(max(xy[((size_t)f * max_points + k) * 2 + 1], 0), h - 1);
         for (int e = lane; e < 256; e += 64) {
             const int i = e >> 4, j = e & 15;
             int yy = cy + i, xx = cx + j;
@@ -353,7 +353,8 @@ int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int ma
     int32_t *cnt = (int32_t *)(base + o_cnt);
     int32_t *err = (int32_t *)(base + o_err);
     HCand *cands = (HCand *)(base + o_c);
-    PANO_HIP(ctx, hipMemsetAsync(base + o_max, 0, o_c - o_max, ctx->stream));
+    rc = launch_fill(ctx, base + o_max, 0, o_c - o_max);
+    if (rc) return rc;
     {
         PanoProf prof_(ctx, PK_H_GRAY);
         to_gray<<<(unsigned)((plane * n + 255) / 256), 256, 0, ctx->stream>>>(bgr, gray, plane * n);

@@ -80,8 +80,8 @@ dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
     const int p = blockIdx.z;
     const int fa = pairs.a[p], fb = pairs.b[p];
     int NA = counts[fa], NB = counts[fb];
-    NA = NA < cap ? NA : cap;
-    NB = NB < cap ? NB : cap;
+    NA = min(max(NA, 0), cap);
+    NB = min(max(NB, 0), cap);
     const int i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
     if (i0 >= NA || j0 >= NB) return;
     const float *dA = desc + (size_t)fa * cap * PANO_DESC_DIM;
@@ -173,7 +173,7 @@ pack_rows(const float *__restrict__ desc, const int32_t *__restrict__ counts, in
     if (row >= (size_t)n_frames * cap) return;
     const int f = (int)(row / cap), r = (int)(row % cap);
     int cnt = counts[f];
-    cnt = cnt < cap ? cnt : cap;
+    cnt = min(max(cnt, 0), cap);
     const bool live = r < cnt;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
     if (live) {
@@ -209,8 +209,8 @@ dist_bf16(const unsigned short *__restrict__ pk, const float *__restrict__ norms
     const int p = blockIdx.z;
     const int fa = pairs.a[p], fb = pairs.b[p];
     int NA = counts[fa], NB = counts[fb];
-    NA = NA < cap ? NA : cap;
-    NB = NB < cap ? NB : cap;
+    NA = min(max(NA, 0), cap);
+    NB = min(max(NB, 0), cap);
     const int i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
     if (i0 >= NA || j0 >= NB) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -290,8 +290,8 @@ __global__ void reduce_parts(const Part *__restrict__ parts, const int32_t *__re
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     int NA = counts[pairs.a[p]], NB = counts[pairs.b[p]];
-    NA = NA < cap ? NA : cap;
-    NB = NB < cap ? NB : cap;
+    NA = min(max(NA, 0), cap);
+    NB = min(max(NB, 0), cap);
     float b = INFINITY, s = INFINITY;
     int j = -1;
     if (i < NA) {
@@ -343,8 +343,8 @@ dist_direct(const float *__restrict__ desc, const int32_t *__restrict__ counts, 
     const int p = blockIdx.y, i = blockIdx.x, tid = threadIdx.x;
     const int fa = pairs.a[p], fb = pairs.b[p];
     int NA = counts[fa], NB = counts[fb];
-    NA = NA < cap ? NA : cap;
-    NB = NB < cap ? NB : cap;
+    NA = min(max(NA, 0), cap);
+    NB = min(max(NB, 0), cap);
     if (i >= cap) return;
     if (i >= NA) {
         if (tid == 0) {

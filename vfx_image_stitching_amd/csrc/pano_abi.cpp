@@ -27,6 +27,9 @@ int pano_hip_check(pano_ctx *ctx, hipError_t e, const char *what) {
 
 int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need) {
     if (need <= *have && *p) return PANO_OK;
+    if (ctx->capturing)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED,
+                         "scratch growth inside a graph capture: run the sequence once eagerly first");
     if (*p) {
         hipError_t e = hipStreamSynchronize(ctx->stream);
         if (e != hipSuccess) return pano_hip_check(ctx, e, "grow sync");
@@ -267,6 +270,88 @@ int pano_prof_read(pano_ctx *ctx, int kernel_class, int *launches, double *total
     if (min_ms) *min_ms = n ? mn : 0.0;
     if (max_ms) *max_ms = mx;
     ctx->prof.used = 0;
+    return PANO_OK;
+}
+
+// ------------------------------------------------------------------ hipGraph capture
+struct pano_graph {
+    hipGraphExec_t exec = nullptr;
+    std::vector<hipEvent_t> ev;          // profiler event pairs captured into the graph
+    std::vector<int> kid;
+};
+
+int pano_graph_begin(pano_ctx *ctx) {
+    if (!ctx || ctx->capturing) return PANO_E_ARG;
+    sift_join_tail(ctx);
+    ctx->cap_prof_start = ctx->prof.used;
+    PANO_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    ctx->capturing = true;
+    return PANO_OK;
+}
+
+int pano_graph_end(pano_ctx *ctx, pano_graph **out) {
+    if (!ctx || !out || !ctx->capturing) return PANO_E_ARG;
+    *out = nullptr;
+    sift_join_tail(ctx);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    ctx->capturing = false;
+    ProfState &p = ctx->prof;
+    const size_t a = ctx->cap_prof_start, b = p.used;
+    if (e != hipSuccess || !g) {
+        p.used = a;
+        return pano_hip_check(ctx, e != hipSuccess ? e : hipErrorUnknown, "hipStreamEndCapture");
+    }
+    pano_graph *pg = new pano_graph;
+    e = hipGraphInstantiate(&pg->exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        delete pg;
+        p.used = a;
+        return pano_hip_check(ctx, e, "hipGraphInstantiate");
+    }
+    // the graph owns the event pairs recorded during capture (they are re-recorded on
+    // every replay); take them out of the context's pool
+    for (size_t i = a; i + 1 < b; i += 2) {
+        pg->ev.push_back(p.ev[i]);
+        pg->ev.push_back(p.ev[i + 1]);
+        pg->kid.push_back(p.kid[i / 2]);
+    }
+    p.ev.erase(p.ev.begin() + a, p.ev.begin() + b);
+    p.kid.erase(p.kid.begin() + a / 2, p.kid.begin() + b / 2);
+    p.used = a;
+    *out = pg;
+    return PANO_OK;
+}
+
+int pano_graph_launch(pano_ctx *ctx, pano_graph *g) {
+    if (!ctx || !g) return PANO_E_ARG;
+    PANO_HIP(ctx, hipGraphLaunch(g->exec, ctx->stream));
+    return PANO_OK;
+}
+
+int pano_graph_prof(pano_graph *g, int kernel_class, int *launches, double *total_ms) {
+    if (!g || !launches || !total_ms) return PANO_E_ARG;
+    int n = 0;
+    double tot = 0.0;
+    for (size_t i = 0; i + 1 < g->ev.size(); i += 2) {
+        if (kernel_class != PK_COUNT && g->kid[i / 2] != kernel_class) continue;
+        float ms = 0.0f;
+        const hipError_t e = hipEventElapsedTime(&ms, g->ev[i], g->ev[i + 1]);
+        if (e != hipSuccess) return PANO_E_HIP - 100 * (int)e;   // caller decodes the HIP code
+        ++n;
+        tot += ms;
+    }
+    *launches = n;
+    *total_ms = tot;
+    return PANO_OK;
+}
+
+int pano_graph_destroy(pano_graph *g) {
+    if (!g) return PANO_OK;
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    for (hipEvent_t e : g->ev) (void)hipEventDestroy(e);
+    delete g;
     return PANO_OK;
 }
 

@@ -101,6 +101,9 @@ struct pano_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool tail_pending = false;           // blur_tail enqueued on `side`, not yet joined
     int o_tail = 0;                      // first octave of the tail
+    // ---- hipGraph capture (pano_graph_begin / end)
+    bool capturing = false;
+    size_t cap_prof_start = 0;           // first profiler event of the capture
     // ---- live profiler
     ProfState prof;
 };
@@ -157,6 +160,7 @@ int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need);
     } while (0)
 
 // ---- host launchers implemented in the .hip translation units
+int launch_fill(pano_ctx *ctx, void *dst, uint8_t value, size_t bytes);   // graph-safe memset
 int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
                        const double *h_focal, uint8_t *colnz);
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,

@@ -92,8 +92,8 @@ pair_shifts(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
     __shared__ double2 tile[RB];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int fa = pairs.a[p], fb = pairs.b[p];
-    int NA = counts[fa];
-    NA = NA < cap ? NA : cap;
+    const int NA = min(max(counts[fa], 0), cap);
+    const int NB = min(max(counts[fb], 0), cap);
     const int32_t *bp = best + (size_t)p * cap;
     const float *p1 = d1 + (size_t)p * cap, *p2 = d2 + (size_t)p * cap;
     double2 *mv = moves + (size_t)p * cap;
@@ -102,7 +102,7 @@ pair_shifts(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
     for (int base = 0; base < NA; base += RB) {
         const int i = base + tid;
         int acc = 0;
-        if (i < NA && bp[i] >= 0 && p1[i] < desc_thresh)
+        if (i < NA && bp[i] >= 0 && bp[i] < NB && p1[i] < desc_thresh)
             acc = ratio2 > 0.0 ? ((double)p1[i] < ratio2 * (double)p2[i]) : 1;
         int tot;
         const int pos = block_excl_scan(acc, ish, tot);

@@ -718,6 +718,7 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     __shared__ unsigned long long acc[4][128];   // one histogram per wave
     __shared__ uint32_t list[kDescWin];          // compacted candidate samples (xi << 16 | yi)
     __shared__ int list_n;
+    __shared__ int col_lo[256], col_pre[256], wtot[4];
     __shared__ float vec[128];
     __shared__ float sh_norm;
     const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
@@ -747,80 +748,135 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     const float angle_f = (float)angle;
     const float bins_per_deg = (float)(8.0 / 360.0);
     __syncthreads();
-    // Two phases per window of kDescWin samples: (A) a cheap, conservative test of the
-    // rotated-bin range (no divisions) compacts the candidate samples into an LDS list with
-    // one ballot per wave; (B) the threads process the list densely -- exact bin test, then
-    // the gradient / exp / atan2 / trilinear work -- so about half the square patch (outside
-    // the 4 x 4 bins) costs almost nothing and the heavy path runs without divergence.
-    // The fixed-point histogram sums are integers, hence independent of this order.
+    // Samples: the 4 x 4 bins cover a rotated square of half-width 2.5 hw inside the
+    // (2 half + 1)^2 patch, so about half the patch is outside.  For patches up to 256
+    // columns each thread derives, for one column, the row interval inside the rotated square
+    // and the image (conservative; `sample` applies the exact bin test), a block scan turns
+    // the interval lengths into a dense sample index, and the threads walk that index (column
+    // by binary search).  Larger patches compact candidates through an LDS list instead.
+    // The fixed-point histogram sums are integers, hence independent of the sample order.
     const int S = side * side;
     const int lane = tid & 63, wv = tid >> 6;
     unsigned long long *wacc = acc[wv];
-    const float inv_side = 1.0f / (float)side;
     const double inv_hwd = 1.0 / hwd;
     const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hwd < 2.5 with slack
-    for (int win = 0; win < S; win += kDescWin) {
-        if (tid == 0) list_n = 0;
-        __syncthreads();
-        const int wend = min(win + kDescWin, S);
-        for (int j = win + tid; j < wend + ((256 - (wend - win) % 256) % 256); j += 256) {
-            bool ok = false;
-            int xi = 0, yi = 0;
-            if (j < wend) {
-                // column-major j -> (xi, yi); the f32 quotient is exact for side < 2048
-                xi = side < 2048 ? (int)(((float)j + 0.5f) * inv_side) : j / side;
-                yi = j - xi * side;
-                const int xs = xi - half, ys = yi - half;
-                const int rr = py + ys, cc = px + xs;
-                const double rrot = (double)xs * sin_a + (double)ys * cos_a;
-                const double crot = (double)xs * cos_a - (double)ys * sin_a;
-                ok = rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1 && fabs(rrot) < lim &&
-                     fabs(crot) < lim;
-            }
-            const unsigned long long m = __ballot(ok);
-            int off = 0;
-            if (lane == 0 && m) off = atomicAdd(&list_n, __popcll(m));
-            off = __shfl(off, 0);
-            if (ok) list[off + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)(xi << 16 | yi);
-        }
-        __syncthreads();
-        const int nl = list_n;
-        for (int t = tid; t < nl; t += 256) {
-            const int xi = (int)(list[t] >> 16), yi = (int)(list[t] & 0xffff);
-            const int xs = xi - half, ys = yi - half;
-            const int rr = py + ys, cc = px + xs;
-            const double rrot = (double)xs * sin_a + (double)ys * cos_a;
-            const double crot = (double)xs * cos_a - (double)ys * sin_a;
-            const double rq = div_rn(rrot, hwd, inv_hwd), cq = div_rn(crot, hwd, inv_hwd);
-            const double rbin = (rq + 2.0) - 0.5;
-            const double cbin = (cq + 2.0) - 0.5;
-            if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) continue;
-            const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
-            const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
-            const float mag = sqrtf(gx * gx + gy * gy);
-            const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
-            const double w = exp(-0.125 * (rq * rq + cq * cq));
-            const double wm = (w * (double)mag) * kDescScale;   // 2^40 fixed point, exact scaling
-            const float ob = np_remainder_pos_f((ori - angle_f) * bins_per_deg, 8.0f);
-            const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
-            const int o0 = ((int)floorf(ob)) % 8;
-            const double rf = rbin - r0, cf = cbin - c0;
-            const double of = (double)ob - (double)o0;
-            const double c1 = wm * rf;
-            const double c0w = wm - c1;
-            const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
+    // one sample (column xi, row yi of the square patch): exact bin test, gradient, weight,
+    // trilinear split into this wave's fixed-point histogram
+    auto sample = [&](int xi, int yi) {
+        const int xs = xi - half, ys = yi - half;
+        const int rr = py + ys, cc = px + xs;
+        const double rrot = (double)xs * sin_a + (double)ys * cos_a;
+        const double crot = (double)xs * cos_a - (double)ys * sin_a;
+        const double rq = div_rn(rrot, hwd, inv_hwd), cq = div_rn(crot, hwd, inv_hwd);
+        const double rbin = (rq + 2.0) - 0.5;
+        const double cbin = (cq + 2.0) - 0.5;
+        if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) return;
+        const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
+        const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
+        const float mag = sqrtf(gx * gx + gy * gy);
+        const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+        const double w = exp(-0.125 * (rq * rq + cq * cq));
+        const double wm = (w * (double)mag) * kDescScale;   // 2^40 fixed point, exact scaling
+        const float ob = np_remainder_pos_f((ori - angle_f) * bins_per_deg, 8.0f);
+        const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
+        const int o0 = ((int)floorf(ob)) % 8;
+        const double rf = rbin - r0, cf = cbin - c0;
+        const double of = (double)ob - (double)o0;
+        const double c1 = wm * rf;
+        const double c0w = wm - c1;
+        const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rb = r0 + 1 + (q >> 1), cb = c0 + 1 + (q & 1);
-                if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
-                const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
-                const double v0 = part[q] * (1 - of);
-                const double v1 = part[q] * of;
-                atomicAdd(&wacc[base + o0], rint_fix(v0));
-                atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1));
+        for (int q = 0; q < 4; ++q) {
+            const int rb = r0 + 1 + (q >> 1), cb = c0 + 1 + (q & 1);
+            if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
+            const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
+            const double v0 = part[q] * (1 - of);
+            const double v1 = part[q] * of;
+            atomicAdd(&wacc[base + o0], rint_fix(v0));
+            atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1));
+        }
+    };
+    if (side <= 256) {
+        int lo = 1, hi = 0;
+        if (tid < side) {
+            const int xs = tid - half, cc = px + xs;
+            if (cc > 0 && cc < cols - 1) {
+                lo = max(-half, 1 - py);
+                hi = min(half, rows - 2 - py);
+                // |a ys + b| < lim  ->  ys in an interval (rrot: a = cos, b = xs sin;
+                // crot: a = -sin, b = xs cos), widened by 1e-6 and clipped before rounding
+                const double ab[2][2] = {{cos_a, xs * sin_a}, {-sin_a, xs * cos_a}};
+                for (int q = 0; q < 2; ++q) {
+                    const double av = ab[q][0], bv = ab[q][1];
+                    if (fabs(av) < 1e-12) {
+                        if (!(fabs(bv) < lim)) hi = lo - 1;
+                        continue;
+                    }
+                    const double t1 = (-lim - bv) / av, t2 = (lim - bv) / av;
+                    const double l = fmax(fmin(t1, t2) - 1e-6, -half - 1.0);
+                    const double u = fmin(fmax(t1, t2) + 1e-6, half + 1.0);
+                    lo = max(lo, (int)ceil(l));
+                    hi = min(hi, (int)floor(u));
+                }
             }
         }
+        const int cnt = hi >= lo ? hi - lo + 1 : 0;
+        int incl = cnt;                                     // block exclusive scan of cnt
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) wtot[wv] = incl;
         __syncthreads();
+        int pre = incl - cnt;
+        for (int w2 = 0; w2 < wv; ++w2) pre += wtot[w2];
+        const int total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        if (tid < side) {
+            col_lo[tid] = lo;
+            col_pre[tid] = pre;
+        }
+        __syncthreads();
+        for (int t = tid; t < total; t += 256) {
+            int c0 = 0, c1 = side - 1;                      // largest c with col_pre[c] <= t
+            while (c0 < c1) {
+                const int mid = (c0 + c1 + 1) >> 1;
+                if (col_pre[mid] <= t) c0 = mid;
+                else c1 = mid - 1;
+            }
+            sample(c0, col_lo[c0] + (t - col_pre[c0]) + half);
+        }
+    } else {
+        const float inv_side = 1.0f / (float)side;
+        for (int win = 0; win < S; win += kDescWin) {
+            if (tid == 0) list_n = 0;
+            __syncthreads();
+            const int wend = min(win + kDescWin, S);
+            for (int j = win + tid; j < wend + ((256 - (wend - win) % 256) % 256); j += 256) {
+                bool ok = false;
+                int xi = 0, yi = 0;
+                if (j < wend) {
+                    // column-major j -> (xi, yi); the f32 quotient is exact for side < 2048
+                    xi = side < 2048 ? (int)(((float)j + 0.5f) * inv_side) : j / side;
+                    yi = j - xi * side;
+                    const int xs = xi - half, ys = yi - half;
+                    const int rr = py + ys, cc = px + xs;
+                    const double rrot = (double)xs * sin_a + (double)ys * cos_a;
+                    const double crot = (double)xs * cos_a - (double)ys * sin_a;
+                    ok = rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1 && fabs(rrot) < lim &&
+                         fabs(crot) < lim;
+                }
+                const unsigned long long m = __ballot(ok);
+                int off = 0;
+                if (lane == 0 && m) off = atomicAdd(&list_n, __popcll(m));
+                off = __shfl(off, 0);
+                if (ok) list[off + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)(xi << 16 | yi);
+            }
+            __syncthreads();
+            const int nl = list_n;
+            for (int t = tid; t < nl; t += 256) sample((int)(list[t] >> 16), (int)(list[t] & 0xffff));
+            __syncthreads();
+        }
     }
     __syncthreads();
     if (tid < 128) {
@@ -871,7 +927,8 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     int32_t *cand_cnt = err + kCntStride;
     int32_t *raw_cnt = cand_cnt + (size_t)n * kCntStride;
     int32_t *ext_cnt = raw_cnt + (size_t)n * kCntStride;
-    PANO_HIP(ctx, hipMemsetAsync(ctx->counters, 0, cnt_ints * sizeof(int32_t), ctx->stream));
+    rc = launch_fill(ctx, ctx->counters, 0, cnt_ints * sizeof(int32_t));
+    if (rc) return rc;
 
     LocParams lp;
     lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);

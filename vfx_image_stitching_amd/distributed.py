@@ -167,12 +167,9 @@ def band_plan(steps, first, w, H, f0, count, n_frames=None):
     return loc, first_loc, x_lo, x_hi - x_lo, (own_lo, own_hi)
 
 
-def local_records(stitcher, frames_dev, focals):
+def local_records(stitcher, frames_dev, focals, graph=False):
     """Cylindrical projection, features, matching and RANSAC of one rank's frames."""
-    n_local = frames_dev.shape[0]
-    cyl, colnz = stitcher.cylindrical(frames_dev, focals)
-    feats = stitcher.features(cyl)
-    recs_dev, _ = stitcher.pair_records(feats, [(i, i + 1) for i in range(n_local - 1)])
+    cyl, colnz, recs_dev = stitcher.records(frames_dev, focals, graph)
     return recs_dev, cyl, colnz
 
 
@@ -215,7 +212,8 @@ def global_bbox(local_bbox, group=None):
     return int(-v[0]), int(v[1]), int(-v[2]), int(v[3])
 
 
-def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15):
+def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15,
+             graph=False):
     """One rank's share of a sharded stitch (frames_dev = its pair range + boundary frame).
 
     Returns dict(records=global PAIR_NP, band=device canvas of the owned band,
@@ -223,7 +221,8 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
     """
     import torch
     import torch.distributed as dist
-    recs_dev, cyl, colnz = local_records(stitcher, frames_dev, focals)
+    stitcher.last_graphs = []
+    recs_dev, cyl, colnz = local_records(stitcher, frames_dev, focals, graph)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world > 1:
         recs = gather_records(recs_dev, pair_counts, group)

@@ -21,6 +21,7 @@ Two small device->host reads are the only synchronisation points.
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -72,6 +73,9 @@ class Stitcher:
         # SIFT distance GEMM: "bf16" (exact for integer descriptors, 16x MFMA rate) or "f32"
         self.match = match or os.environ.get("PANO_MATCH", "bf16")
         self._buf = {}
+        self._graphs = {}                # key -> (pano_graph, outputs of the captured call)
+        self._gstream = None             # private stream for capture / replay
+        self.last_graphs = []            # graphs replayed by the last run(graph=True)
 
     # ------------------------------------------------------------------ buffers
     def _get(self, name, shape, dtype):
@@ -149,7 +153,8 @@ class Stitcher:
             raise PanoError(rc, "pano_plan_composite")
         return steps, first, (int(hw[0]), int(hw[1]))
 
-    def composite(self, cyl, colnz, shifts_corr, pairs_xy, bbox=False, sequential=False):
+    def composite(self, cyl, colnz, shifts_corr, pairs_xy, bbox=False, sequential=False,
+                  graph=False):
         """The mosaic loop on a pre-sized canvas; optionally the crop bbox in the same pass."""
         n, h, w, _ = cyl.shape
         steps, first, (H, W) = self.plan(n, h, w, shifts_corr, pairs_xy)
@@ -160,9 +165,18 @@ class Stitcher:
                                                          _lib.i32p(first), ptr(canvas), H, W))
             return canvas
         bb = self._get("bbox", (4,), self.torch.int32) if bbox else None
-        self.ctx.check(lib.pano_composite_bbox(c, ptr(cyl), ptr(colnz), n, h, w, steps,
-                                               _lib.i32p(first), ptr(canvas), H, W, 0,
-                                               ptr(bb) if bbox else None))
+
+        def seg():
+            self.ctx.check(lib.pano_composite_bbox(c, ptr(cyl), ptr(colnz), n, h, w, steps,
+                                                   _lib.i32p(first), ptr(canvas), H, W, 0,
+                                                   ptr(bb) if bbox else None))
+
+        if graph:
+            key = ("composite", cyl.data_ptr(), colnz.data_ptr(), tuple(cyl.shape), bytes(steps),
+                   first.tobytes(), H, W, canvas.data_ptr(), bb.data_ptr() if bbox else 0)
+            self._replay(key, seg)
+        else:
+            seg()
         return (canvas, bb) if bbox else canvas
 
     def bbox(self, img, thr=0):
@@ -171,19 +185,86 @@ class Stitcher:
         self.ctx.check(self.ctx.lib.pano_gray_bbox(self.ctx.h, ptr(img), H, W, thr, ptr(bb)))
         return bb
 
-    # ------------------------------------------------------------------ whole run
-    def run(self, frames_dev, focals, margin: int = 15, timers: bool = False) -> StitchResult:
+    # ------------------------------------------------------------------ hipGraph replay
+    def _replay(self, key, fn):
+        """fn() through a cached hipGraph: one eager call sizes every scratch buffer, the
+        second is captured; later calls with the same key replay it (same device pointers
+        and kernel arguments -- the key must pin everything fn's launches depend on)."""
         T = self.torch
+        # capture needs a non-default stream: graphs are captured and replayed on a private
+        # stream ordered after the caller's stream on entry, and the caller's after it on exit
+        if self._gstream is None:
+            self._gstream = T.cuda.Stream(self.device)
+        outer = T.cuda.current_stream(self.device)
+        self._gstream.wait_stream(outer)
+        try:
+            with T.cuda.stream(self._gstream):
+                self.ctx.bind_stream()
+                dbg = os.environ.get("PANO_DEBUG_SYNC") == "1"
+                ent = self._graphs.get(key)
+                if ent is None:
+                    fn()
+                    if dbg:
+                        T.cuda.synchronize()
+                        print(f"[pano graph] eager ok {key[0]}", flush=True)
+                    self.ctx.graph_begin()
+                    try:
+                        out = fn()
+                    except BaseException:
+                        try:
+                            self.ctx.graph_destroy(self.ctx.graph_end())
+                        except PanoError:
+                            pass
+                        raise
+                    g = self.ctx.graph_end()
+                    if len(self._graphs) >= 16:
+                        old = next(iter(self._graphs))
+                        self.ctx.graph_destroy(self._graphs.pop(old)[0])
+                    ent = self._graphs[key] = (g, out)
+                self.ctx.graph_launch(ent[0])
+                self.last_graphs.append(ent[0])
+                if dbg:
+                    T.cuda.synchronize()
+                    print(f"[pano graph] replay ok {key[0]}", flush=True)
+        finally:
+            outer.wait_stream(self._gstream)
+            self.ctx.bind_stream()
+        return ent[1]
+
+    def release_graphs(self):
+        for g, _ in self._graphs.values():
+            self.ctx.graph_destroy(g)
+        self._graphs.clear()
+
+    def records(self, frames_dev, focals, graph: bool = False):
+        """Cylindrical projection, features, matching and RANSAC of a frame sequence.
+
+        Returns (cyl, colnz, recs_dev); with graph=True the launches replay a hipGraph."""
+        n = frames_dev.shape[0]
+        if n < 2:
+            raise PanoError(_lib.PANO_E_ARG, "need at least two frames")
+
+        def seg():
+            cyl, colnz = self.cylindrical(frames_dev, focals)
+            feats = self.features(cyl)
+            recs_dev, _ = self.pair_records(feats, [(i, i + 1) for i in range(n - 1)])
+            return cyl, colnz, recs_dev
+
+        if not graph:
+            return seg()
+        key = ("records", frames_dev.data_ptr(), tuple(frames_dev.shape),
+               tuple(float(f) for f in np.asarray(focals, np.float64)), self.method, self.match,
+               bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh)
+        return self._replay(key, seg)
+
+    # ------------------------------------------------------------------ whole run
+    def run(self, frames_dev, focals, margin: int = 15, timers: bool = False,
+            graph: bool = False) -> StitchResult:
         t = {}
         tick = time.perf_counter
         t0 = tick()
-        n = frames_dev.shape[0]
-        cyl, colnz = self.cylindrical(frames_dev, focals)
-        feats = self.features(cyl)
-        pairs = [(i, i + 1) for i in range(n - 1)]
-        if not pairs:
-            raise PanoError(_lib.PANO_E_ARG, "need at least two frames")
-        recs_dev, _ = self.pair_records(feats, pairs)
+        self.last_graphs = []
+        cyl, colnz, recs_dev = self.records(frames_dev, focals, graph)
         recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)   # sync point 1
         t["features_match_ransac"] = tick() - t0
         self.ctx.sync()
@@ -200,7 +281,7 @@ class Stitcher:
                 best_pairs.append(((int(r["xA"]), int(r["yA"])), (int(r["xB"]), int(r["yB"]))))
         corr = drift_correct(shifts)
         pxy = [(a[0], a[1], b[0], b[1]) for a, b in best_pairs]
-        canvas, bb_dev = self.composite(cyl, colnz, corr, pxy, bbox=True)
+        canvas, bb_dev = self.composite(cyl, colnz, corr, pxy, bbox=True, graph=graph)
         bb = bb_dev.cpu().numpy()                                        # sync point 2
         H = canvas.shape[0]
         if bb[1] < 0:
