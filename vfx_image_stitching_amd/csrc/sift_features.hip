@@ -718,7 +718,7 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     __shared__ unsigned long long acc[4][128];   // one histogram per wave
     __shared__ uint32_t list[kDescWin];          // compacted candidate samples (xi << 16 | yi)
     __shared__ int list_n;
-    __shared__ int col_lo[256], col_pre[256], wtot[4];
+    __shared__ int col_lo[256], col_pre[257], wtot[4];
     __shared__ float vec[128];
     __shared__ float sh_norm;
     const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
@@ -836,15 +836,29 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             col_lo[tid] = lo;
             col_pre[tid] = pre;
         }
+        if (tid == 0) col_pre[side] = total;
         __syncthreads();
-        for (int t = tid; t < total; t += 256) {
-            int c0 = 0, c1 = side - 1;                      // largest c with col_pre[c] <= t
-            while (c0 < c1) {
-                const int mid = (c0 + c1 + 1) >> 1;
-                if (col_pre[mid] <= t) c0 = mid;
+        // thread t takes the run [t Q, t Q + Q) of the dense index: neighbouring lanes are Q
+        // samples apart (different cells / orientations -> few same-address LDS atomics);
+        // one binary search per thread, then a column-by-column walk
+        const int Q = (total + 255) >> 8;
+        int t = tid * Q;
+        const int tend = min(t + Q, total);
+        if (t < tend) {
+            int c = 0, c1 = side - 1;                       // largest c with col_pre[c] <= t
+            while (c < c1) {
+                const int mid = (c + c1 + 1) >> 1;
+                if (col_pre[mid] <= t) c = mid;
                 else c1 = mid - 1;
             }
-            sample(c0, col_lo[c0] + (t - col_pre[c0]) + half);
+            int r = t - col_pre[c];
+            for (; t < tend; ++t, ++r) {
+                while (r >= col_pre[c + 1] - col_pre[c]) {
+                    r -= col_pre[c + 1] - col_pre[c];
+                    ++c;
+                }
+                sample(c, col_lo[c] + r + half);
+            }
         }
     } else {
         const float inv_side = 1.0f / (float)side;
