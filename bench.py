@@ -45,18 +45,30 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=4)
     ap.add_argument("--match", default=None, choices=["f32", "bf16"])
+    ap.add_argument("--cap", type=int, default=0, help="keypoint capacity per frame (0 = auto)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch eagerly instead of replaying captured hipGraphs")
     return ap.parse_args()
 
 
+SYNTH_PAIRS_PER_RANK = 18      # config 5: 8 ranks x 18 pairs ~ the 143-pair 144-frame loop
+
+
+def synthetic_shards(world):
+    """Pair ranges of the synthetic 144-frame sequence: 18 pairs per rank (weak scaling),
+    the 143 pairs of SURVEY 8(d) config 5 at 8 ranks."""
+    from vfx_image_stitching_amd import distributed as D
+    return D.shard_ranges(min(143, SYNTH_PAIRS_PER_RANK * world), world)
+
+
 def workload(name, rank, world):
     from vfx_image_stitching_amd import data
     if name == "synthetic":
-        frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920)
-        per = 143 // world
-        s = rank * per
-        return frames[s:s + per + 1], focals[s:s + per + 1], 15, (1080, 1920), 143
+        shards = synthetic_shards(world)
+        s, c = shards[rank]
+        # each rank generates only its own frames (the generator is window-independent)
+        frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920, start=s, count=c + 1)
+        return frames, focals, 15, (1080, 1920), sum(cc for _, cc in shards) + 1
     names, frames, focals, margin = data.load_set(name)
     n = len(frames)
     fr, fo = data.cyclic_sequence(frames, focals, start=(n - 1) * rank, count=n)
@@ -113,10 +125,10 @@ def main():
 
     frames, focals, margin, (h, w), distinct = workload(args.workload, rank, world)
     n_local = len(frames)
-    cap = 4096 if args.workload != "synthetic" else 8192
+    cap = args.cap or (4096 if args.workload != "synthetic" else 65536)
     st = Stitcher(args.method, cap=cap, match=args.match)
     dev = st.upload(frames)                                   # resident in HBM
-    counts = [c for _, c in D.shard_ranges(distinct - 1, world)] if args.workload == "synthetic" \
+    counts = [c for _, c in synthetic_shards(world)] if args.workload == "synthetic" \
         else [n_local - 1] * world
     pair_start = sum(counts[:rank])
 

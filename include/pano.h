@@ -143,13 +143,15 @@ int pano_harris(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w, int ma
  * Batched over pairs: pair p matches frame h_pairs[2p] (A) against h_pairs[2p+1] (B) of a
  * [frames][cap][128] descriptor array with d_counts[frames].
  * Outputs per pair p, row i (< cap): d_best[p][i] (first minimum, -1 if B empty),
- * d_d1[p][i] best distance, d_d2[p][i] second-best distance (Lowe ratio input). */
+ * d_d1[p][i] best distance, d_d2[p][i] second-best distance (Lowe ratio input; with
+ * exact_int == 2 d_d2 may be NULL, and the second-best is then not computed). */
 int pano_match(pano_ctx *ctx, const float *d_desc, const int32_t *d_counts, int cap,
                const int32_t *h_pairs, int n_pairs, int exact_int,
                int32_t *d_best, float *d_d1, float *d_d2);
 
 /* ---------------------------------------------------------------- R1
- * Match filter (distance < desc_thresh, optional Lowe ratio d1 < ratio*d2 when ratio > 0)
+ * Match filter (distance < desc_thresh, optional Lowe ratio d1 < ratio*d2 when ratio > 0;
+ * d_d2 is read only then and may be NULL otherwise)
  * + ransac(matches, dist_sq_thresh)  image_stitching_sift.py:74-111.
  * Keypoint coordinates come from d_xy_f32 [frames][cap][2] (SIFT: pano_kp x,y are read
  * when d_kps != NULL; Harris: pass d_xy_i32).  Writes d_recs[n_pairs]. */

@@ -200,6 +200,50 @@ def test_match_ties_pick_first_index(gpu, mode):
     np.testing.assert_array_equal(d2.cpu().numpy()[0], d1.cpu().numpy()[0])
 
 
+@pytest.mark.parametrize("with_d2", [True, False])
+def test_match_bf16_multi_pair_ragged(gpu, with_d2):
+    """bf16 MFMA path over several pairs with ragged counts (0, 1, a partial tile, many
+    tiles so workgroups walk several candidate tiles), a capacity that is not a multiple of
+    the 128-row tile, and heavy ties: indices, d1 and d2 equal the exact integer distances
+    (first index on ties; d2 = inf with a single candidate); d2 may be omitted."""
+    import torch
+    from vfx_image_stitching_amd import _lib
+    rng = np.random.default_rng(11)
+    cap = 5000
+    counts_h = [5000, 1, 0, 777, 4321]
+    d = np.zeros((len(counts_h), cap, 128), np.float32)
+    pool = rng.integers(0, 256, (600, 128))                 # rows drawn from a small pool: ties
+    for f, c in enumerate(counts_h):
+        d[f, :c] = pool[rng.integers(0, len(pool), c)] if f % 2 == 0 else rng.integers(0, 256, (c, 128))
+    pairs = [(0, 4), (4, 0), (3, 1), (1, 3), (0, 2), (2, 3), (3, 3)]
+    desc = torch.from_numpy(d).cuda()
+    counts = torch.tensor(counts_h, dtype=torch.int32).cuda()
+    P = len(pairs)
+    best = torch.full((P, cap), -7, dtype=torch.int32).cuda()
+    d1 = torch.empty((P, cap)).cuda()
+    d2 = torch.empty((P, cap)).cuda() if with_d2 else None
+    hp = np.array(pairs, np.int32).reshape(-1)
+    gpu.check(gpu.lib.pano_match(gpu.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), P, 2,
+                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2) if with_d2 else None))
+    b_h, d1_h = best.cpu().numpy(), d1.cpu().numpy()
+    d2_h = d2.cpu().numpy() if with_d2 else None
+    for p, (fa, fb) in enumerate(pairs):
+        na, nb = counts_h[fa], counts_h[fb]
+        A = d[fa, :na].astype(np.float64)
+        B = d[fb, :nb].astype(np.float64)
+        if na == 0:
+            continue
+        if nb == 0:
+            assert (b_h[p, :na] == -1).all()
+            continue
+        full = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2 * A @ B.T   # exact integers
+        np.testing.assert_array_equal(b_h[p, :na], full.argmin(1), err_msg=str((fa, fb)))
+        np.testing.assert_array_equal(d1_h[p, :na], full.min(1).astype(np.float32))
+        if with_d2:
+            want2 = np.sort(full, axis=1)[:, 1] if nb > 1 else np.full(na, np.inf)
+            np.testing.assert_array_equal(d2_h[p, :na], want2.astype(np.float32))
+
+
 @pytest.mark.parametrize("k", [0, 1, 2, 5, 300, 2500])
 def test_ransac_translate_vs_oracle(gpu, k):
     import torch

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; *) [ "$1" -gt 128 ] && return 0; return 1;; esac; }
 STEPS=${STEPS:-20}
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.txt 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.txt 2>&1
   rc=$?; echo "pytest rc=$rc" | tee -a gpurun_out/pytest_gpu.txt; tail -n 5 gpurun_out/pytest_gpu.txt
   # any failing GPU test may be a device fault: run nothing more on the GPU in this call
   [ $rc -ne 0 ] && exit $rc

@@ -19,6 +19,8 @@
 // Roofline unit M1 = 2*N*M*128 flop/pair.
 #include "pano_internal.h"
 
+#include <algorithm>
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -161,115 +163,156 @@ dist_mfma(const float *__restrict__ desc, const float *__restrict__ norms,
 }
 
 // ---------------------------------------------------------------- bf16 path (default)
-// pack_rows: one pass over the live descriptor rows -> bf16 rows (exact: integers 0..255)
-// + exact f32 norms.  16 threads per row, 8 elements each; the norm partials are integers
-// < 2^24, so the shuffle reduction is exact in any order.
+// The distance is folded into the GEMM: with K extended from 128 to KA = 144 (one more
+// 32x32x16 MFMA step), query rows are packed as  A' = [ a | 65536, 256, 1, 0 ... ]  and
+// candidate rows as  B' = [ -2 b | c2, c1, c0, 0 ... ]  where ||b||^2 = c2 65536 + c1 256 + c0,
+// so C = A'.B' = ||b||^2 - 2 a.b.  Every entry is a bf16-exact integer (|2b| <= 510 has 8
+// significant bits, c* < 256, powers of two) and every partial sum is an integer < 2^21, so
+// the f32 MFMA accumulation is exact in any order; ||a - b||^2 = ||a||^2 + C exactly, and the
+// epilogue is a bare compare / select per element (||a||^2 is constant along the argmin).
+// Rows past a frame's count (up to the 128-row padded stride) are packed as b = 0 with
+// ||b||^2 = 2^22: never a best, and a second-best that large means "none" (reduce_parts).
+constexpr int KA = 144;              // augmented K
+constexpr int KS = KA / 16;          // MFMA K steps
+constexpr float kPadNorm = 4194304.0f;
+
+__device__ __forceinline__ unsigned short bf16_of_int(int v) {     // exact for |v| < 2^9
+    return (unsigned short)(__float_as_uint((float)v) >> 16);
+}
+
+// 16 threads per row, 9 bf16 columns each (thread 15 also writes the augmentation).
 __global__ void __launch_bounds__(256)
-pack_rows(const float *__restrict__ desc, const int32_t *__restrict__ counts, int cap,
-          int n_frames, unsigned short *__restrict__ pk, float *__restrict__ norms) {
+pack_rows(const float *__restrict__ desc, const int32_t *__restrict__ counts, int cap, int capP,
+          int n_frames, unsigned short *__restrict__ pa, unsigned short *__restrict__ pb,
+          float *__restrict__ norms) {
     const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t row = gid >> 4;
     const int part = (int)(gid & 15);
-    if (row >= (size_t)n_frames * cap) return;
-    const int f = (int)(row / cap), r = (int)(row % cap);
+    if (row >= (size_t)n_frames * capP) return;
+    const int f = (int)(row / capP), r = (int)(row % capP);
     int cnt = counts[f];
     cnt = min(max(cnt, 0), cap);
     const bool live = r < cnt;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
     if (live) {
-        const float4 *src = (const float4 *)(desc + row * PANO_DESC_DIM + part * 8);
+        const float4 *src = (const float4 *)(desc + ((size_t)f * cap + r) * PANO_DESC_DIM + part * 8);
         a = src[0];
         b = src[1];
     }
     float s = a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z +
-              b.w * b.w;
+              b.w * b.w;                                  // integers: exact in any order
     for (int d = 8; d > 0; d >>= 1) s += __shfl_xor(s, d, 16);
-    if (!live) return;
-    ushort4 u0 = make_ushort4(f32_to_bf16_exact(a.x), f32_to_bf16_exact(a.y),
-                              f32_to_bf16_exact(a.z), f32_to_bf16_exact(a.w));
-    ushort4 u1 = make_ushort4(f32_to_bf16_exact(b.x), f32_to_bf16_exact(b.y),
-                              f32_to_bf16_exact(b.z), f32_to_bf16_exact(b.w));
-    ushort4 *dst = (ushort4 *)(pk + row * PANO_DESC_DIM + part * 8);
-    dst[0] = u0;
-    dst[1] = u1;
-    if (part == 0) norms[row] = s;
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    unsigned short ua[8], ub[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ua[k] = f32_to_bf16_exact(v[k]);
+        ub[k] = bf16_of_int(-2 * (int)v[k]);
+    }
+    unsigned short *da = pa + row * KA + part * 8, *db = pb + row * KA + part * 8;
+    *(uint4 *)da = make_uint4(ua[0] | ua[1] << 16, ua[2] | ua[3] << 16, ua[4] | ua[5] << 16, ua[6] | ua[7] << 16);
+    *(uint4 *)db = make_uint4(ub[0] | ub[1] << 16, ub[2] | ub[3] << 16, ub[4] | ub[5] << 16, ub[6] | ub[7] << 16);
+    if (part == 0) {
+        const int nb = live ? (int)s : (int)kPadNorm;
+        unsigned short ta[16] = {}, tb[16] = {};
+        ta[0] = (unsigned short)(__float_as_uint(65536.0f) >> 16);
+        ta[1] = (unsigned short)(__float_as_uint(256.0f) >> 16);
+        ta[2] = (unsigned short)(__float_as_uint(1.0f) >> 16);
+        tb[0] = (nb >> 16) ? (unsigned short)(__float_as_uint((float)(nb >> 16)) >> 16) : 0;
+        tb[1] = (unsigned short)(__float_as_uint((float)((nb >> 8) & 255)) >> 16);
+        tb[2] = (unsigned short)(__float_as_uint((float)(nb & 255)) >> 16);
+        uint4 *qa = (uint4 *)(pa + row * KA + 128), *qb = (uint4 *)(pb + row * KA + 128);
+        for (int h = 0; h < 2; ++h) {
+            qa[h] = make_uint4(ta[8 * h] | ta[8 * h + 1] << 16, ta[8 * h + 2] | ta[8 * h + 3] << 16,
+                               ta[8 * h + 4] | ta[8 * h + 5] << 16, ta[8 * h + 6] | ta[8 * h + 7] << 16);
+            qb[h] = make_uint4(tb[8 * h] | tb[8 * h + 1] << 16, tb[8 * h + 2] | tb[8 * h + 3] << 16,
+                               tb[8 * h + 4] | tb[8 * h + 5] << 16, tb[8 * h + 6] | tb[8 * h + 7] << 16);
+        }
+        norms[row] = live ? s : 0.0f;
+    }
 }
 
-// dist_bf16: 128 x 128 tile per workgroup, 4 waves as 2 (j) x 2 (i), each 64 x 64 = 2 x 2
-// v_mfma_f32_32x32x16_bf16 blocks.  Every wave loads its A / B fragments for the whole
-// K = 128 straight from the packed rows into registers (32 independent 16-byte loads: one
-// memory round trip), then issues 32 MFMAs and folds argmin / second-min in registers.
-// Rows past the live count are clamped to a live row and masked in the epilogue.
+// dist_bf16: workgroup = 128 query rows (4 waves as 2 (j) x 2 (i), each 64 x 64 = 2 x 2
+// v_mfma_f32_32x32x16_bf16 blocks).  The query fragments stay in registers while the
+// workgroup walks candidate tiles split, split + n_split, ... (the next tile's fragments are
+// loaded while the current one is folded), so the partials are n_split per row, not one per
+// tile.  Per element the fold is compare / select (plus min / max when SECOND).
+template <bool SECOND>
 __global__ void __launch_bounds__(256)
-dist_bf16(const unsigned short *__restrict__ pk, const float *__restrict__ norms,
-          const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
-          int n_jt) {
-    __shared__ float nB[MT];
+dist_bf16(const unsigned short *__restrict__ pa, const unsigned short *__restrict__ pb,
+          const float *__restrict__ norms, const int32_t *__restrict__ counts, int cap, int capP,
+          PairArg pairs, Part *__restrict__ parts, int n_split) {
     __shared__ Part red[2][MT];
     const int p = blockIdx.z;
     const int fa = pairs.a[p], fb = pairs.b[p];
     int NA = counts[fa], NB = counts[fb];
     NA = min(max(NA, 0), cap);
     NB = min(max(NB, 0), cap);
-    const int i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
-    if (i0 >= NA || j0 >= NB) return;
+    const int i0 = blockIdx.y * MT;
+    const int n_jt = (NB + MT - 1) / MT;
+    if (i0 >= NA || (int)blockIdx.x >= n_jt) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wj = wv >> 1, wi = wv & 1;
     const int lr = lane & 31, lh = lane >> 5;
-    const unsigned short *rA = pk + (size_t)fa * cap * PANO_DESC_DIM;
-    const unsigned short *rB = pk + (size_t)fb * cap * PANO_DESC_DIM;
-    if (tid < MT) nB[tid] = j0 + tid < NB ? norms[(size_t)fb * cap + j0 + tid] : 0.0f;
-    bf16x8 fj[2][8], fi[2][8];
+    const unsigned short *rA = pa + (size_t)fa * capP * KA;
+    const unsigned short *rB = pb + (size_t)fb * capP * KA;
+    bf16x8 fi[2][KS], fj[2][KS];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-        const int jr = min(j0 + wj * 64 + m * 32 + lr, NB - 1);
-        const int ir = min(i0 + wi * 64 + m * 32 + lr, NA - 1);
-        const bf16x8 *qj = (const bf16x8 *)(rB + (size_t)jr * PANO_DESC_DIM + 8 * lh);
-        const bf16x8 *qi = (const bf16x8 *)(rA + (size_t)ir * PANO_DESC_DIM + 8 * lh);
+        const bf16x8 *qi = (const bf16x8 *)(rA + (size_t)(i0 + wi * 64 + m * 32 + lr) * KA + 8 * lh);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            fj[m][k] = qj[2 * k];
-            fi[m][k] = qi[2 * k];
-        }
+        for (int k = 0; k < KS; ++k) fi[m][k] = qi[2 * k];
     }
-    f32x16 acc[2][2];
+    auto load_b = [&](int jt) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+        for (int m = 0; m < 2; ++m) {
+            const bf16x8 *qj = (const bf16x8 *)(rB + (size_t)(jt * MT + wj * 64 + m * 32 + lr) * KA + 8 * lh);
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
+            for (int k = 0; k < KS; ++k) fj[m][k] = qj[2 * k];
+        }
+    };
+    float best[2] = {INFINITY, INFINITY}, second[2] = {INFINITY, INFINITY};
+    int bj[2] = {0x7fffffff, 0x7fffffff};
+    int jt = blockIdx.x;
+    load_b(jt);
+    for (; jt < n_jt; jt += n_split) {
+        f32x16 acc[2][2];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a][k], fi[b][k], acc[a][b], 0, 0, 0);
-    __syncthreads();                                    // nB
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a][k], fi[b][k], acc[a][b], 0, 0, 0);
+        if (jt + n_split < n_jt) load_b(jt + n_split);      // in flight during the fold
+        const int jb = jt * MT + wj * 64 + 4 * lh;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {   // j increasing within the lane: strict <
+                    const float d = acc[a][b][r];
+                    if (SECOND) second[b] = fminf(second[b], fmaxf(best[b], d));
+                    const bool lt = d < best[b];
+                    bj[b] = lt ? jb + a * 32 + (r & 3) + 8 * (r >> 2) : bj[b];
+                    best[b] = lt ? d : best[b];
+                }
+    }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
+        const float ob = __shfl_xor(best[b], 32);
+        const int oj = __shfl_xor(bj[b], 32);
+        const float os = __shfl_xor(second[b], 32);
+        merge(best[b], bj[b], second[b], ob, oj, os);
         const int il = wi * 64 + b * 32 + lr;
-        const float na = i0 + il < NA ? norms[(size_t)fa * cap + i0 + il] : 0.0f;
-        float best = INFINITY, second = INFINITY;
-        int bj = 0x7fffffff;
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {       // j increasing within the lane: strict <
-                const int jl = wj * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const float d = (na + nB[jl]) - 2.0f * acc[a][b][r];
-                const bool ok = j0 + jl < NB;
-                const bool lt = ok && d < best;
-                second = lt ? best : (ok ? fminf(second, d) : second);
-                bj = lt ? j0 + jl : bj;
-                best = lt ? d : best;
-            }
-        const float ob = __shfl_xor(best, 32);
-        const int oj = __shfl_xor(bj, 32);
-        const float os = __shfl_xor(second, 32);
-        merge(best, bj, second, ob, oj, os);
-        if (lh == 0) red[wj][il] = Part{best, bj, second};
+        if (lh == 0) red[wj][il] = Part{best[b], bj[b], second[b]};
     }
     __syncthreads();
     if (tid < MT) {
@@ -279,7 +322,10 @@ dist_bf16(const unsigned short *__restrict__ pk, const float *__restrict__ norms
         int jj = x.idx;
         merge(bb, jj, ss, y.best, y.idx, y.second);
         const int gi = i0 + tid;
-        if (gi < NA) parts[((size_t)p * n_jt + blockIdx.x) * cap + gi] = Part{bb, jj, ss};
+        if (gi < NA) {
+            const float na = norms[(size_t)fa * capP + gi];
+            parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{na + bb, jj, na + ss};
+        }
     }
 }
 
@@ -296,16 +342,17 @@ __global__ void reduce_parts(const Part *__restrict__ parts, const int32_t *__re
     int j = -1;
     if (i < NA) {
         j = 0x7fffffff;
-        const int nt = (NB + MT - 1) / MT;
+        const int nt = min((NB + MT - 1) / MT, n_jt);
         for (int t = 0; t < nt; ++t) {
             const Part q = parts[((size_t)p * n_jt + t) * cap + i];
             merge(b, j, s, q.best, q.idx, q.second);
         }
         if (NB == 0) j = -1;
+        if (s >= kPadNorm) s = INFINITY;      // only padding rows: no real second candidate
     }
     best[(size_t)p * cap + i] = j;
     d1[(size_t)p * cap + i] = b;
-    d2[(size_t)p * cap + i] = s;
+    if (d2) d2[(size_t)p * cap + i] = s;
 }
 
 // ---------------------------------------------------------------- Harris (float descriptors)
@@ -383,7 +430,7 @@ int match_set_attributes(pano_ctx *) { return PANO_OK; }
 int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
                  const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
                  float *d2) {
-    if (cap <= 0 || n_pairs <= 0 || !desc || !counts || !best || !d1 || !d2)
+    if (cap <= 0 || n_pairs <= 0 || !desc || !counts || !best || !d1 || (!d2 && exact_int != 2))
         return pano_fail(ctx, PANO_E_ARG, "pano_match: bad arguments");
     int n_frames = 0;
     for (int q = 0; q < 2 * n_pairs; ++q) n_frames = h_pairs[q] + 1 > n_frames ? h_pairs[q] + 1 : n_frames;
@@ -395,7 +442,7 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
             pa.b[q] = h_pairs[2 * (p0 + q) + 1];
         }
         int32_t *bp = best + (size_t)p0 * cap;
-        float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 + (size_t)p0 * cap;
+        float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 ? d2 + (size_t)p0 * cap : nullptr;
         if (!exact_int) {
             dim3 grid(cap, np);
             {
@@ -406,43 +453,65 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
             continue;
         }
         const int n_t = (cap + MT - 1) / MT;
-        const size_t norm_bytes = ((size_t)n_frames * cap * sizeof(float) + 255) & ~size_t(255);
+        const size_t norm_bytes = ((size_t)n_frames * n_t * MT * sizeof(float) + 255) & ~size_t(255);
+        dim3 g2((cap + 255) / 256, np);
+        if (exact_int == 2) {
+            // query tiles x candidate splits x pairs: enough workgroups to fill the GPU even
+            // when each pair is small; large pairs walk their candidate tiles in-kernel
+            const int capP = n_t * MT;
+            const int n_split = std::max(1, std::min(n_t, (4096 + n_t * np - 1) / (n_t * np)));
+            const size_t part_bytes = ((size_t)np * n_split * cap * sizeof(Part) + 255) & ~size_t(255);
+            const size_t pk_bytes = (size_t)n_frames * capP * KA * sizeof(unsigned short);
+            int rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes,
+                               norm_bytes + part_bytes + 2 * pk_bytes);
+            if (rc) return rc;
+            float *norms = (float *)ctx->mscratch;
+            Part *parts = (Part *)((char *)ctx->mscratch + norm_bytes);
+            unsigned short *pka = (unsigned short *)((char *)ctx->mscratch + norm_bytes + part_bytes);
+            unsigned short *pkb = (unsigned short *)((char *)pka + pk_bytes);
+            const size_t rows = (size_t)n_frames * capP;
+            {
+                PanoProf prof_(ctx, PK_NORMS);
+                pack_rows<<<(unsigned)((rows * 16 + 255) / 256), 256, 0, ctx->stream>>>(
+                    desc, counts, cap, capP, n_frames, pka, pkb, norms);
+            }
+            PANO_LAUNCH_CHECK(ctx, "pack_rows");
+            dim3 grid(n_split, n_t, np);
+            {
+                PanoProf prof_(ctx, PK_DIST_MFMA);
+                if (p2)
+                    dist_bf16<true><<<grid, 256, 0, ctx->stream>>>(pka, pkb, norms, counts, cap, capP,
+                                                                   pa, parts, n_split);
+                else
+                    dist_bf16<false><<<grid, 256, 0, ctx->stream>>>(pka, pkb, norms, counts, cap, capP,
+                                                                    pa, parts, n_split);
+            }
+            PANO_LAUNCH_CHECK(ctx, "dist_bf16");
+            {
+                PanoProf prof_(ctx, PK_REDUCE);
+                reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_split, bp, p1, p2);
+            }
+            PANO_LAUNCH_CHECK(ctx, "reduce_parts");
+            continue;
+        }
         const size_t part_bytes = (size_t)np * n_t * cap * sizeof(Part);
         int rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes, norm_bytes + part_bytes);
         if (rc) return rc;
         float *norms = (float *)ctx->mscratch;
         Part *parts = (Part *)((char *)ctx->mscratch + norm_bytes);
         const size_t rows = (size_t)n_frames * cap;
-        dim3 grid(n_t, n_t, np);
-        if (exact_int == 2) {
-            // packed bf16 rows live after the partials
-            const size_t pk_off = (norm_bytes + part_bytes + 255) & ~size_t(255);
-            rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes,
-                           pk_off + rows * PANO_DESC_DIM * sizeof(unsigned short));
-            if (rc) return rc;
-            norms = (float *)ctx->mscratch;
-            parts = (Part *)((char *)ctx->mscratch + norm_bytes);
-            unsigned short *pk = (unsigned short *)((char *)ctx->mscratch + pk_off);
-            {
-                PanoProf prof_(ctx, PK_NORMS);
-                pack_rows<<<(unsigned)((rows * 16 + 255) / 256), 256, 0, ctx->stream>>>(
-                    desc, counts, cap, n_frames, pk, norms);
-            }
-            PANO_LAUNCH_CHECK(ctx, "pack_rows");
-            PanoProf prof_(ctx, PK_DIST_MFMA);
-            dist_bf16<<<grid, 256, 0, ctx->stream>>>(pk, norms, counts, cap, pa, parts, n_t);
-        } else {
-            {
-                PanoProf prof_(ctx, PK_NORMS);
-                row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
-            }
-            PANO_LAUNCH_CHECK(ctx, "row_norms");
+        {
+            PanoProf prof_(ctx, PK_NORMS);
+            row_norms<<<(unsigned)((rows + 255) / 256), 256, 0, ctx->stream>>>(desc, counts, cap, n_frames, norms);
+        }
+        PANO_LAUNCH_CHECK(ctx, "row_norms");
+        {
+            dim3 grid(n_t, n_t, np);
             const size_t sm = 2 * (size_t)MT * LDA * sizeof(float);
             PanoProf prof_(ctx, PK_DIST_MFMA);
             dist_mfma<<<grid, 256, sm, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_t);
         }
         PANO_LAUNCH_CHECK(ctx, "dist_mfma");
-        dim3 g2((cap + 255) / 256, np);
         {
             PanoProf prof_(ctx, PK_REDUCE);
             reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_t, bp, p1, p2);

@@ -176,7 +176,8 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
                        const int32_t *counts, int cap, const int32_t *h_pairs, int n_pairs,
                        const int32_t *best, const float *d1, const float *d2,
                        double desc_thresh, double ratio, double thr, pano_pair_rec *recs) {
-    if (cap <= 0 || n_pairs <= 0 || (!kps && !xy_i32) || !counts || !best || !d1 || !d2 || !recs)
+    if (cap <= 0 || n_pairs <= 0 || (!kps && !xy_i32) || !counts || !best || !d1 ||
+        (!d2 && ratio > 0) || !recs)
         return pano_fail(ctx, PANO_E_ARG, "pano_pair_shifts: bad arguments");
     const size_t need = (size_t)n_pairs * cap * (sizeof(double2) + sizeof(int32_t)) + 256;
     int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, need);
@@ -194,7 +195,7 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
             pair_shifts<<<np, RB, 0, ctx->stream>>>(
                 kps, xy_i32, counts, cap, pa, best + (size_t)p0 * cap, d1 + (size_t)p0 * cap,
-                d2 + (size_t)p0 * cap, (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, thr,
+                d2 ? d2 + (size_t)p0 * cap : nullptr, (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, thr,
                 moves + (size_t)p0 * cap, midx + (size_t)p0 * cap, recs + p0);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_shifts");

@@ -25,6 +25,8 @@
 //    integer descriptors to <= 1 LSB.
 #include "pano_internal.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr float kRad2DegF32 = 180.0f / 3.14159265358979323846f;   // numpy f32 rad2deg
@@ -49,7 +51,12 @@ __device__ __forceinline__ unsigned long long rint_fix(double x) {
     return (unsigned long long)(__double_as_longlong(x + magic) - __double_as_longlong(magic));
 }
 constexpr double kDescInv = 1.0 / 1099511627776.0;
-constexpr int kSortMax = 8192;
+// Per-frame scratch capacities scale with the pyramid: raw DoG extrema <= sum(Po) / 32
+// (32768 at 512 x 384, 345k at 1080p), localised candidates and oriented keypoints <= 1/4
+// of that.  Every count is checked against its capacity (PANO_E_OVERFLOW), never clamped
+// silently.
+constexpr int kExtMin = 32768;
+constexpr int kCandMin = 8192;
 
 struct PyrArgs {   // all octaves, for the descriptor (level pointers are per frame batch)
     const float *gauss[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
@@ -608,13 +615,15 @@ rank_keys(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, in
 __global__ void __launch_bounds__(1024)
 emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
                const uint32_t *__restrict__ sorted, pano_kp *__restrict__ out, int cap,
-               int32_t *__restrict__ counts, int32_t *__restrict__ err) {
+               int32_t *__restrict__ counts, int32_t *__restrict__ err,
+               const int32_t *__restrict__ ext_cnt, int ext_cap,
+               const int32_t *__restrict__ cand_cnt, int cand_cap) {
     __shared__ int32_t scan[1024];
     const int f = blockIdx.x, tid = threadIdx.x;
     const RawKp *rec = raw + (size_t)f * raw_cap;
     const uint32_t *idx = sorted + (size_t)f * raw_cap;
     const int cnt = raw_cnt[f * kCntStride];
-    if (cnt > raw_cap) {
+    if (cnt > raw_cap || ext_cnt[f * kCntStride] > ext_cap || cand_cnt[f * kCntStride] > cand_cap) {
         if (tid == 0) { err[0] = PANO_E_OVERFLOW; counts[f] = -1; }
         return;
     }
@@ -923,14 +932,16 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
                           int cap, int32_t *counts) {
     const int n = ctx->n, no = ctx->n_oct, nl = ctx->n_lvl, ni = p->num_intervals;
     if (cap <= 0 || !kps || !desc || !counts) return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
-    // per-frame candidate / raw capacities (raw <= sort capacity)
-    const size_t cand_cap = (size_t)kSortMax;
-    const size_t raw_cap = (size_t)kSortMax;
+    // per-frame candidate / raw capacities, scaled with the pyramid (see kExtMin)
+    size_t spo = 0;
+    for (int o = 0; o < no; ++o) spo += (size_t)ctx->oct_h[o] * ctx->oct_w[o];
+    const size_t ext_cap = std::max<size_t>(kExtMin, ((spo / 32) + 1023) & ~size_t(1023));
+    const size_t cand_cap = std::max<size_t>(kCandMin, ext_cap / 4);
+    const size_t raw_cap = cand_cap;
     int rc = pano_grow(ctx, (void **)&ctx->cands, &ctx->cand_cap, cand_cap * n * sizeof(Cand));
     if (rc) return rc;
     rc = pano_grow(ctx, (void **)&ctx->raw, &ctx->raw_cap, raw_cap * n * sizeof(RawKp));
     if (rc) return rc;
-    const size_t ext_cap = 4 * (size_t)kSortMax;
     rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint32_t));
     if (rc) return rc;
     uint32_t *raw_ext = (uint32_t *)ctx->frame_off;
@@ -1023,7 +1034,8 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         {
             PanoProf prof_(ctx, PK_SORT);
             emit_keypoints<<<n, 1024, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted,
-                                                        kps, cap, counts, err);
+                                                        kps, cap, counts, err, ext_cnt, (int)ext_cap,
+                                                        cand_cnt, (int)cand_cap);
         }
         PANO_LAUNCH_CHECK(ctx, "emit_keypoints");
     }

@@ -57,7 +57,7 @@ class Stitcher:
 
     def __init__(self, method: str = "sift", device: int | None = None, cap: int = 4096,
                  max_points: int = 200, ransac_thr: float = 3.0, desc_thresh: float | None = None,
-                 sift_params: dict | None = None, match: str | None = None):
+                 sift_params: dict | None = None, match: str | None = None, ratio: float = 0.0):
         import os
         import torch
         self.torch = torch
@@ -70,6 +70,9 @@ class Stitcher:
         self.desc_thresh = float(desc_thresh if desc_thresh is not None
                                  else (25000 if method == "sift" else 1.0))
         self.params = _lib.default_sift_params(**(sift_params or {}))
+        # Lowe ratio test (0 = off, as the reference's stitcher; the visualiser uses 0.7 with
+        # FLANN, sift_visualizeUI.py:252-257)
+        self.ratio = float(ratio)
         # SIFT distance GEMM: "bf16" (exact for integer descriptors, 16x MFMA rate) or "f32"
         self.match = match or os.environ.get("PANO_MATCH", "bf16")
         self._buf = {}
@@ -128,16 +131,19 @@ class Stitcher:
         hp = np.ascontiguousarray(np.array(pairs, np.int32).reshape(-1))
         best = self._get("best", (P, cap), T.int32)
         d1 = self._get("d1", (P, cap), T.float32)
-        d2 = self._get("d2", (P, cap), T.float32)
+        # the second-best distance is only computed when the Lowe ratio test needs it (the
+        # reference's stitcher has none: image_stitching_sift.py:63-79)
         exact = (2 if self.match == "bf16" else 1) if self.method == "sift" else 0
+        d2 = self._get("d2", (P, cap), T.float32) if (self.ratio > 0 or exact != 2) else None
+        d2p = ptr(d2) if d2 is not None else None
         self.ctx.check(self.ctx.lib.pano_match(self.ctx.h, ptr(desc), ptr(counts), cap,
-                                               _lib.i32p(hp), P, exact, ptr(best), ptr(d1), ptr(d2)))
+                                               _lib.i32p(hp), P, exact, ptr(best), ptr(d1), d2p))
         recs = self._get("recs", (P, 64), T.uint8)
         kps_p = ptr(pts) if self.method == "sift" else None
         xy_p = None if self.method == "sift" else ptr(pts)
         self.ctx.check(self.ctx.lib.pano_pair_shifts(self.ctx.h, kps_p, xy_p, ptr(counts), cap,
-                                                     _lib.i32p(hp), P, ptr(best), ptr(d1), ptr(d2),
-                                                     self.desc_thresh, 0.0, self.ransac_thr,
+                                                     _lib.i32p(hp), P, ptr(best), ptr(d1), d2p,
+                                                     self.desc_thresh, self.ratio, self.ransac_thr,
                                                      ptr(recs)))
         return recs, (best, d1, d2)
 
@@ -254,7 +260,7 @@ class Stitcher:
             return seg()
         key = ("records", frames_dev.data_ptr(), tuple(frames_dev.shape),
                tuple(float(f) for f in np.asarray(focals, np.float64)), self.method, self.match,
-               bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh)
+               bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh, self.ratio)
         return self._replay(key, seg)
 
     # ------------------------------------------------------------------ whole run
