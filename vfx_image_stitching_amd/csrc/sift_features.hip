@@ -166,7 +166,8 @@ __device__ __forceinline__ bool solve3_lu(const double A[3][3], const double b[3
 // octave of one frame; the ni+2 DoG levels of the tile (+1 halo) are staged in LDS and each
 // pixel is checked against its 26 neighbours there (exact f32 comparisons).  Candidates are
 // appended per frame with their scan-order key; S6 runs densely, thread per candidate.
-constexpr int ETX = 64, ETY = 16;
+constexpr int ETX = 62, ETY = 16;   // output columns / rows of a tile
+constexpr int ELW = 64;             // staged columns (ETX + 2 halo): one per lane
 
 struct DogArgs {
     const float *dog[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
@@ -180,10 +181,12 @@ __device__ __forceinline__ uint32_t scan_key(int o, int layer0, int y, int x) {
     return ((uint32_t)(o * 8 + layer0) << 24) | ((uint32_t)y << 12) | (uint32_t)x;
 }
 
+template <int NL>
 __global__ void __launch_bounds__(256)
-extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict__ raw,
+extrema_scan(DogArgs a, int border, double thresh, uint32_t *__restrict__ raw,
              int32_t *__restrict__ raw_cnt, int raw_cap, int tile_base) {
-    __shared__ float s[PANO_MAX_LEVELS - 1][ETY + 2][ETX + 2];
+    constexpr int ni = NL - 2;
+    __shared__ float s[NL][ETY + 2][ELW];
     __shared__ int wtot[4], wbase;
     const int f = blockIdx.y;
     int t = blockIdx.x + tile_base, o = 0;
@@ -193,46 +196,31 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
     const int x0 = border + (t % a.tiles_x[o]) * ETX;
     const int y0 = border + (t / a.tiles_x[o]) * ETY;
     const int tid = threadIdx.x;
-    const int nl = ni + 2;
-    // stage the ni+2 DoG levels of the tile (+1 halo): wave w stages rows w, w+4, ... of the
-    // (level, row) list with lane = column; the two right-halo columns of every row are one
-    // extra load per thread.  Level / row are wave-uniform and all of a thread's loads are
-    // issued before the first LDS store (one memory round trip for ni <= 3).
-    const int lane = tid & 63, wv = tid >> 6;
-    const int nrows = nl * (ETY + 2);
-    const int gxa = min(x0 - 1 + lane, W - 1);
-    constexpr int RB = 24;                       // rows per wave per batch (90 rows at ni = 3)
-    for (int r0 = wv; r0 < nrows; r0 += 4 * RB) {
-        float va[RB];
-        float vh = 0.0f;
-        const int hr = r0 - wv + (tid >> 1);       // right-halo: (row, column 64 + (tid & 1))
-        const bool hv = (tid >> 1) < 4 * RB && hr < nrows;
-        if (hv) {
-            const int l = hr / (ETY + 2), yy = hr - l * (ETY + 2);
+    // stage the NL DoG levels of the tile (+1 halo): wave w stages (level, row) w, w+4, ...
+    // with lane = column (62 outputs + 2 halo columns per row).  Level and row are scalar
+    // (readfirstlane), so each staged row is one scalar row pointer + one coalesced load;
+    // all of a lane's loads are issued before its first LDS store.
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int NROWS = NL * (ETY + 2);
+    constexpr int RB = (NROWS + 3) / 4;
+    const int gx = min(x0 - 1 + lane, W - 1);
+    float va[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+        const int rr = wv + 4 * u;
+        if (rr < NROWS) {
+            const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
             const int gy = min(y0 - 1 + yy, H - 1);
-            vh = a.dog[o][l][((size_t)f * H + gy) * W + min(x0 + 63 + (tid & 1), W - 1)];
+            va[u] = a.dog[o][l][((size_t)f * H + gy) * W + gx];
         }
+    }
 #pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int rr = r0 + 4 * u;
-            va[u] = 0.0f;
-            if (rr < nrows) {
-                const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
-                const int gy = min(y0 - 1 + yy, H - 1);
-                va[u] = a.dog[o][l][((size_t)f * H + gy) * W + gxa];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int rr = r0 + 4 * u;
-            if (rr < nrows) {
-                const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
-                s[l][yy][lane] = va[u];
-            }
-        }
-        if (hv) {
-            const int l = hr / (ETY + 2), yy = hr - l * (ETY + 2);
-            s[l][yy][64 + (tid & 1)] = vh;
+    for (int u = 0; u < RB; ++u) {
+        const int rr = wv + 4 * u;
+        if (rr < NROWS) {
+            const int l = rr / (ETY + 2), yy = rr - l * (ETY + 2);
+            s[l][yy][lane] = va[u];
         }
     }
     __syncthreads();
@@ -241,17 +229,16 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
     // horizontal then 3-tall vertical max/min per level in registers (4 output rows per
     // thread), then the 3-level max/min per layer.  Exact: only f32 max/min/compare.
     constexpr int RPT = ETY / 4;                  // output rows per thread
-    static_assert(ETX == 64 && ETY % 4 == 0, "lane = column, 4 row groups");
+    static_assert(ETX + 2 == ELW && ETY % 4 == 0, "lane = column, 4 row groups");
     const int py0 = wv * RPT;
-    float vmx[PANO_MAX_LEVELS - 1][RPT], vmn[PANO_MAX_LEVELS - 1][RPT];
+    float vmx[NL][RPT], vmn[NL][RPT];
 #pragma unroll
-    for (int l = 0; l < PANO_MAX_LEVELS - 1; ++l) {
-        if (l >= nl) break;
+    for (int l = 0; l < NL; ++l) {
         float hmx[RPT + 2], hmn[RPT + 2];
 #pragma unroll
         for (int r = 0; r < RPT + 2; ++r) {
-            const float *row = &s[l][py0 + r][lane];
-            const float a0 = row[0], a1 = row[1], a2 = row[2];
+            const float *row = &s[l][py0 + r][0];
+            const float a0 = row[lane], a1 = row[min(lane + 1, ELW - 1)], a2 = row[min(lane + 2, ELW - 1)];
             hmx[r] = fmaxf(fmaxf(a0, a1), a2);
             hmn[r] = fminf(fminf(a0, a1), a2);
         }
@@ -263,14 +250,13 @@ extrema_scan(DogArgs a, int ni, int border, double thresh, uint32_t *__restrict_
     }
     const int x = x0 + lane;
     uint32_t hits = 0;                            // bit i * 8 + L: extremum at row i, layer L
-    if (x < W - border) {
+    if (lane < ETX && x < W - border) {
 #pragma unroll
         for (int i = 0; i < RPT; ++i) {
             const int py = py0 + i, y = y0 + py;
             if (y >= H - border) break;
 #pragma unroll
-            for (int L = 1; L < PANO_MAX_LEVELS - 2; ++L) {
-                if (L > ni) break;
+            for (int L = 1; L <= ni; ++L) {
                 const float v = s[L][py + 1][lane + 1];
                 if (!((double)fabsf(v) > thresh)) continue;
                 const bool ext = v > 0
@@ -991,8 +977,17 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
             dim3 grid(t1 - t0, n);
             {
                 PanoProf prof_(ctx, PK_EXTREMA);
-                extrema_scan<<<grid, 256, 0, ctx->stream>>>(da, ni, p->border, lp.thresh, raw_ext,
-                                                            ext_cnt, (int)ext_cap, t0);
+#define PANO_EXTREMA(NLV) extrema_scan<NLV><<<grid, 256, 0, ctx->stream>>>(da, p->border, lp.thresh, \
+                                                                raw_ext, ext_cnt, (int)ext_cap, t0)
+                switch (ni + 2) {            // DoG levels per octave
+                    case 3: PANO_EXTREMA(3); break;
+                    case 4: PANO_EXTREMA(4); break;
+                    case 5: PANO_EXTREMA(5); break;
+                    case 6: PANO_EXTREMA(6); break;
+                    case 7: PANO_EXTREMA(7); break;
+                    default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "num_intervals above 5");
+                }
+#undef PANO_EXTREMA
             }
             PANO_LAUNCH_CHECK(ctx, "extrema_scan");
         }

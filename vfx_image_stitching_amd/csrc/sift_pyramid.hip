@@ -57,63 +57,97 @@ __device__ __forceinline__ int reflect_fast(int i, int n) {
     return (unsigned)i < (unsigned)n ? i : reflect101(i, n);
 }
 
-// Tile staging split into a per-lane column part (computed once per lane) and a per-row
-// part (wave-uniform), so the inner staging loop is one or a few loads per element.
+// Tile staging.  Wave w stages tile rows w, w + NW, ... with lane = column (lane and
+// 64 + lane): every row quantity (source row, reflection, bilinear row weights) is computed
+// once per row in scalar registers (the row index is readfirstlane'd), every column
+// quantity once per lane, so a staged element costs its load(s) and an LDS store.
+struct ColMap {          // per-lane column part of a stager
+    int c0, c1;          // source column(s)
+    float w1;            // MODE_BASE: bilinear weight of c1
+};
+
 template <int MODE> struct Stager;
 
-template <> struct Stager<MODE_LEVEL> {
-    const float *src;
-    int W;
-    __device__ Stager(const LoadArgs &a, int f, int H, int W_, int x)
-        : src(a.src + (size_t)f * H * W_ + x), W(W_) {}
-    __device__ __forceinline__ float get(int gy) const { return src[(size_t)gy * W]; }
+template <> struct Stager<MODE_LEVEL> {   // plain: source = previous level of this octave
+    const float *base;
+    int W, H;
+    __device__ Stager(const LoadArgs &a, int f, int H_, int W_) : base(a.src + (size_t)f * H_ * W_), W(W_), H(H_) {}
+    __device__ __forceinline__ ColMap col(int x) const { return ColMap{reflect_fast(x, W), 0, 0.f}; }
+    __device__ __forceinline__ float get(int y, const ColMap &c) const {
+        return base[(size_t)reflect_fast(y, H) * W + c.c0];
+    }
 };
 
-template <> struct Stager<MODE_DOWN> {   // OpenCV INTER_NEAREST 1/2 of the previous octave
-    const float *src;
-    int sx, sw, sh;
-    double ify;
-    __device__ Stager(const LoadArgs &a, int f, int H, int W, int x) {
-        (void)H;
-        (void)W;
-        src = a.src + (size_t)f * a.sh * a.sw;
-        sw = a.sw;
-        sh = a.sh;
-        ify = a.ify;
-        const int t = (int)floor(x * a.ifx);
-        sx = t < a.sw - 1 ? t : a.sw - 1;
+template <> struct Stager<MODE_DOWN> {    // OpenCV INTER_NEAREST 1/2 of the previous octave
+    const float *base;
+    int W, H, sh, sw;
+    double ifx, ify;
+    __device__ Stager(const LoadArgs &a, int f, int H_, int W_)
+        : base(a.src + (size_t)f * a.sh * a.sw), W(W_), H(H_), sh(a.sh), sw(a.sw), ifx(a.ifx), ify(a.ify) {}
+    __device__ __forceinline__ ColMap col(int x) const {
+        const int t = (int)floor(reflect_fast(x, W) * ifx);
+        return ColMap{t < sw - 1 ? t : sw - 1, 0, 0.f};
     }
-    __device__ __forceinline__ float get(int gy) const {
-        int sy = (int)floor(gy * ify);
+    __device__ __forceinline__ float get(int y, const ColMap &c) const {
+        int sy = (int)floor(reflect_fast(y, H) * ify);
         sy = sy < sh - 1 ? sy : sh - 1;
-        return src[(size_t)sy * sw + sx];
+        return base[(size_t)sy * sw + c.c0];
     }
 };
 
-template <> struct Stager<MODE_BASE> {   // gray (u8) -> x2 INTER_LINEAR, exact
+template <> struct Stager<MODE_BASE> {    // gray (u8) -> x2 INTER_LINEAR, exact
     const uint8_t *fr;
-    int c0, c1, sh, sw;
-    float wx, wx0;
-    __device__ Stager(const LoadArgs &a, int f, int H, int W, int x) {
-        (void)H;
-        (void)W;
-        sh = a.sh;
-        sw = a.sw;
-        fr = a.gray + (size_t)f * a.sh * a.sw;
-        lin_map(x, a.sw, c0, c1, wx);
-        wx0 = 1.0f - wx;
+    int W, H, sh, sw;
+    __device__ Stager(const LoadArgs &a, int f, int H_, int W_)
+        : fr(a.gray + (size_t)f * a.sh * a.sw), W(W_), H(H_), sh(a.sh), sw(a.sw) {}
+    __device__ __forceinline__ ColMap col(int x) const {
+        ColMap c;
+        lin_map(reflect_fast(x, W), sw, c.c0, c.c1, c.w1);
+        return c;
     }
-    __device__ __forceinline__ float get(int gy) const {
+    __device__ __forceinline__ float get(int y, const ColMap &c) const {
         int y0, y1;
         float wy;
-        lin_map(gy, sh, y0, y1, wy);
-        const float g00 = fr[(size_t)y0 * sw + c0], g01 = fr[(size_t)y0 * sw + c1];
-        const float g10 = fr[(size_t)y1 * sw + c0], g11 = fr[(size_t)y1 * sw + c1];
-        const float h0 = g00 * wx0 + g01 * wx;
-        const float h1 = g10 * wx0 + g11 * wx;
+        lin_map(reflect_fast(y, H), sh, y0, y1, wy);
+        const uint8_t *r0 = fr + (size_t)y0 * sw, *r1 = fr + (size_t)y1 * sw;
+        const float g00 = r0[c.c0], g01 = r0[c.c1];
+        const float g10 = r1[c.c0], g11 = r1[c.c1];
+        const float wx0 = 1.0f - c.w1;
+        const float h0 = g00 * wx0 + g01 * c.w1;
+        const float h1 = g10 * wx0 + g11 * c.w1;
         return h0 * (1.0f - wy) + h1 * wy;
     }
 };
+
+// Stage the (ih x iw) input tile whose top-left source pixel is (y0 - R, x0 - R) into
+// t[ih][IWP] (iw <= 128).  NW waves; all of a lane's loads are issued before its stores.
+template <int MODE, int NW, int RPW>
+__device__ __forceinline__ void stage_tile(const LoadArgs &la, int f, int H, int W, int x0, int y0,
+                                           int R, int ih, int iw, int IWP, float *t) {
+    const Stager<MODE> sg(la, f, H, W);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool has1 = 64 + lane < iw;
+    const ColMap m0 = sg.col(x0 - R + lane);
+    const ColMap m1 = sg.col(x0 - R + (has1 ? 64 + lane : lane));
+    float v0[RPW], v1[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        const int ty = wv + NW * k;
+        if (ty < ih) {
+            v0[k] = sg.get(y0 - R + ty, m0);
+            v1[k] = has1 ? sg.get(y0 - R + ty, m1) : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        const int ty = wv + NW * k;
+        if (ty < ih) {
+            t[ty * IWP + lane] = v0[k];
+            if (has1) t[ty * IWP + 64 + lane] = v1[k];
+        }
+    }
+}
 
 // cvtColor(BGR2GRAY) of every frame, 4 pixels per thread (sift_impl.py:27-28).
 __global__ void __launch_bounds__(256)
@@ -181,16 +215,8 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     const int tid = threadIdx.x;
     const int ih = th + 2 * r, iw = tw + 2 * r;              // staged extent actually needed
 
-    {
-        // lane -> staged column tid % 128 (iw <= 64 + 62 < 128), rows step 2 per half-block
-        const int cx = tid & 127;
-        if (cx < iw) {
-            const Stager<MODE> sg(la, f, H, W, reflect_fast(x0 - r + cx, W));
-#pragma unroll 4
-            for (int ty = tid >> 7; ty < ih; ty += 2)
-                tin[ty * IWP + cx] = sg.get(reflect_fast(y0 - r + ty, H));
-        }
-    }
+    for (int yb = 0; yb < ih; yb += 64)       // generic tap count: rows in chunks of 64
+        stage_tile<MODE, 4, 16>(la, f, H, W, x0, y0 + yb, r, min(64, ih - yb), iw, IWP, tin + yb * IWP);
     __syncthreads();
     if constexpr (NT > 0) {
         // row pass: lanes walk consecutive rows (odd pitch), each SEG outputs along x
@@ -246,7 +272,7 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
 // busy) writes level, DoG and level-0 copy.  Half the LDS of a two-tile design, twice the
 // waves per CU; per output the arithmetic is blur_level's (sequential fma in tap order).
 template <int MODE, int NT>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512, 6)
 blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
           float *__restrict__ in_copy, int H, int W, Taps taps) {
     constexpr int R = (NT - 1) / 2;
@@ -259,15 +285,7 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     const int tw = min(TX, W - x0), th = min(TY, H - y0);
     const int tid = threadIdx.x;
     const int ih = th + 2 * R, iw = tw + 2 * R;
-    {
-        const int cx = tid & 127;
-        if (cx < iw) {
-            const Stager<MODE> sg(la, f, H, W, reflect_fast(x0 - R + cx, W));
-#pragma unroll 4
-            for (int ty = tid >> 7; ty < ih; ty += 4)
-                tin[ty * IWP + cx] = sg.get(reflect_fast(y0 - R + ty, H));
-        }
-    }
+    stage_tile<MODE, 8, (TY + 2 * R + 7) / 8>(la, f, H, W, x0, y0, R, ih, iw, IWP, tin);
     __syncthreads();
     // column-pass item of this thread and its centres (before the row pass overwrites them)
     const int nrs = (th + SC - 1) / SC;
@@ -277,29 +295,22 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
 #pragma unroll
     for (int j = 0; j < SC; ++j)
         cen[j] = (CENTER && colw) ? tin[(crs * SC + j + R) * IWP + cxp + R] : 0.0f;
-    // row pass, in place
+    // row pass, in place: each thread reads its SR + NT - 1 inputs and accumulates its SR
+    // outputs before the barrier (inputs streamed, not held), then overwrites them
     const int nseg = (tw + SR - 1) / SR;
     const bool roww = tid < ih * nseg;
     const int row = roww ? tid % ih : 0, sg = roww ? tid / ih : 0;
-    float v[SR + NT - 1];
-#pragma unroll
-    for (int i = 0; i < SR + NT - 1; ++i) v[i] = roww ? tin[row * IWP + sg * SR + i] : 0.0f;
-    __syncthreads();
+    float ro[SR];
     if (roww) {
         double acc[SR];
+        conv_seg<NT, SR>(tin + row * IWP + sg * SR, 1, taps.k, acc);
 #pragma unroll
-        for (int j = 0; j < SR; ++j) acc[j] = 0.0;
+        for (int j = 0; j < SR; ++j) ro[j] = (float)acc[j];
+    }
+    __syncthreads();
+    if (roww) {
 #pragma unroll
-        for (int i = 0; i < SR + NT - 1; ++i) {
-            const double x = (double)v[i];
-#pragma unroll
-            for (int j = 0; j < SR; ++j) {
-                const int t = i - j;
-                if (t >= 0 && t < NT) acc[j] = fma(taps.k[t], x, acc[j]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < SR; ++j) tin[row * IWP + sg * SR + j] = (float)acc[j];
+        for (int j = 0; j < SR; ++j) tin[row * IWP + sg * SR + j] = ro[j];
     }
     __syncthreads();
     if (!colw) return;
