@@ -705,22 +705,42 @@ struct DescParams {
     float max_value;   // f32(descriptor_max_value)
 };
 
-constexpr int kDescWin = 4096;
+// Wave-level restatement of sdot_skx(x, 128) (OpenBLAS SkylakeX order): lane L holds
+// x[L] and x[64 + L]; returns the same float on every lane.
+__device__ __forceinline__ float sdot_skx_wave128(float lo, float hi) {
+    const int lane = threadIdx.x & 63;
+    const float a16 = fmaf(hi, hi, fmaf(lo, lo, 0.0f));              // a16[k][j], L = 16k + j
+    const float a8 = a16 + __shfl(a16, (lane & ~15) | ((lane + 8) & 15));   // valid for j < 8
+    // v[j] = ((a8[0][j] + a8[1][j]) + a8[2][j]) + a8[3][j], j < 8 (a8[k][j] at lane 16k + j)
+    const int j = lane & 7;
+    const float v = ((__shfl(a8, j) + __shfl(a8, 16 + j)) + __shfl(a8, 32 + j)) + __shfl(a8, 48 + j);
+    const float h = v + __shfl(v, (j + 4) & 7);                      // h[j] = v[j] + v[j + 4], j < 4
+    const float kern = (__shfl(h, 0) + __shfl(h, 1)) + (__shfl(h, 2) + __shfl(h, 3));
+    return (float)((double)kern + 0.0);
+}
+
+// Descriptors, one WAVE per keypoint (4 keypoints per workgroup, no block barriers): the
+// wave derives, per patch column, the row interval inside the rotated square and the image
+// (conservative; `sample` applies the exact bin test), scans the interval lengths into a
+// dense sample index, and each lane walks its own run of that index, spreading into the
+// wave's 2^40 fixed-point histogram (integer sums: order independent).  The normalisation
+// is the reference's, with np.linalg.norm in OpenBLAS's sdot order across the lanes.
+constexpr int kDescCols = 256;   // patch sides up to this use the dense index
 
 __global__ void __launch_bounds__(256)
-descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
-           const int32_t *__restrict__ counts, int cap, float *__restrict__ desc) {
-    __shared__ unsigned long long acc[4][128];   // one histogram per wave
-    __shared__ uint32_t list[kDescWin];          // compacted candidate samples (xi << 16 | yi)
-    __shared__ int list_n;
-    __shared__ int col_lo[256], col_pre[257], wtot[4];
-    __shared__ float vec[128];
-    __shared__ float sh_norm;
-    const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
+                const int32_t *__restrict__ counts, int cap, float *__restrict__ desc) {
+    __shared__ unsigned long long acc[4][128];
+    __shared__ int col_lo[4][kDescCols], col_pre[4][kDescCols + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int f = blockIdx.y;
+    const int k = blockIdx.x * 4 + wv;
     int cnt = counts[f];
     cnt = cnt < cap ? cnt : cap;
-    if (k >= cnt) return;
-    for (int i = tid; i < 4 * 128; i += 256) (&acc[0][0])[i] = 0ull;
+    if (k >= cnt) return;                                  // whole wave
+    unsigned long long *wacc = acc[wv];
+    wacc[lane] = 0ull;
+    wacc[64 + lane] = 0ull;
     const pano_kp kp = kps[(size_t)f * cap + k];
     int oct = kp.octave & 255;
     if (oct >= 128) oct |= -128;
@@ -742,21 +762,8 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     const int side = 2 * half + 1;
     const float angle_f = (float)angle;
     const float bins_per_deg = (float)(8.0 / 360.0);
-    __syncthreads();
-    // Samples: the 4 x 4 bins cover a rotated square of half-width 2.5 hw inside the
-    // (2 half + 1)^2 patch, so about half the patch is outside.  For patches up to 256
-    // columns each thread derives, for one column, the row interval inside the rotated square
-    // and the image (conservative; `sample` applies the exact bin test), a block scan turns
-    // the interval lengths into a dense sample index, and the threads walk that index (column
-    // by binary search).  Larger patches compact candidates through an LDS list instead.
-    // The fixed-point histogram sums are integers, hence independent of the sample order.
-    const int S = side * side;
-    const int lane = tid & 63, wv = tid >> 6;
-    unsigned long long *wacc = acc[wv];
     const double inv_hwd = 1.0 / hwd;
     const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hwd < 2.5 with slack
-    // one sample (column xi, row yi of the square patch): exact bin test, gradient, weight,
-    // trilinear split into this wave's fixed-point histogram
     auto sample = [&](int xi, int yi) {
         const int xs = xi - half, ys = yi - half;
         const int rr = py + ys, cc = px + xs;
@@ -766,8 +773,9 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         const double rbin = (rq + 2.0) - 0.5;
         const double cbin = (cq + 2.0) - 0.5;
         if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) return;
-        const float gx = img[(size_t)rr * cols + cc + 1] - img[(size_t)rr * cols + cc - 1];
-        const float gy = img[(size_t)(rr - 1) * cols + cc] - img[(size_t)(rr + 1) * cols + cc];
+        const float *q = img + (size_t)rr * cols + cc;
+        const float gx = q[1] - q[-1];
+        const float gy = q[-cols] - q[cols];
         const float mag = sqrtf(gx * gx + gy * gy);
         const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
         const double w = exp(-0.125 * (rq * rq + cq * cq));
@@ -781,133 +789,118 @@ descriptor(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         const double c0w = wm - c1;
         const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rb = r0 + 1 + (q >> 1), cb = c0 + 1 + (q & 1);
+        for (int qd = 0; qd < 4; ++qd) {
+            const int rb = r0 + 1 + (qd >> 1), cb = c0 + 1 + (qd & 1);
             if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
             const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
-            const double v0 = part[q] * (1 - of);
-            const double v1 = part[q] * of;
+            const double v0 = part[qd] * (1 - of);
+            const double v1 = part[qd] * of;
             atomicAdd(&wacc[base + o0], rint_fix(v0));
             atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1));
         }
     };
-    if (side <= 256) {
-        int lo = 1, hi = 0;
-        if (tid < side) {
-            const int xs = tid - half, cc = px + xs;
-            if (cc > 0 && cc < cols - 1) {
-                lo = max(-half, 1 - py);
-                hi = min(half, rows - 2 - py);
-                // |a ys + b| < lim  ->  ys in an interval (rrot: a = cos, b = xs sin;
-                // crot: a = -sin, b = xs cos), widened by 1e-6 and clipped before rounding
-                const double ab[2][2] = {{cos_a, xs * sin_a}, {-sin_a, xs * cos_a}};
-                for (int q = 0; q < 2; ++q) {
-                    const double av = ab[q][0], bv = ab[q][1];
-                    if (fabs(av) < 1e-12) {
-                        if (!(fabs(bv) < lim)) hi = lo - 1;
-                        continue;
+    if (side <= kDescCols) {
+        int *clo = col_lo[wv], *cpre = col_pre[wv];
+        int run = 0;                                       // wave-wide running total
+#pragma unroll
+        for (int c4 = 0; c4 < kDescCols; c4 += 64) {
+            if (c4 >= side) break;
+            const int c = c4 + lane;
+            int lo = 1, hi = 0;
+            if (c < side) {
+                const int xs = c - half, cc = px + xs;
+                if (cc > 0 && cc < cols - 1) {
+                    lo = max(-half, 1 - py);
+                    hi = min(half, rows - 2 - py);
+                    // |a ys + b| < lim  ->  ys in an interval (rrot: a = cos, b = xs sin;
+                    // crot: a = -sin, b = xs cos), widened by 1e-6 and clipped before rounding
+                    const double ab[2][2] = {{cos_a, xs * sin_a}, {-sin_a, xs * cos_a}};
+#pragma unroll
+                    for (int qd = 0; qd < 2; ++qd) {
+                        const double av = ab[qd][0], bv = ab[qd][1];
+                        if (fabs(av) < 1e-12) {
+                            if (!(fabs(bv) < lim)) hi = lo - 1;
+                            continue;
+                        }
+                        const double t1 = (-lim - bv) / av, t2 = (lim - bv) / av;
+                        const double l = fmax(fmin(t1, t2) - 1e-6, -half - 1.0);
+                        const double u = fmin(fmax(t1, t2) + 1e-6, half + 1.0);
+                        lo = max(lo, (int)ceil(l));
+                        hi = min(hi, (int)floor(u));
                     }
-                    const double t1 = (-lim - bv) / av, t2 = (lim - bv) / av;
-                    const double l = fmax(fmin(t1, t2) - 1e-6, -half - 1.0);
-                    const double u = fmin(fmax(t1, t2) + 1e-6, half + 1.0);
-                    lo = max(lo, (int)ceil(l));
-                    hi = min(hi, (int)floor(u));
                 }
             }
-        }
-        const int cnt = hi >= lo ? hi - lo + 1 : 0;
-        int incl = cnt;                                     // block exclusive scan of cnt
+            const int n_c = hi >= lo ? hi - lo + 1 : 0;
+            int incl = n_c;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int t = __shfl_up(incl, d);
-            if (lane >= d) incl += t;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int t = __shfl_up(incl, d);
+                if (lane >= d) incl += t;
+            }
+            if (c < side) {
+                clo[c] = lo;
+                cpre[c] = run + incl - n_c;
+            }
+            run += __shfl(incl, 63);
         }
-        if (lane == 63) wtot[wv] = incl;
-        __syncthreads();
-        int pre = incl - cnt;
-        for (int w2 = 0; w2 < wv; ++w2) pre += wtot[w2];
-        const int total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-        if (tid < side) {
-            col_lo[tid] = lo;
-            col_pre[tid] = pre;
-        }
-        if (tid == 0) col_pre[side] = total;
-        __syncthreads();
-        // thread t takes the run [t Q, t Q + Q) of the dense index: neighbouring lanes are Q
-        // samples apart (different cells / orientations -> few same-address LDS atomics);
-        // one binary search per thread, then a column-by-column walk
-        const int Q = (total + 255) >> 8;
-        int t = tid * Q;
+        if (lane == 0) cpre[side] = run;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // lane L takes the run [L Q, L Q + Q) of the dense index: one binary search, then a
+        // column-by-column walk (neighbouring lanes are Q samples apart: different cells /
+        // orientations, few same-address LDS atomics)
+        const int total = run;
+        const int Q = (total + 63) >> 6;
+        int t = lane * Q;
         const int tend = min(t + Q, total);
         if (t < tend) {
-            int c = 0, c1 = side - 1;                       // largest c with col_pre[c] <= t
+            int c = 0, c1 = side - 1;                      // largest c with cpre[c] <= t
             while (c < c1) {
                 const int mid = (c + c1 + 1) >> 1;
-                if (col_pre[mid] <= t) c = mid;
+                if (cpre[mid] <= t) c = mid;
                 else c1 = mid - 1;
             }
-            int r = t - col_pre[c];
+            int r = t - cpre[c];
+            int ncol = cpre[c + 1] - cpre[c];
             for (; t < tend; ++t, ++r) {
-                while (r >= col_pre[c + 1] - col_pre[c]) {
-                    r -= col_pre[c + 1] - col_pre[c];
+                while (r >= ncol) {
+                    r -= ncol;
                     ++c;
+                    ncol = cpre[c + 1] - cpre[c];
                 }
-                sample(c, col_lo[c] + r + half);
+                sample(c, clo[c] + r + half);
             }
         }
     } else {
-        const float inv_side = 1.0f / (float)side;
-        for (int win = 0; win < S; win += kDescWin) {
-            if (tid == 0) list_n = 0;
-            __syncthreads();
-            const int wend = min(win + kDescWin, S);
-            for (int j = win + tid; j < wend + ((256 - (wend - win) % 256) % 256); j += 256) {
-                bool ok = false;
-                int xi = 0, yi = 0;
-                if (j < wend) {
-                    // column-major j -> (xi, yi); the f32 quotient is exact for side < 2048
-                    xi = side < 2048 ? (int)(((float)j + 0.5f) * inv_side) : j / side;
-                    yi = j - xi * side;
-                    const int xs = xi - half, ys = yi - half;
-                    const int rr = py + ys, cc = px + xs;
-                    const double rrot = (double)xs * sin_a + (double)ys * cos_a;
-                    const double crot = (double)xs * cos_a - (double)ys * sin_a;
-                    ok = rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1 && fabs(rrot) < lim &&
-                         fabs(crot) < lim;
-                }
-                const unsigned long long m = __ballot(ok);
-                int off = 0;
-                if (lane == 0 && m) off = atomicAdd(&list_n, __popcll(m));
-                off = __shfl(off, 0);
-                if (ok) list[off + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)(xi << 16 | yi);
-            }
-            __syncthreads();
-            const int nl = list_n;
-            for (int t = tid; t < nl; t += 256) sample((int)(list[t] >> 16), (int)(list[t] & 0xffff));
-            __syncthreads();
+        // very large patches: every sample of the (side x side) square, cheap range test first
+        const int S = side * side;
+        for (int j = lane; j < S; j += 64) {
+            const int xi = j / side, yi = j - (j / side) * side;
+            const int xs = xi - half, ys = yi - half;
+            const int rr = py + ys, cc = px + xs;
+            if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
+            const double rrot = (double)xs * sin_a + (double)ys * cos_a;
+            const double crot = (double)xs * cos_a - (double)ys * sin_a;
+            if (fabs(rrot) < lim && fabs(crot) < lim) sample(xi, yi);
         }
     }
-    __syncthreads();
-    if (tid < 128) {
-        const unsigned long long t = acc[0][tid] + acc[1][tid] + acc[2][tid] + acc[3][tid];
-        vec[tid] = (float)((double)(long long)t * kDescInv);
-    }
-    __syncthreads();
-    if (tid == 0) sh_norm = sqrtf(sdot_skx(vec, 128)) * dp.max_value;
-    __syncthreads();
-    if (tid < 128 && vec[tid] > sh_norm) vec[tid] = sh_norm;
-    __syncthreads();
-    if (tid == 0) {
-        float nv = sqrtf(sdot_skx(vec, 128));
-        if (nv < 1e-7f) nv = 1e-7f;
-        sh_norm = nv;
-    }
-    __syncthreads();
-    if (tid < 128) {
-        float d = rintf(512.0f * (vec[tid] / sh_norm));
-        d = d < 0.0f ? 0.0f : (d > 255.0f ? 255.0f : d);
-        desc[((size_t)f * cap + k) * PANO_DESC_DIM + tid] = d;
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float lo = (float)((double)(long long)wacc[lane] * kDescInv);
+    float hi = (float)((double)(long long)wacc[64 + lane] * kDescInv);
+    const float thr = sqrtf(sdot_skx_wave128(lo, hi)) * dp.max_value;
+    lo = lo > thr ? thr : lo;
+    hi = hi > thr ? thr : hi;
+    float nv = sqrtf(sdot_skx_wave128(lo, hi));
+    if (nv < 1e-7f) nv = 1e-7f;
+    float dlo = rintf(512.0f * (lo / nv)), dhi = rintf(512.0f * (hi / nv));
+    dlo = dlo < 0.0f ? 0.0f : (dlo > 255.0f ? 255.0f : dlo);
+    dhi = dhi < 0.0f ? 0.0f : (dhi > 255.0f ? 255.0f : dhi);
+    float *out = desc + ((size_t)f * cap + k) * PANO_DESC_DIM;
+    out[lane] = dlo;
+    out[64 + lane] = dhi;
 }
 
 }  // namespace
@@ -1036,10 +1029,10 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     }
     {
         DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
-        dim3 grid(cap, n);
+        dim3 grid((cap + 3) / 4, n);
         {
             PanoProf prof_(ctx, PK_DESC);
-            descriptor<<<grid, 256, 0, ctx->stream>>>(pa, dp, kps, counts, cap, desc);
+            descriptor_wave<<<grid, 256, 0, ctx->stream>>>(pa, dp, kps, counts, cap, desc);
         }
         PANO_LAUNCH_CHECK(ctx, "descriptor");
     }

@@ -333,12 +333,18 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
 // ------------------------------------------------------------------ small-octave tail
 // Octaves whose levels fit one 64 x 64 tile are latency-bound as separate launches (one
 // tiny workgroup per frame, ~7 us each, 5 per octave).  blur_tail runs them all in ONE
-// launch: a 1024-thread workgroup per frame keeps the current level in LDS and cascades
+// launch: a 512-thread workgroup per frame keeps the current level in LDS and cascades
 // level by level, octave by octave (nearest 1/2 of level n_lvl-3 seeds the next octave),
-// writing every Gaussian level and DoG to HBM.  Per output it is the same arithmetic as
-// blur_level (sequential fma in tap order, one f32 rounding per pass), hence bit-identical.
+// writing every Gaussian level and DoG to HBM.  No halo copy: the row pass computes only
+// the H image rows (a reflected halo row IS the row pass of an image row), reading its
+// reflected columns directly; the column pass reads reflected rows of the row-pass output.
+// Two barriers per level.  Odd LDS pitch (65): lanes on consecutive rows / columns are
+// bank-conflict free.  Per output it is blur_level's arithmetic (sequential fma in tap
+// order, one f32 rounding per pass), hence bit-identical.
 constexpr int kTailDim = 64;
 constexpr int kTailOct = 8;
+constexpr int kTP = kTailDim + 1;             // LDS pitch
+constexpr int kTailThreads = 512;
 
 struct TailArgs {
     const float *prev;                          // G[o_tail-1][n_lvl-3], frame stride ph*pw
@@ -346,7 +352,7 @@ struct TailArgs {
     float *G[kTailOct][PANO_MAX_LEVELS];        // level planes (frame 0)
     float *D[kTailOct][PANO_MAX_LEVELS];        // DoG planes (frame 0)
     int H[kTailOct], W[kTailOct];
-    int n_oct, n_lvl, rmax;
+    int n_oct, n_lvl;
     const double *taps;                         // [n_lvl][PANO_MAX_TAPS], level 0 unused
     int ntap[PANO_MAX_LEVELS];
 };
@@ -355,64 +361,109 @@ __device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_N
     return (int)floor(d * inv);
 }
 
-// One tail level for a compile-time tap count: halo staging with the in-range reflect
-// first, register-blocked row pass (8 outputs per thread) into rowt, register-blocked column
-// pass (8 outputs per thread) writing the LDS level, the Gaussian level and the DoG.
-// Taps are uniform loads kept in registers.  Caller synchronises after it.
+// One tail level, compile-time tap count (NT = 0: runtime count n).  in / outb / rowt are
+// [64][kTP] LDS planes; g / d the frame's Gaussian and DoG planes in HBM.  SG outputs per
+// thread per pass (register-blocked sliding window, taps in tap order).
 template <int NT>
-__device__ __forceinline__ void tail_level(const float *in, float *outb, float *halo, float *rowt,
-                                           int HPP, int H, int W,
-                                           const double *__restrict__ taps_g, float *g, float *d,
-                                           int tid) {
-    constexpr int R = (NT - 1) / 2, SG = 8, P = kTailDim;
-    const int hh = H + 2 * R, hw = W + 2 * R;
-    {
-        const int cx = tid & 127;                  // hw <= 64 + 2 * 13 < 128
-        if (cx < hw) {
-            const int sx = reflect_fast(cx - R, W);
-            for (int y = tid >> 7; y < hh; y += 8) halo[y * HPP + cx] = in[reflect_fast(y - R, H) * P + sx];
-        }
-    }
-    double k[NT];
+__device__ __forceinline__ void tail_level(const float *in, float *outb, float *rowt, int H, int W,
+                                           const double *__restrict__ taps_g, int n_rt, float *g,
+                                           float *d, int tid) {
+    constexpr int SG = 8;
+    const int n = NT > 0 ? NT : n_rt;
+    const int R = (n - 1) / 2;
+    constexpr int KMAX = NT > 0 ? NT : PANO_MAX_TAPS;
+    double k[NT > 0 ? NT : 1];
+    if constexpr (NT > 0) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) k[t] = taps_g[t];
-    __syncthreads();
+        for (int t = 0; t < NT; ++t) k[t] = taps_g[t];
+    }
+    (void)KMAX;
+    auto tap = [&](int t) -> double { if constexpr (NT > 0) return k[t]; else return taps_g[t]; };
+    // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
     const int nseg = (W + SG - 1) / SG;
-    if (tid < hh * nseg) {
-        const int y = tid % hh, sg = tid / hh;
+    for (int it = tid; it < H * nseg; it += kTailThreads) {
+        const int y = it % H, x0 = (it / H) * SG;
+        const float *src = in + y * kTP;
         double acc[SG];
-        conv_seg<NT, SG>(halo + y * HPP + sg * SG, 1, k, acc);
 #pragma unroll
-        for (int j = 0; j < SG; ++j) rowt[y * (P + 1) + sg * SG + j] = (float)acc[j];
+        for (int j = 0; j < SG; ++j) acc[j] = 0.0;
+        if constexpr (NT > 0) {
+            if (x0 - R >= 0 && x0 + SG + R <= W) {
+                conv_seg<NT, SG>(src + x0 - R, 1, k, acc);
+            } else {
+#pragma unroll
+                for (int i = 0; i < SG + NT - 1; ++i) {
+                    const double v = (double)src[reflect_fast(x0 - R + i, W)];
+#pragma unroll
+                    for (int j = 0; j < SG; ++j) {
+                        const int t = i - j;
+                        if (t >= 0 && t < NT) acc[j] = fma(k[t], v, acc[j]);
+                    }
+                }
+            }
+        } else {
+            for (int i = 0; i < SG + n - 1; ++i) {
+                const double v = (double)src[reflect101(x0 - R + i, W)];
+#pragma unroll
+                for (int j = 0; j < SG; ++j) {
+                    const int t = i - j;
+                    if (t >= 0 && t < n) acc[j] = fma(tap(t), v, acc[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SG; ++j)
+            if (x0 + j < W) rowt[y * kTP + x0 + j] = (float)acc[j];
     }
     __syncthreads();
+    // column pass: item = (column x, segment of SG rows); lanes on consecutive columns
     const int nrs = (H + SG - 1) / SG;
-    if (tid < W * nrs) {
-        const int x = tid % W, rs = tid / W;
+    for (int it = tid; it < W * nrs; it += kTailThreads) {
+        const int x = it % W, y0 = (it / W) * SG;
         double acc[SG];
-        conv_seg<NT, SG>(rowt + rs * SG * (P + 1) + x, P + 1, k, acc);
+#pragma unroll
+        for (int j = 0; j < SG; ++j) acc[j] = 0.0;
+        if constexpr (NT > 0) {
+            if (y0 - R >= 0 && y0 + SG + R <= H) {
+                conv_seg<NT, SG>(rowt + (y0 - R) * kTP + x, kTP, k, acc);
+            } else {
+#pragma unroll
+                for (int i = 0; i < SG + NT - 1; ++i) {
+                    const double v = (double)rowt[reflect_fast(y0 - R + i, H) * kTP + x];
+#pragma unroll
+                    for (int j = 0; j < SG; ++j) {
+                        const int t = i - j;
+                        if (t >= 0 && t < NT) acc[j] = fma(k[t], v, acc[j]);
+                    }
+                }
+            }
+        } else {
+            for (int i = 0; i < SG + n - 1; ++i) {
+                const double v = (double)rowt[reflect101(y0 - R + i, H) * kTP + x];
+#pragma unroll
+                for (int j = 0; j < SG; ++j) {
+                    const int t = i - j;
+                    if (t >= 0 && t < n) acc[j] = fma(tap(t), v, acc[j]);
+                }
+            }
+        }
 #pragma unroll
         for (int j = 0; j < SG; ++j) {
-            const int y = rs * SG + j;
+            const int y = y0 + j;
             if (y >= H) break;
             const float o = (float)acc[j];
-            outb[y * P + x] = o;
+            outb[y * kTP + x] = o;
             g[y * W + x] = o;
-            d[y * W + x] = o - in[y * P + x];
+            d[y * W + x] = o - in[y * kTP + x];
         }
     }
 }
 
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(kTailThreads)
 blur_tail(TailArgs ta) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
+    __shared__ float lv[3][kTailDim * kTP];      // current / next level, octave seed
+    __shared__ float rowt[kTailDim * kTP];
     const int f = blockIdx.x, tid = threadIdx.x;
-    constexpr int NT = 1024, P = kTailDim;
-    const int HD = kTailDim + 2 * ta.rmax;        // halo tile side
-    const int HPP = HD | 1;
-    float *halo = smem + 3 * P * P;               // [HD][HPP]
-    float *rowt = halo + HD * HPP;                // [HD][P + 1]
-    double *tp = (double *)(((uintptr_t)(rowt + HD * (P + 1)) + 7) & ~(uintptr_t)7);
     int cur = 0, keep = -1;
     for (int oi = 0; oi < ta.n_oct; ++oi) {
         const int H = ta.H[oi], W = ta.W[oi];
@@ -423,14 +474,14 @@ blur_tail(TailArgs ta) {
             const double ifx = 1.0 / ((double)W / sw), ify = 1.0 / ((double)H / sh);
             int dst = 0;
             while (dst == keep) ++dst;
-            float *o0 = smem + dst * P * P;
+            float *o0 = lv[dst];
             float *g0 = ta.G[oi][0] + (size_t)f * H * W;
-            for (int i = tid; i < H * W; i += NT) {
+            for (int i = tid; i < H * W; i += kTailThreads) {
                 const int y = i / W, x = i - (i / W) * W;
                 const int sy = min(tail_src(y, ify), sh - 1), sx = min(tail_src(x, ifx), sw - 1);
                 const float v = oi == 0 ? ta.prev[(size_t)f * sh * sw + (size_t)sy * sw + sx]
-                                        : smem[keep * P * P + sy * P + sx];
-                o0[y * P + x] = v;
+                                        : lv[keep][sy * kTP + sx];
+                o0[y * kTP + x] = v;
                 g0[i] = v;
             }
             cur = dst;
@@ -438,64 +489,25 @@ blur_tail(TailArgs ta) {
             __syncthreads();
         }
         for (int l = 1; l < ta.n_lvl; ++l) {
-            const int n = ta.ntap[l], r = (n - 1) / 2;
-            const float *in = smem + cur * P * P;
+            const int n = ta.ntap[l];
             int out = 0;
             while (out == cur || out == keep) ++out;
             float *g = ta.G[oi][l] + (size_t)f * H * W;
             float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
             const double *tg = ta.taps + l * PANO_MAX_TAPS;
-            bool done = true;
-            switch (n) {   // the reference's kernel sizes; others take the generic loop below
-                case 11: tail_level<11>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
-                case 13: tail_level<13>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
-                case 17: tail_level<17>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
-                case 21: tail_level<21>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
-                case 27: tail_level<27>(in, smem + out * P * P, halo, rowt, HPP, H, W, tg, g, d, tid); break;
-                default: done = false;
-            }
-            if (done) {
-                __syncthreads();
-                cur = out;
-                if (l == ta.n_lvl - 3) keep = cur;
-                continue;
-            }
-            if (tid < n) tp[tid] = ta.taps[l * PANO_MAX_TAPS + tid];
-            const int hh = H + 2 * r, hw = W + 2 * r;
-            for (int i = tid; i < hh * hw; i += NT) {
-                const int y = i / hw, x = i - (i / hw) * hw;
-                halo[y * HPP + x] = in[reflect101(y - r, H) * P + reflect101(x - r, W)];
-            }
-            __syncthreads();
-            for (int i = tid; i < hh * W; i += NT) {       // row pass
-                const int y = i / W, x = i - (i / W) * W;
-                const float *q = halo + y * HPP + x;
-                double acc = 0.0;
-                for (int t = 0; t < n; ++t) acc = fma(tp[t], (double)q[t], acc);
-                rowt[y * (P + 1) + x] = (float)acc;
-            }
-            __syncthreads();
-            for (int i = tid; i < H * W; i += NT) {        // column pass + DoG
-                const int y = i / W, x = i - (i / W) * W;
-                const float *q = rowt + y * (P + 1) + x;
-                double acc = 0.0;
-                for (int t = 0; t < n; ++t) acc = fma(tp[t], (double)q[t * (P + 1)], acc);
-                const float o = (float)acc;
-                smem[out * P * P + y * P + x] = o;
-                g[i] = o;
-                d[i] = o - in[y * P + x];
+            switch (n) {   // the reference's kernel sizes; others take the runtime-count path
+                case 11: tail_level<11>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
+                case 13: tail_level<13>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
+                case 17: tail_level<17>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
+                case 21: tail_level<21>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
+                case 27: tail_level<27>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
+                default: tail_level<0>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
             }
             __syncthreads();
             cur = out;
             if (l == ta.n_lvl - 3) keep = cur;
         }
     }
-}
-
-size_t tail_smem_bytes(int rmax) {
-    const int HD = kTailDim + 2 * rmax;
-    return (size_t)(3 * kTailDim * kTailDim + HD * (HD | 1) + HD * (kTailDim + 1)) * sizeof(float) +
-           8 + PANO_MAX_TAPS * sizeof(double);
 }
 
 // getGaussianKernel(ksize, sigma, CV_32F) (cv2_compat.getGaussianKernel): f32 taps widened.
@@ -689,11 +701,9 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         // device copy of the level taps (uploaded only when they change)
         double th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
         TailArgs ta{};
-        int rmax = 0;
         for (int l = 1; l < nl; ++l) {
             for (int t = 0; t < tl[l].n; ++t) th[l * PANO_MAX_TAPS + t] = tl[l].k[t];
             ta.ntap[l] = tl[l].n;
-            rmax = std::max(rmax, (tl[l].n - 1) / 2);
         }
         if (!ctx->taps) {
             PANO_HIP(ctx, hipMalloc((void **)&ctx->taps, sizeof(th)));
@@ -705,7 +715,6 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
             ctx->taps_valid = true;
         }
         ta.taps = ctx->taps;
-        ta.rmax = rmax;
         ta.prev = G + ctx->gauss_off[o_tail - 1][nl - 3];
         ta.ph = ctx->oct_h[o_tail - 1];
         ta.pw = ctx->oct_w[o_tail - 1];
@@ -718,9 +727,6 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
             for (int l = 0; l < nl; ++l) ta.G[oi][l] = G + ctx->gauss_off[o][l];
             for (int l = 0; l + 1 < nl; ++l) ta.D[oi][l] = D + ctx->dog_off[o][l];
         }
-        const size_t sm = tail_smem_bytes(rmax);
-        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_tail,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
         if (!ctx->side) {
             PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
             PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
@@ -730,7 +736,7 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         PANO_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
         {
             PanoProf prof_(ctx, PK_BLUR, ctx->side);
-            blur_tail<<<n, 1024, sm, ctx->side>>>(ta);
+            blur_tail<<<n, kTailThreads, 0, ctx->side>>>(ta);
         }
         PANO_LAUNCH_CHECK(ctx, "blur_tail");
         PANO_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
