@@ -52,11 +52,20 @@ def test_cylindrical_bit_exact(gpu, setname, gold_json):
 
 
 # ------------------------------------------------------------------ S1..S4
-def test_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl):
+@pytest.mark.parametrize("api", ["pano_sift_pyramid", "pano_sift"])
+def test_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl, api):
+    """Every level of the full pyramid (pano_sift_pyramid) is bit-exact; after pano_sift the
+    levels it materialises are too, and the ones it skips are refused, not stale."""
+    from vfx_image_stitching_amd import _lib
     dev, cyl, _ = parr_dev
-    st_sift.features(cyl[:1].contiguous())
-    _, _, stg = osift.detect_and_describe(parrington_cyl[0], return_stages=True)
+    one = cyl[:1].contiguous()
     ctx = st_sift.ctx
+    if api == "pano_sift":
+        st_sift.features(one)
+    else:
+        ctx.check(ctx.lib.pano_sift_pyramid(ctx.h, _lib.ptr(one), 1, one.shape[1], one.shape[2],
+                                            ctypes.byref(st_sift.params)))
+    _, _, stg = osift.detect_and_describe(parrington_cyl[0], return_stages=True)
     import torch
     for o in range(len(stg["gauss"])):
         h, w, no = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
@@ -66,8 +75,11 @@ def test_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl):
         for dog, levels in ((0, stg["gauss"][o]), (1, stg["dog"][o])):
             for l, ref in enumerate(levels):
                 out = torch.empty((h.value, w.value), dtype=torch.float32, device=st_sift.device)
-                from vfx_image_stitching_amd import _lib
-                ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, 0, o, l, dog, _lib.ptr(out)))
+                rc = ctx.lib.pano_sift_copy_level(ctx.h, 0, o, l, dog, _lib.ptr(out))
+                if api == "pano_sift" and not dog and ((l == 0 and o > 0) or l == len(levels) - 1):
+                    assert rc == _lib.PANO_E_UNSUPPORTED, (o, l)
+                    continue
+                ctx.check(rc)
                 assert np.array_equal(out.cpu().numpy(), ref), (o, l, dog)
 
 

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Per kernel class HBM bytes per step from FETCH_SIZE / WRITE_SIZE passes (see pmc_traffic.sh).
+The first stitch of the run is a warm-up (allocations) and is skipped."""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+# device kernel name -> libpano profiler class (_lib.KERNELS)
+CLASSES = [
+    (r"^(gray_frames|blur_fast|blur_level|blur_tail)", "blur_level"),
+    (r"^(extrema_scan|localize)", "extrema_localize"),
+    (r"^orientation", "orientation"),
+    (r"^(rank_keys|emit_keypoints)", "sort_dedup"),
+    (r"^descriptor", "descriptor"),
+    (r"^(pack_rows|row_norms)", "row_norms"),
+    (r"^(dist_bf16|dist_mfma)", "dist_mfma"),
+    (r"^reduce_parts", "reduce_parts"),
+    (r"^pair_shifts", "pair_shifts"),
+    (r"^composite", "composite_step"),
+    (r"^(bbox_|gray_bbox)", "gray_bbox"),
+    (r"^cyl_scatter", "cyl_scatter"),
+    (r"^cyl_gather", "cyl_gather"),
+]
+
+
+def cls(name):
+    k = name.replace("(anonymous namespace)::", "").split("(")[0]
+    k = k[5:] if k.startswith("void ") else k
+    for pat, c in CLASSES:
+        if re.match(pat, k):
+            return c
+    return None
+
+
+root, runs = sys.argv[1], int(sys.argv[2])
+out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, tools/pmc_traffic.sh, parrington SIFT step",
+       "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (profiles/r01_fetch_calibration.txt)",
+       "steps": runs - 1, "classes": {}}
+acc = collections.defaultdict(lambda: collections.defaultdict(float))
+launches = collections.defaultdict(int)
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    rows = []
+    for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    # skip the first stitch: everything before the second cyl_scatter dispatch
+    starts = [i for i, r in enumerate(rows) if "cyl_scatter" in r["Kernel_Name"]]
+    for r in rows[starts[1] if len(starts) > 1 else 0:]:
+        k = cls(r["Kernel_Name"])
+        if k is None:
+            continue
+        acc[k][c] += float(r["Counter_Value"]) * 1024
+        if c == "FETCH_SIZE":
+            launches[k] += 1
+for k, v in acc.items():
+    steps = runs - 1
+    out["classes"][k] = {"hbm_bytes_per_step": round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) / steps),
+                         "read_bytes_per_step": round(2 * v["FETCH_SIZE"] / steps),
+                         "write_bytes_per_step": round(v["WRITE_SIZE"] / steps),
+                         "launches_per_step": launches[k] / steps}
+print(json.dumps(out, indent=1, sort_keys=True))

@@ -157,7 +157,7 @@ int pano_sift(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     if (!ctx) return PANO_E_ARG;
     pano_sift_params p;
     if (params) p = *params; else pano_sift_default_params(&p);
-    int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true);
+    int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
     if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, desc, cap, counts);
     sift_join_tail(ctx);                  // no-op unless an error left the tail unjoined
     return rc;
@@ -176,6 +176,9 @@ int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int do
         return PANO_E_ARG;
     const int nl = dog ? ctx->n_lvl - 1 : ctx->n_lvl;
     if (level < 0 || level >= nl) return PANO_E_ARG;
+    if (!dog && !ctx->pyr_full && ((level == 0 && octave > 0) || level == nl - 1))
+        return pano_fail(ctx, PANO_E_UNSUPPORTED,
+                         "pano_sift does not materialise this Gaussian level; use pano_sift_pyramid");
     const size_t plane = (size_t)ctx->oct_h[octave] * ctx->oct_w[octave];
     const float *src = dog ? ctx->dog + ctx->dog_off[octave][level] : ctx->pyr + ctx->gauss_off[octave][level];
     PANO_HIP(ctx, hipMemcpyAsync(out, src + (size_t)frame * plane, plane * sizeof(float),

@@ -101,6 +101,7 @@ struct pano_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool tail_pending = false;           // blur_tail enqueued on `side`, not yet joined
     int o_tail = 0;                      // first octave of the tail
+    bool pyr_full = false;               // every Gaussian level materialised (see launch_sift_pyramid)
     // ---- hipGraph capture (pano_graph_begin / end)
     bool capturing = false;
     size_t cap_prof_start = 0;           // first profiler event of the capture
@@ -163,8 +164,11 @@ int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need);
 int launch_fill(pano_ctx *ctx, void *dst, uint8_t value, size_t bytes);   // graph-safe memset
 int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
                        const double *h_focal, uint8_t *colnz);
+// full = true materialises every Gaussian level (stage access, pano_sift_pyramid); the
+// hot path (pano_sift) skips the planes nothing downstream reads: level 0 of octaves > 0 and
+// the top level (only its DoG is used).
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
-                        const pano_sift_params *p, bool defer_tail = false);
+                        const pano_sift_params *p, bool defer_tail = false, bool full = true);
 int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
                           int cap, int32_t *counts);
 int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int max_points,
@@ -192,6 +196,27 @@ int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint
 int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox);
 
 // ---- device helpers
+// XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"):
+// workgroups are dealt round-robin over the 8 XCDs, so linear id b runs on the XCD labelled
+// b % 8.  Returns a bijective remap giving each XCD label a CONTIGUOUS range of tile ids, so
+// neighbouring tiles (shared halos, overlapping patches) hit the same XCD's L2.  Speed only.
+__device__ __forceinline__ unsigned xcd_swizzle(unsigned b, unsigned n) {
+    const unsigned q = n / 8, r = n % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+// Chunked variant for grids with uneven work per tile (per-frame keypoint counts): runs of
+// CH consecutive tiles stay on one XCD (locality) while the runs rotate over the XCDs
+// (balance).  Bijective: the tail that does not fill 8 * CH tiles maps to itself.
+template <unsigned CH>
+__device__ __forceinline__ unsigned xcd_swizzle_chunked(unsigned b, unsigned n) {
+    const unsigned head = n / (8 * CH) * (8 * CH);
+    if (b >= head) return b;
+    const unsigned i = b / 8;
+    return (i / CH) * (8 * CH) + (b % 8) * CH + i % CH;
+}
+__device__ __forceinline__ unsigned linear_block_id() {
+    return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+}
 __device__ __forceinline__ int reflect101(int i, int n) {
     // BORDER_REFLECT_101, periodic beyond one reflection (cv2_compat.reflect101).
     if (n == 1) return 0;

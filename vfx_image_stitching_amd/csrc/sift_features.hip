@@ -188,8 +188,9 @@ extrema_scan(DogArgs a, int border, double thresh, uint32_t *__restrict__ raw,
     constexpr int ni = NL - 2;
     __shared__ float s[NL][ETY + 2][ELW];
     __shared__ int wtot[4], wbase;
-    const int f = blockIdx.y;
-    int t = blockIdx.x + tile_base, o = 0;
+    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y);
+    const int f = (int)(tb / gridDim.x);
+    int t = (int)(tb % gridDim.x) + tile_base, o = 0;
     while (o + 1 < a.n_oct && t >= a.tile_start[o + 1]) ++o;
     t -= a.tile_start[o];
     const int H = a.H[o], W = a.W[o];
@@ -402,11 +403,12 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     __shared__ double sm[4][PANO_ORI_BINS];
     __shared__ float patch[4][kOriPatch * kOriPatch];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    const int ci = blockIdx.x * 4 + wv;
+    const unsigned tb = xcd_swizzle_chunked<16>(linear_block_id(), gridDim.x * gridDim.y);
+    const int f = (int)(tb / gridDim.x), bx = (int)(tb % gridDim.x);
+    const int ci = bx * 4 + wv;
     int cnt = cand_cnt[f * kCntStride];
     cnt = cnt < cand_cap ? cnt : cand_cap;
-    if ((int)blockIdx.x * 4 >= cnt) return;   // uniform: no wave of this block is active
+    if (bx * 4 >= cnt) return;   // uniform: no wave of this block is active
     const bool active = ci < cnt;
     if (lane < PANO_ORI_BINS) hist[wv][lane] = 0ull;
     __syncthreads();
@@ -733,8 +735,9 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     __shared__ unsigned long long acc[4][128];
     __shared__ int col_lo[4][kDescCols], col_pre[4][kDescCols + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int f = blockIdx.y;
-    const int k = blockIdx.x * 4 + wv;
+    const unsigned tb = xcd_swizzle_chunked<16>(linear_block_id(), gridDim.x * gridDim.y);
+    const int f = (int)(tb / gridDim.x);
+    const int k = (int)(tb % gridDim.x) * 4 + wv;
     int cnt = counts[f];
     cnt = cnt < cap ? cnt : cap;
     if (k >= cnt) return;                                  // whole wave

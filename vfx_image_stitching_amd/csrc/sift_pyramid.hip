@@ -206,7 +206,9 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int n = NT > 0 ? NT : taps.n;
     const int r = (n - 1) / 2;
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY, f = blockIdx.z;
+    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
+    const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TY;
+    const int f = (int)(tb / (gridDim.x * gridDim.y));
     const int tw = min(TX, W - x0), th = min(TY, H - y0);   // valid outputs of this tile
     const int IW = TX + 2 * r, IH = TY + 2 * r;
     const int IWP = IW | 1;                                  // odd row pitch: no bank conflicts
@@ -241,7 +243,7 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
                 if (ty >= th) break;
                 const float o = (float)acc[j];
                 const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + x;
-                out[gi] = o;
+                if (out) out[gi] = o;
                 const float c = tin[(ty + r) * IWP + x + r];
                 if (dog) dog[gi] = o - c;
                 if (in_copy) in_copy[gi] = c;
@@ -257,7 +259,7 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
             const int ty = i / tw, tx = i - ty * tw;
             const float o = (float)conv_one(trow + ty * TXP + tx, TXP, taps.k, n);
             const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + tx;
-            out[gi] = o;
+            if (out) out[gi] = o;
             const float c = tin[(ty + r) * IWP + tx + r];
             if (dog) dog[gi] = o - c;
             if (in_copy) in_copy[gi] = c;
@@ -281,7 +283,9 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     constexpr bool CENTER = MODE != MODE_BASE;
     static_assert((TY + 2 * R) * (TX / SR) <= 512 && TX * (TY / SC) <= 512, "one item per thread");
     extern __shared__ __attribute__((aligned(16))) float tin[];   // [TY + 2R][IWP]
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY, f = blockIdx.z;
+    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
+    const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TY;
+    const int f = (int)(tb / (gridDim.x * gridDim.y));
     const int tw = min(TX, W - x0), th = min(TY, H - y0);
     const int tid = threadIdx.x;
     const int ih = th + 2 * R, iw = tw + 2 * R;
@@ -322,7 +326,7 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         if (ty >= th) break;
         const float o = (float)acc[j];
         const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + cxp;
-        out[gi] = o;
+        if (out) out[gi] = o;
         if constexpr (CENTER) {
             if (dog) dog[gi] = o - cen[j];
             if (in_copy) in_copy[gi] = cen[j];
@@ -353,6 +357,7 @@ struct TailArgs {
     float *D[kTailOct][PANO_MAX_LEVELS];        // DoG planes (frame 0)
     int H[kTailOct], W[kTailOct];
     int n_oct, n_lvl;
+    int full;                                   // write level 0 and the top level too
     const double *taps;                         // [n_lvl][PANO_MAX_TAPS], level 0 unused
     int ntap[PANO_MAX_LEVELS];
 };
@@ -453,7 +458,7 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
             if (y >= H) break;
             const float o = (float)acc[j];
             outb[y * kTP + x] = o;
-            g[y * W + x] = o;
+            if (g) g[y * W + x] = o;
             d[y * W + x] = o - in[y * kTP + x];
         }
     }
@@ -475,14 +480,14 @@ blur_tail(TailArgs ta) {
             int dst = 0;
             while (dst == keep) ++dst;
             float *o0 = lv[dst];
-            float *g0 = ta.G[oi][0] + (size_t)f * H * W;
+            float *g0 = ta.full ? ta.G[oi][0] + (size_t)f * H * W : nullptr;
             for (int i = tid; i < H * W; i += kTailThreads) {
                 const int y = i / W, x = i - (i / W) * W;
                 const int sy = min(tail_src(y, ify), sh - 1), sx = min(tail_src(x, ifx), sw - 1);
                 const float v = oi == 0 ? ta.prev[(size_t)f * sh * sw + (size_t)sy * sw + sx]
                                         : lv[keep][sy * kTP + sx];
                 o0[y * kTP + x] = v;
-                g0[i] = v;
+                if (g0) g0[i] = v;
             }
             cur = dst;
             keep = -1;
@@ -492,7 +497,7 @@ blur_tail(TailArgs ta) {
             const int n = ta.ntap[l];
             int out = 0;
             while (out == cur || out == keep) ++out;
-            float *g = ta.G[oi][l] + (size_t)f * H * W;
+            float *g = (ta.full || l < ta.n_lvl - 1) ? ta.G[oi][l] + (size_t)f * H * W : nullptr;
             float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
             const double *tg = ta.taps + l * PANO_MAX_TAPS;
             switch (n) {   // the reference's kernel sizes; others take the runtime-count path
@@ -651,7 +656,7 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
 }
 
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
-                        const pano_sift_params *p, bool defer_tail) {
+                        const pano_sift_params *p, bool defer_tail, bool full) {
     sift_join_tail(ctx);                  // a previous call's tail must finish first
     int no, nl;
     double sb, sl[PANO_MAX_LEVELS];
@@ -720,6 +725,7 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         ta.pw = ctx->oct_w[o_tail - 1];
         ta.n_oct = no - o_tail;
         ta.n_lvl = nl;
+        ta.full = full ? 1 : 0;
         for (int oi = 0; oi < ta.n_oct; ++oi) {
             const int o = o_tail + oi;
             ta.H[oi] = ctx->oct_h[o];
@@ -758,11 +764,12 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                 la.sw = ctx->oct_w[o - 1];
                 la.ifx = 1.0 / ((double)W / la.sw);
                 la.ify = 1.0 / ((double)H / la.sh);
-                rc = launch_blur<MODE_DOWN>(ctx, la, out, dg, G + ctx->gauss_off[o][0], n, H, W,
-                                            tl[l]);
+                rc = launch_blur<MODE_DOWN>(ctx, la, (full || l < nl - 1) ? out : nullptr, dg,
+                                            full ? G + ctx->gauss_off[o][0] : nullptr, n, H, W, tl[l]);
             } else {
                 la.src = G + ctx->gauss_off[o][l - 1];
-                rc = launch_blur<MODE_LEVEL>(ctx, la, out, dg, nullptr, n, H, W, tl[l]);
+                rc = launch_blur<MODE_LEVEL>(ctx, la, (full || l < nl - 1) ? out : nullptr, dg, nullptr,
+                                             n, H, W, tl[l]);
             }
             if (rc) return rc;
             if (o == o_tail - 1 && l == nl - 3 && o_tail < no) {
@@ -772,5 +779,6 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         }
     }
     if (o_tail < no && !defer_tail) sift_join_tail(ctx);
+    ctx->pyr_full = full;
     return PANO_OK;
 }
