@@ -34,6 +34,52 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec (the blur's arithmetic)
 
 
+def pmc_traffic(kernel, workload, method):
+    """HBM bytes per launch of a kernel class from the newest committed PMC traffic profile
+    (tools/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over the same
+    parrington SIFT step, corrected per profiles/r01_fetch_calibration.txt)."""
+    import glob
+    if workload != "parrington" or method != "sift":
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_parrington.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    c = d.get("classes", {}).get(kernel)
+    if not c or not c.get("launches_per_step"):
+        return None, None
+    return c["hbm_bytes_per_step"] / c["launches_per_step"], os.path.relpath(files[-1], ROOT)
+
+
+def blur_fp64_flops(st, n_frames):
+    """Algorithmic fp64 FMA flops of the blur class per step: every Gaussian level output is
+    two separable passes of NT taps (no tile-halo recompute), 2 flop per tap."""
+    import ctypes
+    import math
+    ctx = st.ctx
+    p = st.params
+    sig = p.sigma
+    base = math.sqrt(max(sig * sig - (2 * p.assumed_blur) ** 2, 0.01))
+    k = 2 ** (1.0 / p.num_intervals)
+    sig_l = [sig] + [math.sqrt((k * k ** (i - 1) * sig) ** 2 - (k ** (i - 1) * sig) ** 2)
+                     for i in range(1, p.num_intervals + 3)]
+    buf = (ctypes.c_double * 64)()
+    nt = ctypes.c_int()
+
+    def taps(s):
+        ctx.lib.pano_sift_taps(ctypes.c_double(s), buf, ctypes.byref(nt))
+        return nt.value
+    no = ctypes.c_int32()
+    hh, ww = ctypes.c_int32(), ctypes.c_int32()
+    ctx.lib.pano_sift_level_shape(ctx.h, 0, ctypes.byref(hh), ctypes.byref(ww), ctypes.byref(no))
+    fl = 2 * 2 * taps(base) * hh.value * ww.value
+    for o in range(no.value):
+        ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(hh), ctypes.byref(ww), None)
+        for l in range(1, p.num_intervals + 3):
+            fl += 2 * 2 * taps(sig_l[l]) * hh.value * ww.value
+    return fl * n_frames
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,13 +248,25 @@ def main():
         if byts is not None:
             per_launch_bytes = byts / launches_per_step
             ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
+            traffic, tsrc = pmc_traffic(rk, args.workload, args.method)
             roof = {"bound": "hbm", "kernel": rk, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                     "timing": ("HIP events on the library stream, %d eager steps right after the "
                                "graph-replayed timed region" % args.steps) if args.graph
                     else "HIP events on the library stream over the timed region",
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+                    "traffic": round(traffic) if traffic else None,
+                    "traffic_unit": "HBM bytes per launch",
+                    "traffic_source": tsrc,
+                    "algorithmic_bytes_per_launch": round(per_launch_bytes),
                     "avg_launch_ms": round(per_launch_ms, 5), "launches_per_step": launches_per_step,
                     "kernel_ms_per_step": round(per_step_ms, 4)}
+            if rk == "blur_level" and args.method == "sift":
+                fl = blur_fp64_flops(st, n_local)
+                tf = fl / (per_step_ms * 1e-3) / 1e12
+                roof["fp64_fma"] = {"note": "the blur is bit-exact fp64 FMA work (DESIGN.md 3): "
+                                            "its compute roofline", "achieved": round(tf, 2),
+                                    "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                    "frac": round(tf / FP64_PEAK_TFLOPS, 4)}
         else:
             roof = {"bound": "latency", "kernel": rk, "achieved": None, "peak": None, "unit": None,
                     "frac": None, "traffic": None, "avg_launch_ms": round(per_launch_ms, 5),
