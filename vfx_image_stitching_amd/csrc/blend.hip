@@ -176,8 +176,18 @@ composite_tables(const uint8_t *__restrict__ colnz, int w, SeqArg sa, uint8_t *_
     }
 }
 
-__global__ void composite_owner(const uint8_t *__restrict__ mode, int n, int w, int W, SeqArg sa,
-                                int32_t *__restrict__ owner) {
+// Per canvas column: the owning step and everything composite_pixels needs about it
+// (source columns, row offsets, mode, blend weights) -- one coalesced 32-byte record.
+struct ColInfo {
+    int32_t i;          // owning frame (-1: no frame covers the column)
+    int32_t c, fy;      // frame column, frame top row on the canvas
+    int32_t cm, fym;    // previous frame's column (-1: outside it) and top row
+    float w0, w1;       // f32(1 - alpha), f32(alpha)
+    uint8_t mode, is_a, pad0, pad1;
+};
+
+__global__ void composite_owner(const uint8_t *__restrict__ mode, const float2 *__restrict__ wgt,
+                                int n, int w, int W, SeqArg sa, ColInfo *__restrict__ info) {
     const int X = blockIdx.x * blockDim.x + threadIdx.x;
     if (X >= W) return;
     int o = -1;
@@ -185,55 +195,73 @@ __global__ void composite_owner(const uint8_t *__restrict__ mode, int n, int w, 
         const int c = X - sa.fx[i];
         if (c >= 0 && c < w && mode[(size_t)i * w + c]) { o = i; break; }
     }
-    owner[X] = o;
+    ColInfo ci{};
+    ci.i = o;
+    if (o >= 0) {
+        ci.c = X - sa.fx[o];
+        ci.fy = sa.fy[o];
+        ci.mode = mode[(size_t)o * w + ci.c];
+        ci.is_a = sa.is_a[o];
+        const float2 ab = wgt[(size_t)o * w + ci.c];
+        ci.w0 = ab.x;
+        ci.w1 = ab.y;
+        ci.cm = -1;
+        if (o > 0) {
+            const int cm = X - sa.fx[o - 1];
+            ci.cm = (cm >= 0 && cm < w) ? cm : -1;
+            ci.fym = sa.fy[o - 1];
+        }
+    }
+    info[X] = ci;
 }
 
-__device__ __forceinline__ void composite_px(const uint8_t *__restrict__ frames, int h, int w,
-                                             const uint8_t *__restrict__ mode,
-                                             const float2 *__restrict__ wgt, int i, const SeqArg &sa,
-                                             int X, int y, uint8_t o[3]) {
-    o[0] = o[1] = o[2] = 0;
-    if (i < 0) return;
-    const int c = X - sa.fx[i];
-    const int fyl = y - sa.fy[i];
-    uint8_t F[3] = {0, 0, 0};
-    if (fyl >= 0 && fyl < h) {
-        const uint8_t *p = frames + (((size_t)i * h + fyl) * w + c) * 3;
-        F[0] = p[0]; F[1] = p[1]; F[2] = p[2];
-    }
-    if (mode[(size_t)i * w + c] != 2) {
-        o[0] = F[0]; o[1] = F[1]; o[2] = F[2];
-        return;
-    }
-    uint8_t M[3] = {0, 0, 0};
-    const int cm = X - sa.fx[i - 1], ym = y - sa.fy[i - 1];
-    if (cm >= 0 && cm < w && ym >= 0 && ym < h) {
-        const uint8_t *q = frames + (((size_t)(i - 1) * h + ym) * w + cm) * 3;
-        M[0] = q[0]; M[1] = q[1]; M[2] = q[2];
-    }
-    const float2 ab = wgt[(size_t)i * w + c];
-    for (int k = 0; k < 3; ++k)
-        o[k] = sa.is_a[i] ? blend_px(ab.x, ab.y, F[k], M[k]) : blend_px(ab.x, ab.y, M[k], F[k]);
-}
-
-// grid-stride over the canvas with a bounded grid: one bbox atomic per workgroup
+// Workgroup = 64 canvas columns x 32 rows: lane = column (its ColInfo record read once),
+// each thread walks 8 rows; byte loads / stores are contiguous across the wave.  One bbox
+// atomic per workgroup.
+constexpr int kCompRows = 8;
 __global__ void __launch_bounds__(256)
-composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const uint8_t *__restrict__ mode,
-                 const float2 *__restrict__ wgt, const int32_t *__restrict__ owner, SeqArg sa,
+composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const ColInfo *__restrict__ info,
                  uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox) {
     __shared__ int r[4][256];
     const int tid = threadIdx.x;
     int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
-    const size_t total = (size_t)H * W;
-    for (size_t e = (size_t)blockIdx.x * 256 + tid; e < total; e += (size_t)gridDim.x * 256) {
-        const int y = (int)(e / W), X = (int)(e - (size_t)y * W);
-        uint8_t o[3];
-        composite_px(frames, h, w, mode, wgt, owner[X], sa, X, y, o);
-        uint8_t *d = canvas + e * 3;
-        d[0] = o[0]; d[1] = o[1]; d[2] = o[2];
-        if (bbox && gray_u8(o) > thr) {
-            ymin = min(ymin, y); ymax = max(ymax, y);
-            xmin = min(xmin, X); xmax = max(xmax, X);
+    const int X = blockIdx.x * 64 + (tid & 63);
+    const int y0 = (blockIdx.y * 4 + (tid >> 6)) * kCompRows;
+    if (X < W) {
+        const ColInfo ci = info[X];
+        // all rows' source bytes first (loads in flight together), then blend and store
+        uint8_t F[kCompRows][3], M[kCompRows][3];
+        const uint8_t *fp = frames + (((size_t)max(ci.i, 0) * h) * w + ci.c) * 3;
+        const uint8_t *mp = frames + (((size_t)max(ci.i - 1, 0) * h) * w + max(ci.cm, 0)) * 3;
+        const bool blend = ci.i >= 0 && ci.mode == 2;
+#pragma unroll
+        for (int k = 0; k < kCompRows; ++k) {
+            const int y = y0 + k;
+            const int fyl = y - ci.fy, ym = y - ci.fym;
+            const bool fin = ci.i >= 0 && y < H && fyl >= 0 && fyl < h;
+            const bool min_ = blend && y < H && ci.cm >= 0 && ym >= 0 && ym < h;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                F[k][c] = fin ? fp[(size_t)fyl * w * 3 + c] : 0;
+                M[k][c] = min_ ? mp[(size_t)ym * w * 3 + c] : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kCompRows; ++k) {
+            const int y = y0 + k;
+            if (y >= H) break;
+            uint8_t o[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                o[c] = !blend ? F[k][c]
+                              : (ci.is_a ? blend_px(ci.w0, ci.w1, F[k][c], M[k][c])
+                                         : blend_px(ci.w0, ci.w1, M[k][c], F[k][c]));
+            uint8_t *d = canvas + ((size_t)y * W + X) * 3;
+            d[0] = o[0]; d[1] = o[1]; d[2] = o[2];
+            if (bbox && gray_u8(o) > thr) {
+                ymin = min(ymin, y); ymax = max(ymax, y);
+                xmin = min(xmin, X); xmax = max(xmax, X);
+            }
         }
     }
     if (!bbox) return;
@@ -550,11 +578,11 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
     const size_t o_mode = 0;
     const size_t o_w = ((size_t)n * w + 255) & ~size_t(255);
     const size_t o_own = o_w + (((size_t)n * w * sizeof(float2) + 255) & ~size_t(255));
-    rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, o_own + (size_t)W * sizeof(int32_t));
+    rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, o_own + (size_t)W * sizeof(ColInfo));
     if (rc) return rc;
     uint8_t *mode = ctx->flags + o_mode;
     float2 *wgt = (float2 *)(ctx->flags + o_w);
-    int32_t *owner = (int32_t *)(ctx->flags + o_own);
+    ColInfo *info = (ColInfo *)(ctx->flags + o_own);
     if (bbox) {
         PanoProf prof_(ctx, PK_BBOX);
         bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
@@ -566,15 +594,13 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
     PANO_LAUNCH_CHECK(ctx, "composite_tables");
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_owner<<<(W + 255) / 256, 256, 0, ctx->stream>>>(mode, n, w, W, sa, owner);
+        composite_owner<<<(W + 255) / 256, 256, 0, ctx->stream>>>(mode, wgt, n, w, W, sa, info);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_owner");
-    unsigned nb = (unsigned)(((size_t)H * W + 255) / 256);
-    nb = nb < 1024 ? nb : 1024;
     {
+        dim3 grid((W + 63) / 64, (H + 4 * kCompRows - 1) / (4 * kCompRows));
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_pixels<<<nb, 256, 0, ctx->stream>>>(frames, h, w, mode, wgt, owner, sa, canvas,
-                                                        H, W, thr, bbox);
+        composite_pixels<<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, H, W, thr, bbox);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_pixels");
     if (bbox) {

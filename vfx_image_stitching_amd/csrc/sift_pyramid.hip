@@ -468,6 +468,9 @@ __global__ void __launch_bounds__(kTailThreads)
 blur_tail(TailArgs ta) {
     __shared__ float lv[3][kTailDim * kTP];      // current / next level, octave seed
     __shared__ float rowt[kTailDim * kTP];
+    // the tail is a latency chain of 18 workgroups running beside the extrema scan, which
+    // fills every CU: raise its waves' issue priority so the chain is not starved
+    __builtin_amdgcn_s_setprio(3);
     const int f = blockIdx.x, tid = threadIdx.x;
     int cur = 0, keep = -1;
     for (int oi = 0; oi < ta.n_oct; ++oi) {
@@ -734,7 +737,9 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
             for (int l = 0; l + 1 < nl; ++l) ta.D[oi][l] = D + ctx->dog_off[o][l];
         }
         if (!ctx->side) {
-            PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+            int lo_prio = 0, hi_prio = 0;   // numerically lower = higher priority
+            PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+            PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi_prio));
             PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
             PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
         }
