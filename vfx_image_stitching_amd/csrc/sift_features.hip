@@ -734,6 +734,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int32_t *__restrict__ counts, int cap, float *__restrict__ desc) {
     __shared__ unsigned long long acc[4][128];
     __shared__ int col_lo[4][kDescCols], col_pre[4][kDescCols + 1];
+    __shared__ double gwt[4][kDescCols / 2 + 1];          // separable Gaussian weight by |offset|
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const unsigned tb = xcd_swizzle_chunked<16>(linear_block_id(), gridDim.x * gridDim.y);
     const int f = (int)(tb / gridDim.x);
@@ -767,21 +768,34 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     const float bins_per_deg = (float)(8.0 / 360.0);
     const double inv_hwd = 1.0 / hwd;
     const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hwd < 2.5 with slack
-    auto sample = [&](int xi, int yi) {
+    // The reference's weight exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) has (rrot, crot) a rotation
+    // of (xs, ys), so it equals exp(-xs^2/(8hw^2)) * exp(-ys^2/(8hw^2)): one table of side/2+1
+    // entries per keypoint replaces an f64 exp per sample.  The two forms differ by a few f64
+    // ulps (~1e-15 relative), below the 2^-40 quantum of the fixed-point histogram and far
+    // below the f32 rounding of the reference's own np.add.at accumulation.
+    const bool use_tab = side <= kDescCols;
+    // gradient taps of the in-image sample (xi, yi): gx = q[1] - q[-1], gy = q[-cols] - q[cols]
+    auto taps = [&](int xi, int yi, float (&g)[4]) {
+        const float *q = img + (size_t)(py + yi - half) * cols + (px + xi - half);
+        g[0] = q[1];
+        g[1] = q[-1];
+        g[2] = q[-cols];
+        g[3] = q[cols];
+    };
+    auto sample = [&](int xi, int yi, const float (&g)[4]) {
         const int xs = xi - half, ys = yi - half;
-        const int rr = py + ys, cc = px + xs;
         const double rrot = (double)xs * sin_a + (double)ys * cos_a;
         const double crot = (double)xs * cos_a - (double)ys * sin_a;
         const double rq = div_rn(rrot, hwd, inv_hwd), cq = div_rn(crot, hwd, inv_hwd);
         const double rbin = (rq + 2.0) - 0.5;
         const double cbin = (cq + 2.0) - 0.5;
         if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) return;
-        const float *q = img + (size_t)rr * cols + cc;
-        const float gx = q[1] - q[-1];
-        const float gy = q[-cols] - q[cols];
+        const float gx = g[0] - g[1];
+        const float gy = g[2] - g[3];
         const float mag = sqrtf(gx * gx + gy * gy);
         const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
-        const double w = exp(-0.125 * (rq * rq + cq * cq));
+        const double w = use_tab ? gwt[wv][abs(xs)] * gwt[wv][abs(ys)]
+                                 : exp(-0.125 * (rq * rq + cq * cq));
         const double wm = (w * (double)mag) * kDescScale;   // 2^40 fixed point, exact scaling
         const float ob = np_remainder_pos_f((ori - angle_f) * bins_per_deg, 8.0f);
         const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
@@ -802,7 +816,11 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1));
         }
     };
-    if (side <= kDescCols) {
+    if (use_tab) {
+        for (int a = lane; a <= half; a += 64) {
+            const double q = (double)a / hwd;
+            gwt[wv][a] = exp(-0.125 * (q * q));
+        }
         int *clo = col_lo[wv], *cpre = col_pre[wv];
         int run = 0;                                       // wave-wide running total
 #pragma unroll
@@ -866,14 +884,32 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             }
             int r = t - cpre[c];
             int ncol = cpre[c + 1] - cpre[c];
-            for (; t < tend; ++t, ++r) {
+            // software pipeline: the next sample's four gradient taps are in flight while
+            // the current one is binned
+            while (r >= ncol) {
+                r -= ncol;
+                ++c;
+                ncol = cpre[c + 1] - cpre[c];
+            }
+            int xi = c, yi = clo[c] + r + half;
+            float g[4];
+            taps(xi, yi, g);
+            for (++t, ++r; t < tend; ++t, ++r) {
                 while (r >= ncol) {
                     r -= ncol;
                     ++c;
                     ncol = cpre[c + 1] - cpre[c];
                 }
-                sample(c, clo[c] + r + half);
+                const int xn = c, yn = clo[c] + r + half;
+                float gn[4];
+                taps(xn, yn, gn);
+                sample(xi, yi, g);
+                xi = xn;
+                yi = yn;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) g[i] = gn[i];
             }
+            sample(xi, yi, g);
         }
     } else {
         // very large patches: every sample of the (side x side) square, cheap range test first
@@ -885,7 +921,11 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
             const double rrot = (double)xs * sin_a + (double)ys * cos_a;
             const double crot = (double)xs * cos_a - (double)ys * sin_a;
-            if (fabs(rrot) < lim && fabs(crot) < lim) sample(xi, yi);
+            if (fabs(rrot) < lim && fabs(crot) < lim) {
+                float g[4];
+                taps(xi, yi, g);
+                sample(xi, yi, g);
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
