@@ -1,8 +1,10 @@
 #!/bin/bash
 # Kernel-trace profile of N parrington stitches (tools/prof_features.py) -> per-kernel summary.
+# KT=<dir> names the output directory (default gpurun_out/kt).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 N=${N:-5}
-rm -rf gpurun_out/kt && mkdir -p gpurun_out/kt
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/kt -o run -- python3 tools/prof_features.py $N > gpurun_out/kt/log.txt 2>&1 || exit $?
-python tools/ktrace_summary.py gpurun_out/kt $N > gpurun_out/kt/summary.txt && cat gpurun_out/kt/summary.txt
+KT=${KT:-gpurun_out/kt}
+rm -rf $KT && mkdir -p $KT
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $KT -o run -- python3 tools/prof_features.py $N > $KT/log.txt 2>&1 || exit $?
+python tools/ktrace_summary.py $KT $N > $KT/summary.txt && cat $KT/summary.txt

@@ -15,6 +15,10 @@ names, frames, focals, margin = data.load_set("parrington")
 st = Stitcher("sift", match=os.environ.get("PANO_MATCH", "bf16"))
 d = st.upload(frames)
 for _ in range(n):
-    st.run(d, focals, margin=margin)
+    try:
+        st.run(d, focals, margin=margin)
+    except Exception as e:          # ablation builds (PANO_BLUR_DBG) produce garbage features
+        print("run failed:", e)
+        torch.cuda.synchronize()
 torch.cuda.synchronize()
 print("done")
