@@ -196,6 +196,23 @@ int pano_composite_sequential(pano_ctx *ctx, const uint8_t *d_frames, const uint
                               int n, int h, int w, const pano_step *h_steps,
                               const int32_t *h_first_xy, uint8_t *d_canvas, int H, int W);
 
+/* Device-planned mosaic loop (the batched Stitcher's single-launch-chain form of
+ * run_panorama :336-381): pano_plan_device reads the n-1 pair records on the device, applies
+ * run_panorama's record -> shift conversion (int() for Harris: int_shifts = 1), the drift
+ * correction and pano_plan_composite's geometry, and writes a plan of pano_plan_device_bytes()
+ * bytes to d_plan; pano_composite_planned then composites into d_canvas, a buffer of
+ * Hcap x Wcap x 3 bytes laid out as [H][W][3] with the planned H, W.  The plan starts with
+ * int32 {status, H, W, n, first_x, first_y}: status PANO_OK, PANO_E_NOMATCH (a pair had
+ * no match: the reference fails there), or PANO_E_OVERFLOW (canvas above the capacity or a
+ * column covered by three frames: use pano_plan_composite + pano_composite_bbox instead).
+ * Nothing is read back by either call (graph-capturable).  2 <= n <= 256. */
+size_t pano_plan_device_bytes(void);
+int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *d_recs, int n, int h, int w,
+                     int int_shifts, int Hcap, int Wcap, void *d_plan);
+int pano_composite_planned(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t *d_colnz, int n,
+                           int h, int w, const void *d_plan, uint8_t *d_canvas, int Hcap,
+                           int Wcap, int black_threshold, int32_t *d_bbox);
+
 /* blend_two_images(shift_vec, ref_match, imgA, imgB) for arbitrary inputs
  * image_stitching_sift.py:156-202.  Geometry comes from pano_blend_geometry. */
 int pano_blend_geometry(double dx, double dy, const double *h_ref4, int hA, int wA, int hB,

@@ -462,3 +462,32 @@ def test_graph_replay_matches_eager(gpu, method, setname, gold_json):
         assert np.array_equal(res.panorama.cpu().numpy(), e_pano)
     assert digest(e_pano) == gold_json(f"{method}_{setname}.json")["pano_digest"]
     st.release_graphs()
+
+
+# ------------------------------------------------------------------ device-planned stitch
+@pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("harris", "grail"),
+                                            ("harris", "out")])
+def test_device_plan_matches_host_plan(gpu, method, setname, gold_json):
+    """pano_plan_device + pano_composite_planned (one launch chain, one host read) give the
+    host-planned stitch's records, canvas and crop byte for byte; a capacity overflow falls
+    back to the host plan with the same result."""
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = data.load_set(setname)
+    st = Stitcher(method)
+    dev = st.upload(frames)
+    host = st.run(dev, focals, margin=margin, device_plan=False)
+    h_canvas = host.canvas.cpu().numpy()
+    h_pano = host.panorama.cpu().numpy()
+    for graph in (False, True, True):
+        res = st.run(dev, focals, margin=margin, graph=graph)
+        assert np.array_equal(res.records.view(np.uint8), host.records.view(np.uint8))
+        assert res.shifts == host.shifts and res.pairs == host.pairs
+        assert res.bbox == host.bbox
+        assert np.array_equal(res.canvas.cpu().numpy(), h_canvas)
+        assert np.array_equal(res.panorama.cpu().numpy(), h_pano)
+    st.canvas_cap = (8, 8)                              # forces PANO_E_OVERFLOW -> host plan
+    res = st.run(dev, focals, margin=margin)
+    assert np.array_equal(res.panorama.cpu().numpy(), h_pano)
+    assert digest(h_pano) == gold_json(f"{method}_{setname}.json")["pano_digest"]
+    st.release_graphs()

@@ -103,6 +103,9 @@ SIGNATURES = {
     "pano_composite": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I]),
     "pano_composite_bbox": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I,
                                  _I, _P]),
+    "pano_plan_device_bytes": (ctypes.c_size_t, []),
+    "pano_plan_device": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "pano_composite_planned": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
     "pano_composite_sequential": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P,
                                        _I, _I]),
     "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),

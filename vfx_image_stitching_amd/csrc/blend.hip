@@ -139,9 +139,22 @@ struct SeqArg {
     double overlap[kMaxSeq];
 };
 
+// Device-planned stitch (pano_plan_device): the plan kernel writes the sequence table and
+// the canvas size to HBM, so the composite launches read them there and the whole stitch is
+// one launch chain (one hipGraph, one device->host read at the end).
+struct DevPlan {
+    int32_t status, H, W, n;            // status: PANO_OK, PANO_E_NOMATCH, or PANO_E_OVERFLOW
+    int32_t first_x, first_y, pad0, pad1;   //   (-> the host plan path)
+    SeqArg sa;
+    pano_step steps[kMaxSeq];
+};
+
+template <bool DEV>
 __global__ void __launch_bounds__(256)
-composite_tables(const uint8_t *__restrict__ colnz, int w, SeqArg sa, uint8_t *__restrict__ mode,
-                 float2 *__restrict__ wgt) {
+composite_tables(const uint8_t *__restrict__ colnz, int w, SeqArg sa_arg, const DevPlan *__restrict__ dp,
+                 uint8_t *__restrict__ mode, float2 *__restrict__ wgt) {
+    if (DEV && (dp->status != PANO_OK || (int)blockIdx.x >= dp->n)) return;
+    const SeqArg &sa = DEV ? dp->sa : sa_arg;
     __shared__ int sh[256];
     const int i = blockIdx.x, tid = threadIdx.x;
     int carry = 0;
@@ -186,8 +199,16 @@ struct ColInfo {
     uint8_t mode, is_a, pad0, pad1;
 };
 
+template <bool DEV>
 __global__ void composite_owner(const uint8_t *__restrict__ mode, const float2 *__restrict__ wgt,
-                                int n, int w, int W, SeqArg sa, ColInfo *__restrict__ info) {
+                                int n, int w, int W, SeqArg sa_arg, const DevPlan *__restrict__ dp,
+                                ColInfo *__restrict__ info) {
+    if (DEV) {
+        if (dp->status != PANO_OK) return;
+        n = dp->n;
+        W = dp->W;
+    }
+    const SeqArg &sa = DEV ? dp->sa : sa_arg;
     const int X = blockIdx.x * blockDim.x + threadIdx.x;
     if (X >= W) return;
     int o = -1;
@@ -219,9 +240,17 @@ __global__ void composite_owner(const uint8_t *__restrict__ mode, const float2 *
 // each thread walks 8 rows; byte loads / stores are contiguous across the wave.  One bbox
 // atomic per workgroup.
 constexpr int kCompRows = 8;
+template <bool DEV>
 __global__ void __launch_bounds__(256)
 composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const ColInfo *__restrict__ info,
-                 uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox) {
+                 uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox,
+                 const DevPlan *__restrict__ dp) {
+    if (DEV) {   // grid sized for the capacity; the planned canvas is [H][W] inside it
+        if (dp->status != PANO_OK) return;
+        H = dp->H;
+        W = dp->W;
+        if ((int)blockIdx.x * 64 >= W || (int)blockIdx.y * 4 * kCompRows >= H) return;
+    }
     __shared__ int r[4][256];
     const int tid = threadIdx.x;
     int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
@@ -401,9 +430,10 @@ __global__ void bbox_fix(int32_t *bbox) {
 
 }  // namespace
 
-// ---------------------------------------------------------------- host geometry (exact
-// replay of the Python scalar arithmetic of blend_two_images / pad_image / run_panorama)
-static void pad_place(long long mx, long long my, int h, int w, int *top, int *left, int *ph,
+// ---------------------------------------------------------------- geometry (exact replay of
+// the Python scalar arithmetic of blend_two_images / pad_image / run_panorama); shared by the
+// host plan (pano_plan_composite) and the device plan kernel (pano_plan_device)
+static __host__ __device__ void pad_place(long long mx, long long my, int h, int w, int *top, int *left, int *ph,
                       int *pw) {
     *left = mx >= 0 ? (int)mx : 0;
     *top = my >= 0 ? (int)my : 0;
@@ -411,9 +441,8 @@ static void pad_place(long long mx, long long my, int h, int w, int *top, int *l
     *ph = h + (int)(my >= 0 ? my : -my);
 }
 
-extern "C" int pano_blend_geometry(double dx, double dy, const double *ref4, int hA, int wA,
-                                   int hB, int wB, int32_t *geom, double *overlap) {
-    if (!ref4 || !geom || !overlap) return PANO_E_ARG;
+static __host__ __device__ int blend_geometry(double dx, double dy, const double *ref4, int hA, int wA,
+                                              int hB, int wB, int32_t *geom, double *overlap) {
     double r00 = ref4[0], r01 = ref4[1], r10 = ref4[2], r11 = ref4[3];
     const int swapped = dx < 0;
     if (swapped) {
@@ -442,12 +471,19 @@ extern "C" int pano_blend_geometry(double dx, double dy, const double *ref4, int
     return PANO_OK;
 }
 
-extern "C" int pano_plan_composite(const double *shifts, const double *pairs, int n, int h, int w,
-                                   pano_step *steps, int32_t *first_xy, int32_t *canvas_hw) {
-    if (n < 1 || h <= 0 || w <= 0 || !first_xy || !canvas_hw || (n > 1 && (!shifts || !pairs || !steps)))
-        return PANO_E_ARG;
+extern "C" int pano_blend_geometry(double dx, double dy, const double *ref4, int hA, int wA,
+                                   int hB, int wB, int32_t *geom, double *overlap) {
+    if (!ref4 || !geom || !overlap) return PANO_E_ARG;
+    return blend_geometry(dx, dy, ref4, hA, wA, hB, wB, geom, overlap);
+}
+
+// shifts / pairs: element i - 1 of step i, read through the accessors (host arrays, or the
+// device records with drift correction applied on the fly); tmp: 5 x n ints of scratch
+template <typename SH, typename PR>
+static __host__ __device__ int plan_core(SH shift, PR pair, int n, int h, int w, pano_step *steps,
+                                         int32_t *first_xy, int32_t *canvas_hw, int32_t *tmp) {
     int Hm = h, Wm = w;
-    std::vector<int> yM(n), xM(n), yF(n), xF(n), padtop(n);
+    int32_t *yM = tmp, *xM = tmp + n, *yF = tmp + 2 * n, *xF = tmp + 3 * n, *padtop = tmp + 4 * n;
     for (int i = 1; i < n; ++i) {
         // run_panorama pads the new frame to the mosaic height first (:374-376)
         const int diff = Hm - h;
@@ -457,8 +493,10 @@ extern "C" int pano_plan_composite(const double *shifts, const double *pairs, in
         int32_t g[8];
         double ov;
         // blend_two_images(shift, pair, imgA = mosaic, imgB = frame)
-        int rc = pano_blend_geometry(shifts[2 * (i - 1)], shifts[2 * (i - 1) + 1], pairs + 4 * (i - 1),
-                                     Hm, Wm, fh, w, g, &ov);
+        double sd[2], pd[4];
+        shift(i - 1, sd);
+        pair(i - 1, pd);
+        int rc = blend_geometry(sd[0], sd[1], pd, Hm, Wm, fh, w, g, &ov);
         if (rc) return rc;
         const int swapped = g[6];
         // post-swap A is the frame when swapped
@@ -490,6 +528,165 @@ extern "C" int pano_plan_composite(const double *shifts, const double *pairs, in
     first_xy[1] = oy;
     canvas_hw[0] = Hm;
     canvas_hw[1] = Wm;
+    return PANO_OK;
+}
+
+extern "C" int pano_plan_composite(const double *shifts, const double *pairs, int n, int h, int w,
+                                   pano_step *steps, int32_t *first_xy, int32_t *canvas_hw) {
+    if (n < 1 || h <= 0 || w <= 0 || !first_xy || !canvas_hw || (n > 1 && (!shifts || !pairs || !steps)))
+        return PANO_E_ARG;
+    std::vector<int32_t> tmp(5 * (size_t)n);
+    return plan_core([&](int k, double *d) { d[0] = shifts[2 * k]; d[1] = shifts[2 * k + 1]; },
+                     [&](int k, double *d) { for (int q = 0; q < 4; ++q) d[q] = pairs[4 * k + q]; },
+                     n, h, w, steps, first_xy, canvas_hw, tmp.data());
+}
+
+namespace {
+
+
+// run_panorama's record -> shift conversion (floats for SIFT, int() for Harris), drift
+// correction (:336-365) and the whole composite plan, in the host code's exact double
+// arithmetic.  The plan is a sequential scalar chain: the records are staged in LDS and ONE
+// thread runs it over LDS state (a global-memory chain would pay an HBM round trip per
+// dependent access); the parallel-composite check and the write-out use every thread.
+__global__ void __launch_bounds__(256)
+plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int_shifts, int Hcap,
+            int Wcap, DevPlan *__restrict__ dp) {
+    __shared__ double rv[6][kMaxSeq];           // dx dy xA yA xB yB per pair (converted)
+    __shared__ pano_step st[kMaxSeq];
+    __shared__ int32_t tmp[5 * kMaxSeq];
+    __shared__ int32_t fx[kMaxSeq];
+    __shared__ int32_t hdr[6];                  // status H W first_x first_y, bands flag
+    __shared__ int bad;
+    const int tid = threadIdx.x, P = n - 1;
+    auto conv = [&](double v) { return int_shifts ? (double)(long long)v : v; };   // int() truncates
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    for (int k = tid; k < P; k += blockDim.x) {
+        const pano_pair_rec r = recs[k];
+        if (r.status != PANO_OK) atomicOr(&bad, 1);
+        rv[0][k] = conv(r.dx); rv[1][k] = conv(r.dy);
+        rv[2][k] = conv(r.xA); rv[3][k] = conv(r.yA); rv[4][k] = conv(r.xB); rv[5][k] = conv(r.yB);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        hdr[0] = PANO_OK;
+        if (bad) {
+            hdr[0] = PANO_E_NOMATCH;
+        } else {
+            double avg = 0.0;
+            if (int_shifts) {           // Python int sum, then true division
+                long long tot = 0;
+                for (int k = 0; k < P; ++k) tot += (long long)rv[1][k];
+                avg = (double)tot / (double)P;
+            } else {
+                double tot = 0.0;
+                for (int k = 0; k < P; ++k) tot = tot + rv[1][k];
+                avg = tot / (double)P;
+            }
+            int32_t first[2], hw[2];
+            const int rc = plan_core([&](int k, double *d) { d[0] = rv[0][k]; d[1] = rv[1][k] - avg; },
+                                     [&](int k, double *d) { for (int q = 0; q < 4; ++q) d[q] = rv[2 + q][k]; },
+                                     n, h, w, st, first, hw, tmp);
+            hdr[0] = rc ? rc : PANO_OK;
+            hdr[1] = hw[0];
+            hdr[2] = hw[1];
+            hdr[3] = first[0];
+            hdr[4] = first[1];
+            if (!rc && !(first[0] >= 0 && first[1] >= 0 && first[0] + w <= hw[1] && first[1] + h <= hw[0] &&
+                         hw[0] <= Hcap && hw[1] <= Wcap))
+                hdr[0] = PANO_E_OVERFLOW;
+        }
+    }
+    __syncthreads();
+    const int status = hdr[0];
+    if (status == PANO_OK) {
+        const int H = hdr[1], W = hdr[2];
+        for (int i = tid; i < n; i += blockDim.x) fx[i] = i ? st[i - 1].frame_x : hdr[3];
+        __syncthreads();
+        for (int i = tid; i < n; i += blockDim.x) {
+            bool ok = true;
+            if (i) {
+                const pano_step &q = st[i - 1];
+                ok = q.frame_x >= 0 && q.frame_x + w <= W && q.frame_y >= 0 && q.frame_y + h <= H &&
+                     q.canvas_y >= 0 && q.canvas_y + q.canvas_h <= H;
+            }
+            for (int j = 0; ok && j <= i - 2; ++j)      // frame i never meets a frame j <= i - 2
+                ok = fx[i] + w <= fx[j] || fx[j] + w <= fx[i];
+            if (!ok) atomicOr(&bad, 2);
+            dp->sa.fx[i] = fx[i];
+            dp->sa.fy[i] = i ? st[i - 1].frame_y : hdr[4];
+            dp->sa.is_a[i] = i ? (unsigned char)st[i - 1].frame_is_a : 0;
+            dp->sa.overlap[i] = i ? st[i - 1].overlap_range : 0.0;
+            if (i) dp->steps[i - 1] = st[i - 1];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        dp->status = (status == PANO_OK && (bad & 2)) ? PANO_E_OVERFLOW : status;
+        dp->n = n;
+        dp->H = status == PANO_OK ? hdr[1] : 0;
+        dp->W = status == PANO_OK ? hdr[2] : 0;
+        dp->first_x = hdr[3];
+        dp->first_y = hdr[4];
+    }
+}
+
+}  // namespace
+
+size_t plan_device_bytes() { return sizeof(DevPlan); }
+
+int launch_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, int w, int int_shifts,
+                       int Hcap, int Wcap, void *plan) {
+    if (n < 2 || n > kMaxSeq || h <= 0 || w <= 0 || !recs || !plan)
+        return pano_fail(ctx, PANO_E_ARG, "pano_plan_device: bad arguments");
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        plan_device<<<1, 256, 0, ctx->stream>>>(recs, n, h, w, int_shifts, Hcap, Wcap, (DevPlan *)plan);
+    }
+    PANO_LAUNCH_CHECK(ctx, "plan_device");
+    return PANO_OK;
+}
+
+int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                             int w, const void *plan, uint8_t *canvas, int Hcap, int Wcap, int thr,
+                             int32_t *bbox) {
+    if (n < 2 || n > kMaxSeq || !frames || !colnz || !canvas || !plan)
+        return pano_fail(ctx, PANO_E_ARG, "pano_composite_planned: bad arguments");
+    const DevPlan *dp = (const DevPlan *)plan;
+    const size_t o_w = ((size_t)n * w + 255) & ~size_t(255);
+    const size_t o_own = o_w + (((size_t)n * w * sizeof(float2) + 255) & ~size_t(255));
+    int rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, o_own + (size_t)Wcap * sizeof(ColInfo));
+    if (rc) return rc;
+    uint8_t *mode = ctx->flags;
+    float2 *wgt = (float2 *)(ctx->flags + o_w);
+    ColInfo *info = (ColInfo *)(ctx->flags + o_own);
+    static const SeqArg none{};
+    if (bbox) {
+        PanoProf prof_(ctx, PK_BBOX);
+        bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
+    }
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_tables<true><<<n, 256, 0, ctx->stream>>>(colnz, w, none, dp, mode, wgt);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_tables");
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_owner<true><<<(Wcap + 255) / 256, 256, 0, ctx->stream>>>(mode, wgt, n, w, Wcap, none, dp, info);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_owner");
+    {
+        dim3 grid((Wcap + 63) / 64, (Hcap + 4 * kCompRows - 1) / (4 * kCompRows));
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_pixels<true><<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, Hcap, Wcap, thr,
+                                                              bbox, dp);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_pixels");
+    if (bbox) {
+        PanoProf prof_(ctx, PK_BBOX);
+        bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
+    }
     return PANO_OK;
 }
 
@@ -589,18 +786,18 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
     }
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_tables<<<n, 256, 0, ctx->stream>>>(colnz, w, sa, mode, wgt);
+        composite_tables<false><<<n, 256, 0, ctx->stream>>>(colnz, w, sa, nullptr, mode, wgt);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_tables");
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_owner<<<(W + 255) / 256, 256, 0, ctx->stream>>>(mode, wgt, n, w, W, sa, info);
+        composite_owner<false><<<(W + 255) / 256, 256, 0, ctx->stream>>>(mode, wgt, n, w, W, sa, nullptr, info);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_owner");
     {
         dim3 grid((W + 63) / 64, (H + 4 * kCompRows - 1) / (4 * kCompRows));
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_pixels<<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, H, W, thr, bbox);
+        composite_pixels<false><<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, H, W, thr, bbox, nullptr);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_pixels");
     if (bbox) {

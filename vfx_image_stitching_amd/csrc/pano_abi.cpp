@@ -228,6 +228,22 @@ int pano_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *col
                                  black_threshold, bbox);
 }
 
+size_t pano_plan_device_bytes(void) { return plan_device_bytes(); }
+
+int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, int w, int int_shifts,
+                     int Hcap, int Wcap, void *plan) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_plan_device(ctx, recs, n, h, w, int_shifts, Hcap, Wcap, plan);
+}
+
+int pano_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                           int w, const void *plan, uint8_t *canvas, int Hcap, int Wcap,
+                           int black_threshold, int32_t *bbox) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_composite_planned(ctx, frames, colnz, n, h, w, plan, canvas, Hcap, Wcap,
+                                    black_threshold, bbox);
+}
+
 int pano_composite_sequential(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
                               int h, int w, const pano_step *steps, const int32_t *first_xy,
                               uint8_t *canvas, int H, int W) {

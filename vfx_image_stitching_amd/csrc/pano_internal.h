@@ -185,6 +185,12 @@ int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double th
 int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
                      int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
                      int H, int W);
+size_t plan_device_bytes();
+int launch_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, int w, int int_shifts,
+                       int Hcap, int Wcap, void *plan);
+int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
+                             int w, const void *plan, uint8_t *canvas, int Hcap, int Wcap, int thr,
+                             int32_t *bbox);
 int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
                           int h, int w, const pano_step *steps, const int32_t *first_xy,
                           uint8_t *canvas, int H, int W, int thr, int32_t *bbox);

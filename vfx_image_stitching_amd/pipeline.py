@@ -79,6 +79,8 @@ class Stitcher:
         self._graphs = {}                # key -> (pano_graph, outputs of the captured call)
         self._gstream = None             # private stream for capture / replay
         self.last_graphs = []            # graphs replayed by the last run(graph=True)
+        self.canvas_cap = None           # (Hcap, Wcap) of the device-planned canvas; None: auto
+        self._graph_mode = False
 
     # ------------------------------------------------------------------ buffers
     def _get(self, name, shape, dtype):
@@ -123,7 +125,7 @@ class Stitcher:
                                                 self.max_points, ptr(xy), ptr(desc), ptr(counts)))
         return xy, desc, counts
 
-    def pair_records(self, feats, pairs):
+    def pair_records(self, feats, pairs, out=None):
         T = self.torch
         pts, desc, counts = feats
         P = len(pairs)
@@ -138,7 +140,7 @@ class Stitcher:
         d2p = ptr(d2) if d2 is not None else None
         self.ctx.check(self.ctx.lib.pano_match(self.ctx.h, ptr(desc), ptr(counts), cap,
                                                _lib.i32p(hp), P, exact, ptr(best), ptr(d1), d2p))
-        recs = self._get("recs", (P, 64), T.uint8)
+        recs = out if out is not None else self._get("recs", (P, 64), T.uint8)
         kps_p = ptr(pts) if self.method == "sift" else None
         xy_p = None if self.method == "sift" else ptr(pts)
         self.ctx.check(self.ctx.lib.pano_pair_shifts(self.ctx.h, kps_p, xy_p, ptr(counts), cap,
@@ -263,17 +265,78 @@ class Stitcher:
                bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh, self.ratio)
         return self._replay(key, seg)
 
+    # ------------------------------------------------------------------ device-planned run
+    def _planned(self, frames_dev, focals):
+        """The whole stitch as ONE launch chain (one hipGraph with graph=True): records, the
+        device plan (drift correction + composite geometry, pano_plan_device) and the planned
+        composite into a capacity-sized canvas.  Returns (cyl, colnz, head, canvas) where head
+        is the single host read: the records, the crop box and the plan header."""
+        T = self.torch
+        n, h, w, _ = frames_dev.shape
+        P = n - 1
+        lib, c = self.ctx.lib, self.ctx.h
+        off_bb = P * 64
+        off_plan = (off_bb + 16 + 255) // 256 * 256
+        res = self._get("result", (off_plan + int(lib.pano_plan_device_bytes()),), T.uint8)
+        # canvas capacity: every step pads by at most one frame width (|dx| <= w for real
+        # overlaps) and the drift-corrected rows stay within one frame height; a plan above
+        # it reports PANO_E_OVERFLOW and run() composites with the host plan instead
+        Hcap, Wcap = self.canvas_cap or (2 * h, (n + 2) * w)
+        canvas = self._get("canvas_cap", (Hcap * Wcap * 3,), T.uint8)
+
+        def seg():
+            cyl, colnz = self.cylindrical(frames_dev, focals)
+            feats = self.features(cyl)
+            recs_dev, _ = self.pair_records(feats, [(i, i + 1) for i in range(P)], out=res[:off_bb])
+            self.ctx.check(lib.pano_plan_device(c, ptr(recs_dev), n, h, w, int(self.method != "sift"),
+                                                Hcap, Wcap, ptr(res[off_plan:])))
+            self.ctx.check(lib.pano_composite_planned(c, ptr(cyl), ptr(colnz), n, h, w,
+                                                      ptr(res[off_plan:]), ptr(canvas), Hcap, Wcap, 0,
+                                                      ptr(res[off_bb:off_bb + 16])))
+            return cyl, colnz
+
+        self._key_planned = key = (
+            "planned", frames_dev.data_ptr(), tuple(frames_dev.shape),
+            tuple(float(f) for f in np.asarray(focals, np.float64)), self.method, self.match,
+            bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh,
+            self.ratio, res.data_ptr(), canvas.data_ptr())
+        cyl, colnz = self._replay(key, seg) if self._graph_mode else seg()
+        head = res[:off_plan + 32].cpu().numpy()                        # the one sync point
+        return cyl, colnz, head, off_bb, off_plan, canvas
+
     # ------------------------------------------------------------------ whole run
     def run(self, frames_dev, focals, margin: int = 15, timers: bool = False,
-            graph: bool = False) -> StitchResult:
+            graph: bool = False, device_plan: bool = True) -> StitchResult:
+        """run_panorama's numeric body.  device_plan (default): one launch chain and one host
+        read per stitch; the host-planned form (two reads) runs when the plan reports a
+        canvas above capacity or a column covered by three frames, or with device_plan=False."""
         t = {}
         tick = time.perf_counter
         t0 = tick()
         self.last_graphs = []
+        n = frames_dev.shape[0]
+        if device_plan and 2 <= n <= 256:
+            self._graph_mode = graph
+            cyl, colnz, head, off_bb, off_plan, canvas = self._planned(frames_dev, focals)
+            recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1).copy()
+            hdr = head[off_plan:off_plan + 32].view(np.int32)
+            t["features_match_ransac"] = tick() - t0
+            if hdr[0] == _lib.PANO_E_NOMATCH:
+                raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+            if hdr[0] == _lib.PANO_OK:
+                shifts, best_pairs = self._shifts(recs)
+                H, W = int(hdr[1]), int(hdr[2])
+                view = canvas[:H * W * 3].view(H, W, 3)
+                bb = head[off_bb:off_bb + 16].view(np.int32)
+                return self._crop(view, bb, margin, shifts, best_pairs, recs, t, t0)
+            # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
+            return self._finish(cyl, colnz, recs, margin, graph, t, t0)
         cyl, colnz, recs_dev = self.records(frames_dev, focals, graph)
         recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)   # sync point 1
         t["features_match_ransac"] = tick() - t0
-        self.ctx.sync()
+        return self._finish(cyl, colnz, recs, margin, graph, t, t0)
+
+    def _shifts(self, recs):
         shifts, best_pairs = [], []
         for r in recs:
             if r["status"] != _lib.PANO_OK:
@@ -285,10 +348,20 @@ class Stitcher:
             else:
                 shifts.append((int(r["dx"]), int(r["dy"])))
                 best_pairs.append(((int(r["xA"]), int(r["yA"])), (int(r["xB"]), int(r["yB"]))))
+        return shifts, best_pairs
+
+    def _finish(self, cyl, colnz, recs, margin, graph, t, t0):
+        self.ctx.sync()
+        shifts, best_pairs = self._shifts(recs)
         corr = drift_correct(shifts)
         pxy = [(a[0], a[1], b[0], b[1]) for a, b in best_pairs]
         canvas, bb_dev = self.composite(cyl, colnz, corr, pxy, bbox=True, graph=graph)
         bb = bb_dev.cpu().numpy()                                        # sync point 2
+        return self._crop(canvas, bb, margin, shifts, best_pairs, recs, t, t0)
+
+    def _crop(self, canvas, bb, margin, shifts, best_pairs, recs, t, t0):
+        """rectangle_crop (image_stitching_sift.py:208-247) from the fused bbox."""
+        tick = time.perf_counter
         H = canvas.shape[0]
         if bb[1] < 0:
             y0, y1, x0, x1 = 0, H - 1, 0, canvas.shape[1] - 1
