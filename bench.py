@@ -31,6 +31,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
+MFMA_F32_PEAK_TFLOPS = 157.3    # dense f32 MFMA
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec (the blur's arithmetic)
 
 
@@ -273,6 +275,23 @@ def main():
                     "launches_per_step": launches_per_step,
                     "kernel_ms_per_step": round(per_step_ms, 4)}
 
+    # the one dense contraction (M1): the descriptor distance GEMM against the MFMA peak of
+    # its input type.  Algorithmic flops = sum over pairs of 2 N_A N_B 128 with the actual
+    # keypoint counts (tile padding not counted); time from the profiled eager step above.
+    roof_match = None
+    if args.method == "sift" and "dist_mfma" in per_kernel and per_kernel["dist_mfma"]["launches"]:
+        cnt = st._buf["counts"].cpu().numpy().astype(np.float64)
+        pairs = [(i, i + 1) for i in range(len(cnt) - 1)]
+        fl = sum(2.0 * cnt[a] * cnt[b] * 128 for a, b in pairs)
+        ms = per_kernel["dist_mfma"]["total_ms"]
+        pk = MFMA_BF16_PEAK_TFLOPS if st.match == "bf16" else MFMA_F32_PEAK_TFLOPS
+        tf = fl / (ms * 1e-3) / 1e12
+        roof_match = {"bound": "mfma", "kernel": "dist_mfma", "dtype": st.match,
+                      "achieved": round(tf, 2), "peak": pk, "unit": "TFLOP/s",
+                      "frac": round(tf / pk, 5), "flop_per_step": fl,
+                      "mean_keypoints": round(float(cnt.mean()), 1),
+                      "kernel_ms_per_step": round(ms, 4)}
+
     # correctness of what was timed: the single-GPU panorama against the reference's digest
     parity = None
     if world == 1 and args.workload != "synthetic":
@@ -296,6 +315,7 @@ def main():
                    "method": args.method, "match_gemm": st.match,
                    "launch": "hipGraph replay" if args.graph else "eager"},
         "roofline": roof,
+        "roofline_match": roof_match,
         "cpu_baseline": cpu,
         "parity": parity,
         "kernels_ms_per_step": {k: round(v["total_ms"], 4) for k, v in per_kernel.items()},
