@@ -28,8 +28,12 @@ def test_library_exports_every_header_symbol():
     assert sorted(_lib.SIGNATURES) == syms
 
 
-def test_library_is_gfx950():
-    out = os.popen(f"/opt/rocm/lib/llvm/bin/llvm-objdump --offloading {os.path.join(ROOT, 'vfx_image_stitching_amd', 'libpano.so')} 2>&1").read()
+def test_library_is_gfx950(tmp_path):
+    # llvm-objdump --offloading extracts the bundles next to its input: run it on a copy
+    import shutil
+    lib = tmp_path / "libpano.so"
+    shutil.copy(os.path.join(ROOT, "vfx_image_stitching_amd", "libpano.so"), lib)
+    out = os.popen(f"/opt/rocm/lib/llvm/bin/llvm-objdump --offloading {lib} 2>&1").read()
     if "gfx950" not in out:
         # older objdump: grep the embedded bundle name
         data = open(os.path.join(ROOT, "vfx_image_stitching_amd", "libpano.so"), "rb").read()

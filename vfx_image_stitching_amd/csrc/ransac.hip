@@ -81,15 +81,17 @@ __device__ void vote_argmax(const double2 *mv, int k, double thr, double2 *tile,
     __syncthreads();
 }
 
+// Large K (1080p: thousands of matches per pair) makes the K x K vote the bulk of the work,
+// so it is split over many workgroups: pair_compact (one workgroup per pair: the ordered
+// compaction, K to HBM), pair_votes (grid = hypothesis chunks x pairs, LDS-tiled, votes to
+// HBM), pair_select (one workgroup per pair: first maximum, record).
 __global__ void __launch_bounds__(RB)
-pair_shifts(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
-            const int32_t *__restrict__ counts, int cap, PairArg pairs,
-            const int32_t *__restrict__ best, const float *__restrict__ d1,
-            const float *__restrict__ d2, float desc_thresh, double ratio2, double thr,
-            double2 *__restrict__ moves, int32_t *__restrict__ midx,
-            pano_pair_rec *__restrict__ recs) {
+pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
+             const int32_t *__restrict__ counts, int cap, PairArg pairs,
+             const int32_t *__restrict__ best, const float *__restrict__ d1,
+             const float *__restrict__ d2, float desc_thresh, double ratio2,
+             double2 *__restrict__ moves, int32_t *__restrict__ midx, int32_t *__restrict__ kcount) {
     __shared__ int ish[2 * RB];
-    __shared__ double2 tile[RB];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int fa = pairs.a[p], fb = pairs.b[p];
     const int NA = min(max(counts[fa], 0), cap);
@@ -123,7 +125,49 @@ pair_shifts(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
         }
         K += tot;
     }
-    __syncthreads();
+    if (tid == 0) kcount[p] = K;
+}
+
+constexpr int VB = 256;   // hypotheses per pair_votes workgroup
+
+__global__ void __launch_bounds__(VB)
+pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount, int cap,
+           double thr, int32_t *__restrict__ votes) {
+    __shared__ double2 tile[VB];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int K = kcount[p];
+    const int m0 = blockIdx.x * VB;
+    if (m0 >= K) return;                              // whole workgroup
+    const double2 *mv = moves + (size_t)p * cap;
+    const int m = m0 + tid;
+    const double2 me = m < K ? mv[m] : make_double2(0.0, 0.0);
+    int v = 0;
+    for (int j0 = 0; j0 < K; j0 += VB) {
+        __syncthreads();
+        if (j0 + tid < K) tile[tid] = mv[j0 + tid];
+        __syncthreads();
+        const int nj = K - j0 < VB ? K - j0 : VB;
+        for (int j = 0; j < nj; ++j) {
+            const double ddx = tile[j].x - me.x;
+            const double ddy = tile[j].y - me.y;
+            v += (ddx * ddx + ddy * ddy) < thr;
+        }
+    }
+    if (m < K) votes[(size_t)p * cap + m] = v;
+}
+
+__global__ void __launch_bounds__(RB)
+pair_select(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy, int cap, PairArg pairs,
+            const int32_t *__restrict__ best, const double2 *__restrict__ moves,
+            const int32_t *__restrict__ midx, const int32_t *__restrict__ kcount,
+            const int32_t *__restrict__ votes, pano_pair_rec *__restrict__ recs) {
+    __shared__ int ish[2 * RB];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    const int K = kcount[p];
+    const int32_t *bp = best + (size_t)p * cap;
+    const double2 *mv = moves + (size_t)p * cap;
+    const int32_t *mi = midx + (size_t)p * cap;
     pano_pair_rec r{};
     r.n_matches = K;
     if (K == 0) {
@@ -134,8 +178,27 @@ pair_shifts(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
         }
         return;
     }
-    int bm, bv;
-    vote_argmax(mv, K, thr, tile, ish, &bm, &bv);
+    // first maximum (strict '>' in match order, image_stitching_sift.py:107)
+    int my_v = -1, my_m = 0x7fffffff;
+    for (int m = tid; m < K; m += RB) {
+        const int v = votes[(size_t)p * cap + m];
+        if (v > my_v) { my_v = v; my_m = m; }
+    }
+    ish[tid] = my_v;
+    ish[RB + tid] = my_m;
+    __syncthreads();
+    for (int off = RB / 2; off > 0; off >>= 1) {
+        if (tid < off) {
+            const int v2 = ish[tid + off], m2 = ish[RB + tid + off];
+            const int v1 = ish[tid], m1 = ish[RB + tid];
+            if (v2 > v1 || (v2 == v1 && m2 < m1)) {
+                ish[tid] = v2;
+                ish[RB + tid] = m2;
+            }
+        }
+        __syncthreads();
+    }
+    const int bm = ish[RB], bv = ish[0];
     if (tid == 0) {
         const int i = mi[bm];
         const int j = bp[i];
@@ -179,11 +242,14 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
     if (cap <= 0 || n_pairs <= 0 || (!kps && !xy_i32) || !counts || !best || !d1 ||
         (!d2 && ratio > 0) || !recs)
         return pano_fail(ctx, PANO_E_ARG, "pano_pair_shifts: bad arguments");
-    const size_t need = (size_t)n_pairs * cap * (sizeof(double2) + sizeof(int32_t)) + 256;
+    const size_t need = (size_t)n_pairs * cap * (sizeof(double2) + 2 * sizeof(int32_t)) +
+                        (size_t)n_pairs * sizeof(int32_t) + 256;
     int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, need);
     if (rc) return rc;
     double2 *moves = (double2 *)ctx->bscratch;
     int32_t *midx = (int32_t *)(moves + (size_t)n_pairs * cap);
+    int32_t *votes = midx + (size_t)n_pairs * cap;
+    int32_t *kcount = votes + (size_t)n_pairs * cap;
     for (int p0 = 0; p0 < n_pairs; p0 += 256) {
         const int np = n_pairs - p0 < 256 ? n_pairs - p0 : 256;
         PairArg pa;
@@ -191,14 +257,26 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
             pa.a[q] = h_pairs[2 * (p0 + q)];
             pa.b[q] = h_pairs[2 * (p0 + q) + 1];
         }
+        const size_t o = (size_t)p0 * cap;
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
-            pair_shifts<<<np, RB, 0, ctx->stream>>>(
-                kps, xy_i32, counts, cap, pa, best + (size_t)p0 * cap, d1 + (size_t)p0 * cap,
-                d2 ? d2 + (size_t)p0 * cap : nullptr, (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, thr,
-                moves + (size_t)p0 * cap, midx + (size_t)p0 * cap, recs + p0);
+            pair_compact<<<np, RB, 0, ctx->stream>>>(
+                kps, xy_i32, counts, cap, pa, best + o, d1 + o, d2 ? d2 + o : nullptr,
+                (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, moves + o, midx + o, kcount + p0);
         }
-        PANO_LAUNCH_CHECK(ctx, "pair_shifts");
+        PANO_LAUNCH_CHECK(ctx, "pair_compact");
+        {
+            PanoProf prof_(ctx, PK_PAIR_SHIFTS);
+            pair_votes<<<dim3((cap + VB - 1) / VB, np), VB, 0, ctx->stream>>>(moves + o, kcount + p0, cap,
+                                                                             thr, votes + o);
+        }
+        PANO_LAUNCH_CHECK(ctx, "pair_votes");
+        {
+            PanoProf prof_(ctx, PK_PAIR_SHIFTS);
+            pair_select<<<np, RB, 0, ctx->stream>>>(kps, xy_i32, cap, pa, best + o, moves + o, midx + o,
+                                                   kcount + p0, votes + o, recs + p0);
+        }
+        PANO_LAUNCH_CHECK(ctx, "pair_select");
     }
     return PANO_OK;
 }
