@@ -4,7 +4,7 @@
 //                     (LDS-tiled, every octave in one launch)
 //   localize          localize_extremum_via_quadratic_fit :169-211 (thread per candidate)
 //   orientation       compute_keypoints_with_orientations :246-293 (wave per candidate)
-//   rank_keys         compare_keypoints :299-316 (rank = sorted slot, whole-GPU all-pairs)
+//   bucket_*          compare_keypoints :299-316 (rank = sorted slot: counting sort on x)
 //   emit_keypoints    remove_duplicate_keypoints :319-327 + convert_keypoints_to_input_image_size
 //                     :333-343 (workgroup per frame)
 //   descriptor        unpack_octave :349-358 + generate_descriptors :361-526
@@ -534,70 +534,90 @@ __device__ __forceinline__ bool rec_before(const RawKp &a, const RawKp &b) {
 }
 
 // The reference's sort (compare_keypoints, stable) is a strict total order once scan order
-// breaks ties, so each keypoint's sorted position is its RANK: rank_keys counts, for every
-// raw keypoint, how many keys of its frame precede it -- ~count^2 compares per frame spread
-// over the whole GPU, keys staged through LDS in chunks -- and scatters its index to that
-// slot.  emit_keypoints then de-duplicates neighbours and converts (one workgroup per frame).
-constexpr int kRankChunk = 2048;
+// breaks ties, so each keypoint's sorted position is its RANK.  Ranks come from a counting
+// sort on floor(x) (monotone in the primary key): bucket_count histograms the integer x of
+// every raw keypoint (the atomic's return value is its slot), bucket_scan turns the counts
+// into bucket starts, bucket_scatter lists each bucket's members, and bucket_rank adds to
+// the bucket start the number of members that sort before the keypoint (64-bit (x, y) key,
+// the full comparator on an equal key).  O(count x bucket size) instead of count^2 per
+// frame: a handful of compares per keypoint (1080p: ~30k raw keypoints over 3840 buckets).
+// emit_keypoints then de-duplicates neighbours and converts (one workgroup per frame).
+__device__ __forceinline__ int x_bucket(float x, int nb) {
+    const int b = (int)floorf(x);
+    return b < 0 ? 0 : (b >= nb ? nb - 1 : b);
+}
 
-// Block = 64 keypoints x 4 waves: wave q counts, for its lane's keypoint, the keys of
-// quarter q of each LDS chunk that sort before it (8 keys per step, one pass; the full
-// comparator only on a step holding an equal (x, y) key); the 4 partial ranks are summed.
+__device__ __forceinline__ unsigned long long xy_key(const RawKp &r) {
+    return ((unsigned long long)sortable(r.x) << 32) | sortable(r.y);
+}
+
 __global__ void __launch_bounds__(256)
-rank_keys(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
-          uint32_t *__restrict__ sorted) {
-    __shared__ unsigned long long ks[kRankChunk];
-    __shared__ int part[4][64];
-    const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+bucket_count(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
+             int32_t *__restrict__ bstart, int32_t *__restrict__ bslot) {
+    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
     const int cnt = raw_cnt[f * kCntStride];
-    if (cnt > raw_cap || (int)blockIdx.x * 64 >= cnt) return;
+    if (cnt > raw_cap || i >= cnt) return;
+    const int b = x_bucket(raw[(size_t)f * raw_cap + i].x, nb);
+    bslot[(size_t)f * raw_cap + i] = atomicAdd(&bstart[(size_t)f * nb + b], 1);
+}
+
+__global__ void __launch_bounds__(1024)
+bucket_scan(int32_t *__restrict__ bstart, int nb) {   // counts -> exclusive starts, in place
+    __shared__ int sh[1024];
+    int32_t *c = bstart + (size_t)blockIdx.x * nb;
+    const int tid = threadIdx.x;
+    int carry = 0;
+    for (int base = 0; base < nb; base += 1024) {
+        const int v = base + tid < nb ? c[base + tid] : 0;
+        sh[tid] = v;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            const int t = tid >= off ? sh[tid - off] : 0;
+            __syncthreads();
+            sh[tid] += t;
+            __syncthreads();
+        }
+        if (base + tid < nb) c[base + tid] = carry + sh[tid] - v;
+        carry += sh[1023];
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256)
+bucket_scatter(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
+               const int32_t *__restrict__ bstart, const int32_t *__restrict__ bslot,
+               uint32_t *__restrict__ mem) {
+    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int cnt = raw_cnt[f * kCntStride];
+    if (cnt > raw_cap || i >= cnt) return;
+    const int b = x_bucket(raw[(size_t)f * raw_cap + i].x, nb);
+    mem[(size_t)f * raw_cap + bstart[(size_t)f * nb + b] + bslot[(size_t)f * raw_cap + i]] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(256)
+bucket_rank(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
+            const int32_t *__restrict__ bstart, const uint32_t *__restrict__ mem,
+            uint32_t *__restrict__ sorted) {
+    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int cnt = raw_cnt[f * kCntStride];
+    if (cnt > raw_cap || i >= cnt) return;
     const RawKp *rec = raw + (size_t)f * raw_cap;
-    const int i = blockIdx.x * 64 + lane;
-    const bool live = i < cnt;
-    unsigned long long ki = ~0ull;
-    if (live) ki = ((unsigned long long)sortable(rec[i].x) << 32) | sortable(rec[i].y);
-    int rank = 0;
-    for (int c0 = 0; c0 < cnt; c0 += kRankChunk) {
-        const int m = min(kRankChunk, cnt - c0);
-        const int m32 = (m + 31) & ~31;                 // pad: ~0 keys never sort before
-        __syncthreads();
-        for (int t = tid; t < m32; t += 256) {
-            unsigned long long k = ~0ull;
-            if (t < m) {
-                const RawKp &r = rec[c0 + t];
-                k = ((unsigned long long)sortable(r.x) << 32) | sortable(r.y);
-            }
-            ks[t] = k;
-        }
-        __syncthreads();
-        if (!live) continue;
-        const int qs = (m32 >> 2) * q, qe = qs + (m32 >> 2);
-        for (int t = qs; t < qe; t += 8) {
-            unsigned long long k8[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) k8[u] = ks[t + u];
-            bool anyeq = false;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                rank += k8[u] < ki;
-                anyeq |= k8[u] == ki;
-            }
-            if (anyeq) {                                // ties on (x, y): full comparator
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int j = c0 + t + u;
-                    if (k8[u] == ki && j != i && rec_before(rec[j], rec[i])) ++rank;
-                }
-            }
-        }
+    const uint32_t *mb = mem + (size_t)f * raw_cap;
+    const RawKp ri = rec[i];
+    const unsigned long long ki = xy_key(ri);
+    const int b = x_bucket(ri.x, nb);
+    const int s = bstart[(size_t)f * nb + b];
+    const int e = b + 1 < nb ? bstart[(size_t)f * nb + b + 1] : cnt;
+    int r = s;
+    for (int m = s; m < e; ++m) {
+        const uint32_t j = mb[m];
+        if (j == (uint32_t)i) continue;
+        const RawKp &rj = rec[j];
+        const unsigned long long kj = xy_key(rj);
+        r += kj < ki || (kj == ki && rec_before(rj, ri));
     }
-    part[q][lane] = rank;
-    __syncthreads();
-    if (q == 0 && live) {
-        const int r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-        if (r < cnt) sorted[(size_t)f * raw_cap + r] = (uint32_t)i;
-        else atomicExch(&sorted[(size_t)f * raw_cap], 0xFFFFFFFFu);   // order broken: flag
-    }
+    if (r < cnt) sorted[(size_t)f * raw_cap + r] = (uint32_t)i;
+    else atomicExch(&sorted[(size_t)f * raw_cap], 0xFFFFFFFFu);   // order broken: flag
 }
 
 __global__ void __launch_bounds__(1024)
@@ -1054,14 +1074,38 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
     {
-        rc = pano_grow(ctx, (void **)&ctx->sorted, &ctx->sorted_bytes, raw_cap * n * sizeof(uint32_t));
+        const int nb = ctx->oct_w[0] + 1;               // floor(x) buckets over the base width
+        const size_t per = raw_cap * n;
+        rc = pano_grow(ctx, (void **)&ctx->sorted, &ctx->sorted_bytes,
+                       (3 * per + (size_t)nb * n) * sizeof(uint32_t));
         if (rc) return rc;
-        dim3 grid((unsigned)((raw_cap + 63) / 64), n);
+        uint32_t *mem = ctx->sorted + per;
+        int32_t *bslot = (int32_t *)(ctx->sorted + 2 * per);
+        int32_t *bstart = (int32_t *)(ctx->sorted + 3 * per);
+        rc = launch_fill(ctx, bstart, 0, (size_t)nb * n * sizeof(int32_t));
+        if (rc) return rc;
+        dim3 grid((unsigned)((raw_cap + 255) / 256), n);
         {
             PanoProf prof_(ctx, PK_SORT);
-            rank_keys<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted);
+            bucket_count<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, bslot);
         }
-        PANO_LAUNCH_CHECK(ctx, "rank_keys");
+        PANO_LAUNCH_CHECK(ctx, "bucket_count");
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            bucket_scan<<<n, 1024, 0, ctx->stream>>>(bstart, nb);
+        }
+        PANO_LAUNCH_CHECK(ctx, "bucket_scan");
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            bucket_scatter<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, bslot, mem);
+        }
+        PANO_LAUNCH_CHECK(ctx, "bucket_scatter");
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            bucket_rank<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, mem,
+                                                       ctx->sorted);
+        }
+        PANO_LAUNCH_CHECK(ctx, "bucket_rank");
         {
             PanoProf prof_(ctx, PK_SORT);
             emit_keypoints<<<n, 1024, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted,
