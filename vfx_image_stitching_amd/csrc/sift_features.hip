@@ -802,6 +802,13 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         g[2] = q[-cols];
         g[3] = q[cols];
     };
+    // (x-1, x, x+1) of patch row yi at patch column xi
+    auto trip = [&](int xi, int yi, float (&T)[3]) {
+        const float *q = img + (size_t)(py + yi - half) * cols + (px + xi - half) - 1;
+        T[0] = q[0];
+        T[1] = q[1];
+        T[2] = q[2];
+    };
     auto sample = [&](int xi, int yi, const float (&g)[4]) {
         const int xs = xi - half, ys = yi - half;
         const double rrot = (double)xs * sin_a + (double)ys * cos_a;
@@ -904,32 +911,54 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             }
             int r = t - cpre[c];
             int ncol = cpre[c + 1] - cpre[c];
-            // software pipeline: the next sample's four gradient taps are in flight while
-            // the current one is binned
+            // A lane's run walks down patch columns, so its taps come from a sliding window
+            // of three row triples (x-1, x, x+1) at rows y-1, y, y+1: one 12-byte load per
+            // sample (three at a column change) instead of four scattered dword loads -- the
+            // lanes are far apart, so every load instruction costs one L1 tag lookup per lane
+            // and the tap count, not the arithmetic, bounded this kernel.  The next sample's
+            // triple is in flight while the current one is binned.
             while (r >= ncol) {
                 r -= ncol;
                 ++c;
                 ncol = cpre[c + 1] - cpre[c];
             }
             int xi = c, yi = clo[c] + r + half;
-            float g[4];
-            taps(xi, yi, g);
+            float Tm[3], T0[3], Tp[3];
+            trip(xi, yi - 1, Tm);
+            trip(xi, yi, T0);
+            trip(xi, yi + 1, Tp);
             for (++t, ++r; t < tend; ++t, ++r) {
+                bool newcol = false;
                 while (r >= ncol) {
                     r -= ncol;
                     ++c;
                     ncol = cpre[c + 1] - cpre[c];
+                    newcol = true;
                 }
                 const int xn = c, yn = clo[c] + r + half;
-                float gn[4];
-                taps(xn, yn, gn);
-                sample(xi, yi, g);
+                float N0[3], N1[3], N2[3];
+                if (newcol) {
+                    trip(xn, yn - 1, N0);
+                    trip(xn, yn, N1);
+                }
+                trip(xn, yn + 1, N2);
+                {
+                    const float g[4] = {T0[2], T0[0], Tm[1], Tp[1]};
+                    sample(xi, yi, g);
+                }
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    Tm[i] = newcol ? N0[i] : T0[i];
+                    T0[i] = newcol ? N1[i] : Tp[i];
+                    Tp[i] = N2[i];
+                }
                 xi = xn;
                 yi = yn;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) g[i] = gn[i];
             }
-            sample(xi, yi, g);
+            {
+                const float g[4] = {T0[2], T0[0], Tm[1], Tp[1]};
+                sample(xi, yi, g);
+            }
         }
     } else {
         // very large patches: every sample of the (side x side) square, cheap range test first
