@@ -270,6 +270,12 @@ typedef struct pano_graph pano_graph;
 int pano_graph_begin(pano_ctx *ctx);
 int pano_graph_end(pano_ctx *ctx, pano_graph **out);
 int pano_graph_launch(pano_ctx *ctx, pano_graph *g);
+/* Replay g on `hip_stream` (NULL: the context's stream) and wait for it: the batched
+ * stitch's whole per-call GPU work as one call (its last node copies the result header to
+ * pinned host memory, pano_copy_async). */
+int pano_graph_launch_sync(pano_ctx *ctx, pano_graph *g, void *hip_stream);
+/* hipMemcpyAsync on the context's stream (device or pinned host pointers; capturable). */
+int pano_copy_async(pano_ctx *ctx, void *dst, const void *src, size_t bytes);
 int pano_graph_prof(pano_graph *g, int kernel_class, int *launches, double *total_ms);
 int pano_graph_destroy(pano_graph *g);
 

@@ -349,6 +349,20 @@ int pano_graph_launch(pano_ctx *ctx, pano_graph *g) {
     return PANO_OK;
 }
 
+int pano_graph_launch_sync(pano_ctx *ctx, pano_graph *g, void *stream) {
+    if (!ctx || !g) return PANO_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    PANO_HIP(ctx, hipGraphLaunch(g->exec, s));
+    PANO_HIP(ctx, hipStreamSynchronize(s));
+    return PANO_OK;
+}
+
+int pano_copy_async(pano_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!ctx || (bytes && (!dst || !src))) return PANO_E_ARG;
+    if (bytes) PANO_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream));
+    return PANO_OK;
+}
+
 int pano_graph_prof(pano_graph *g, int kernel_class, int *launches, double *total_ms) {
     if (!g || !launches || !total_ms) return PANO_E_ARG;
     int n = 0;

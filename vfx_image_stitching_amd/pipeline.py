@@ -284,6 +284,13 @@ class Stitcher:
         Hcap, Wcap = self.canvas_cap or (2 * h, (n + 2) * w)
         canvas = self._get("canvas_cap", (Hcap * Wcap * 3,), T.uint8)
 
+        nhead = off_plan + 32
+        pin = self._buf.get("head_pin")
+        if pin is None or pin.numel() < nhead:
+            pin = T.empty(max(nhead, 4096), dtype=T.uint8, pin_memory=True)
+            self._buf["head_pin"] = pin
+            self._head_np = pin.numpy()
+
         def seg():
             cyl, colnz = self.cylindrical(frames_dev, focals)
             feats = self.features(cyl)
@@ -293,6 +300,8 @@ class Stitcher:
             self.ctx.check(lib.pano_composite_planned(c, ptr(cyl), ptr(colnz), n, h, w,
                                                       ptr(res[off_plan:]), ptr(canvas), Hcap, Wcap, 0,
                                                       ptr(res[off_bb:off_bb + 16])))
+            # the records, crop box and plan header to pinned host memory: the one host read
+            self.ctx.check(lib.pano_copy_async(c, _lib._P(pin.data_ptr()), ptr(res), nhead))
             return cyl, colnz
 
         self._key_planned = key = (
@@ -300,8 +309,19 @@ class Stitcher:
             tuple(float(f) for f in np.asarray(focals, np.float64)), self.method, self.match,
             bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh,
             self.ratio, res.data_ptr(), canvas.data_ptr())
-        cyl, colnz = self._replay(key, seg) if self._graph_mode else seg()
-        head = res[:off_plan + 32].cpu().numpy()                        # the one sync point
+        ent = self._graphs.get(key) if self._graph_mode else None
+        if ent is not None:       # replay on the caller's stream and wait: one library call
+            cur = T.cuda.current_stream(self.device).cuda_stream
+            self.ctx.check(lib.pano_graph_launch_sync(c, ent[0], _lib._P(cur)))
+            self.last_graphs.append(ent[0])
+            cyl, colnz = ent[1]
+        elif self._graph_mode:
+            cyl, colnz = self._replay(key, seg)
+            T.cuda.current_stream(self.device).synchronize()
+        else:
+            cyl, colnz = seg()
+            self.ctx.sync()
+        head = self._head_np[:nhead]                                     # the one sync point
         return cyl, colnz, head, off_bb, off_plan, canvas
 
     # ------------------------------------------------------------------ whole run
