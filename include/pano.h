@@ -205,6 +205,8 @@ int pano_composite_sequential(pano_ctx *ctx, const uint8_t *d_frames, const uint
  * int32 {status, H, W, n, first_x, first_y}: status PANO_OK, PANO_E_NOMATCH (a pair had
  * no match: the reference fails there), or PANO_E_OVERFLOW (canvas above the capacity or a
  * column covered by three frames: use pano_plan_composite + pano_composite_bbox instead).
+ * d_bbox as pano_composite_bbox's, except that no pixel above the threshold is reported
+ * as d_bbox[1] < 0 with the other three entries unspecified (no fix-up launch).
  * Nothing is read back by either call (graph-capturable).  2 <= n <= 256. */
 size_t pano_plan_device_bytes(void);
 int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *d_recs, int n, int h, int w,

@@ -14,7 +14,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpano.so")
+# PANO_LIB: an alternative build of the same ABI (A/B timing of two revisions, tools/ab_build.sh)
+LIB_PATH = os.environ.get("PANO_LIB") or os.path.join(_HERE, "libpano.so")
 
 PANO_OK = 0
 PANO_E_ARG = -1

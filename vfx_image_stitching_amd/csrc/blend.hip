@@ -152,7 +152,10 @@ struct DevPlan {
 template <bool DEV>
 __global__ void __launch_bounds__(256)
 composite_tables(const uint8_t *__restrict__ colnz, int w, SeqArg sa_arg, const DevPlan *__restrict__ dp,
-                 uint8_t *__restrict__ mode, float2 *__restrict__ wgt) {
+                 uint8_t *__restrict__ mode, float2 *__restrict__ wgt, int32_t *__restrict__ bbox) {
+    if (DEV && bbox && blockIdx.x == 0 && threadIdx.x == 0) {   // crop box init (planned path)
+        bbox[0] = 0x7fffffff; bbox[1] = -1; bbox[2] = 0x7fffffff; bbox[3] = -1;
+    }
     if (DEV && (dp->status != PANO_OK || (int)blockIdx.x >= dp->n)) return;
     const SeqArg &sa = DEV ? dp->sa : sa_arg;
     __shared__ int sh[256];
@@ -245,14 +248,13 @@ __global__ void __launch_bounds__(256)
 composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const ColInfo *__restrict__ info,
                  uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox,
                  const DevPlan *__restrict__ dp) {
-    if (DEV) {   // grid sized for the capacity; the planned canvas is [H][W] inside it
-        if (dp->status != PANO_OK) return;
-        H = dp->H;
-        W = dp->W;
-        if ((int)blockIdx.x * 64 >= W || (int)blockIdx.y * 4 * kCompRows >= H) return;
-    }
     __shared__ int r[4][256];
     const int tid = threadIdx.x;
+    if (DEV) {   // grid sized for the capacity; the planned canvas is [H][W] inside it
+        H = dp->status == PANO_OK ? dp->H : 0;
+        W = dp->status == PANO_OK ? dp->W : 0;
+        if ((int)blockIdx.x * 64 >= W || (int)blockIdx.y * 4 * kCompRows >= H) return;
+    }
     int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
     const int X = blockIdx.x * 64 + (tid & 63);
     const int y0 = (blockIdx.y * 4 + (tid >> 6)) * kCompRows;
@@ -662,13 +664,9 @@ int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t
     float2 *wgt = (float2 *)(ctx->flags + o_w);
     ColInfo *info = (ColInfo *)(ctx->flags + o_own);
     static const SeqArg none{};
-    if (bbox) {
-        PanoProf prof_(ctx, PK_BBOX);
-        bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
-    }
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_tables<true><<<n, 256, 0, ctx->stream>>>(colnz, w, none, dp, mode, wgt);
+        composite_tables<true><<<n, 256, 0, ctx->stream>>>(colnz, w, none, dp, mode, wgt, bbox);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_tables");
     {
@@ -683,10 +681,6 @@ int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t
                                                               bbox, dp);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_pixels");
-    if (bbox) {
-        PanoProf prof_(ctx, PK_BBOX);
-        bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
-    }
     return PANO_OK;
 }
 
@@ -786,7 +780,7 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
     }
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_tables<false><<<n, 256, 0, ctx->stream>>>(colnz, w, sa, nullptr, mode, wgt);
+        composite_tables<false><<<n, 256, 0, ctx->stream>>>(colnz, w, sa, nullptr, mode, wgt, nullptr);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_tables");
     {

@@ -21,11 +21,12 @@ struct FocalArg {
 };
 
 __global__ void __launch_bounds__(256)
-cyl_scatter(int32_t *__restrict__ win, int h, int w, FocalArg focal) {
+cyl_scatter(int32_t *__restrict__ win, int h, int w, FocalArg focal, uint8_t *__restrict__ colnz) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int f = blockIdx.z;
     if (x >= w || y >= h) return;
+    if (colnz && y == 0) colnz[(size_t)f * w + x] = 0;   // cyl_gather sets the non-zero columns
     const double fl = focal.f[f];
     const int cx = w / 2, cy = h / 2;
     const int xd = x - cx, yd = y - cy;
@@ -74,7 +75,6 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
     int32_t *win = (int32_t *)ctx->bscratch;
     rc = launch_fill(ctx, win, 0xFF, plane * n * sizeof(int32_t));
     if (rc) return rc;
-    if (colnz && (rc = launch_fill(ctx, colnz, 0, (size_t)n * w))) return rc;
     for (int f0 = 0; f0 < n; f0 += kFocalChunk) {
         const int nf = n - f0 < kFocalChunk ? n - f0 : kFocalChunk;
         FocalArg fa;
@@ -82,7 +82,8 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
         dim3 grid((w + 63) / 64, (h + 3) / 4, nf);
         {
             PanoProf prof_(ctx, PK_CYL_SCATTER);
-            cyl_scatter<<<grid, 256, 0, ctx->stream>>>(win + f0 * plane, h, w, fa);
+            cyl_scatter<<<grid, 256, 0, ctx->stream>>>(win + f0 * plane, h, w, fa,
+                                                       colnz ? colnz + (size_t)f0 * w : nullptr);
         }
         PANO_LAUNCH_CHECK(ctx, "cyl_scatter");
         {

@@ -397,7 +397,10 @@ struct OriParams {
 __global__ void __launch_bounds__(256)
 orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             const int32_t *__restrict__ cand_cnt, int cand_cap, RawKp *__restrict__ raw,
-            int32_t *__restrict__ raw_cnt, int raw_cap) {
+            int32_t *__restrict__ raw_cnt, int raw_cap, int32_t *__restrict__ zero, int nzero) {
+    // the sort's bucket counters are zeroed here (their first use is the next launch)
+    for (int i = linear_block_id() * 256 + threadIdx.x; i < nzero; i += gridDim.x * gridDim.y * 256)
+        zero[i] = 0;
     __shared__ unsigned long long hist[4][PANO_ORI_BINS];
     __shared__ double hd[4][PANO_ORI_BINS];
     __shared__ double sm[4][PANO_ORI_BINS];
@@ -1093,26 +1096,23 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         for (int l = 0; l < nl; ++l) pa.gauss[o][l] = ctx->pyr + ctx->gauss_off[o][l];
     }
     OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio};
+    const int nb = ctx->oct_w[0] + 1;                   // sort: floor(x) buckets over the base width
+    const size_t per = raw_cap * n;
+    rc = pano_grow(ctx, (void **)&ctx->sorted, &ctx->sorted_bytes, (3 * per + (size_t)nb * n) * sizeof(uint32_t));
+    if (rc) return rc;
+    uint32_t *mem = ctx->sorted + per;
+    int32_t *bslot = (int32_t *)(ctx->sorted + 2 * per);
+    int32_t *bstart = (int32_t *)(ctx->sorted + 3 * per);
     {
         dim3 grid((unsigned)((cand_cap + 3) / 4), n);
         {
             PanoProf prof_(ctx, PK_ORIENT);
             orientation<<<grid, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap,
-                                                       ctx->raw, raw_cnt, (int)raw_cap);
+                                                       ctx->raw, raw_cnt, (int)raw_cap, bstart, nb * n);
         }
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
     {
-        const int nb = ctx->oct_w[0] + 1;               // floor(x) buckets over the base width
-        const size_t per = raw_cap * n;
-        rc = pano_grow(ctx, (void **)&ctx->sorted, &ctx->sorted_bytes,
-                       (3 * per + (size_t)nb * n) * sizeof(uint32_t));
-        if (rc) return rc;
-        uint32_t *mem = ctx->sorted + per;
-        int32_t *bslot = (int32_t *)(ctx->sorted + 2 * per);
-        int32_t *bstart = (int32_t *)(ctx->sorted + 3 * per);
-        rc = launch_fill(ctx, bstart, 0, (size_t)nb * n * sizeof(int32_t));
-        if (rc) return rc;
         dim3 grid((unsigned)((raw_cap + 255) / 256), n);
         {
             PanoProf prof_(ctx, PK_SORT);

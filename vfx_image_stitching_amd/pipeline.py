@@ -357,17 +357,17 @@ class Stitcher:
         return self._finish(cyl, colnz, recs, margin, graph, t, t0)
 
     def _shifts(self, recs):
-        shifts, best_pairs = [], []
-        for r in recs:
-            if r["status"] != _lib.PANO_OK:
-                # the reference's blend would fail on a None pair (image_stitching_sift.py:164)
-                raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
-            if self.method == "sift":
-                shifts.append((float(r["dx"]), float(r["dy"])))
-                best_pairs.append(((float(r["xA"]), float(r["yA"])), (float(r["xB"]), float(r["yB"]))))
-            else:
-                shifts.append((int(r["dx"]), int(r["dy"])))
-                best_pairs.append(((int(r["xA"]), int(r["yA"])), (int(r["xB"]), int(r["yB"]))))
+        """Per-pair moves and best pairs as the reference's Python values: floats of the
+        float32 coordinates for SIFT, int() of them for Harris."""
+        if np.any(recs["status"] != _lib.PANO_OK):
+            # the reference's blend would fail on a None pair (image_stitching_sift.py:164)
+            raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+        cols = [recs[k] for k in ("dx", "dy", "xA", "yA", "xB", "yB")]
+        if self.method != "sift":
+            cols = [np.trunc(c).astype(np.int64) for c in cols]
+        dx, dy, xa, ya, xb, yb = (c.tolist() for c in cols)
+        shifts = list(zip(dx, dy))
+        best_pairs = [((a, b), (c, d)) for a, b, c, d in zip(xa, ya, xb, yb)]
         return shifts, best_pairs
 
     def _finish(self, cyl, colnz, recs, margin, graph, t, t0):
