@@ -366,49 +366,38 @@ __device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_N
     return (int)floor(d * inv);
 }
 
-// One tail level, compile-time tap count (NT = 0: runtime count n).  in / outb / rowt are
-// [64][kTP] LDS planes; g / d the frame's Gaussian and DoG planes in HBM.  SG outputs per
-// thread per pass (register-blocked sliding window, taps in tap order).
+// One tail level, compile-time tap count (NT = 0: runtime count n).  in / outb are [64][kTP]
+// LDS planes; g / d the frame's Gaussian and DoG planes in HBM.  The small octaves are all
+// border: instead of reflecting every tap (a runtime modulo per tap and output), the level
+// is first copied into `pad` with its BORDER_REFLECT_101 columns ([H][W + 2R]), the row pass
+// runs branch-free over it into rows [R, R + H) of `rowt`, whose reflected halo rows are then
+// filled in, and the column pass runs branch-free too.  SG outputs per thread per pass
+// (register-blocked sliding window, taps in tap order: blur_level's arithmetic).
+constexpr int kRMax = (PANO_MAX_TAPS - 1) / 2;
+constexpr int kPP = (kTailDim + 8 + 2 * kRMax) | 1;     // pad pitch (segment overrun included)
+constexpr int kRowtRows = kTailDim + 8 + 2 * kRMax;
+
 template <int NT>
-__device__ __forceinline__ void tail_level(const float *in, float *outb, float *rowt, int H, int W,
-                                           const double *__restrict__ taps_g, int n_rt, float *g,
+__device__ __forceinline__ void tail_level(const float *in, float *outb, float *pad, float *rowt, int H,
+                                           int W, const double *__restrict__ taps_g, int n_rt, float *g,
                                            float *d, int tid) {
     constexpr int SG = 8;
     const int n = NT > 0 ? NT : n_rt;
     const int R = (n - 1) / 2;
-    constexpr int KMAX = NT > 0 ? NT : PANO_MAX_TAPS;
     double k[NT > 0 ? NT : 1];
     if constexpr (NT > 0) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) k[t] = taps_g[t];
     }
-    (void)KMAX;
     auto tap = [&](int t) -> double { if constexpr (NT > 0) return k[t]; else return taps_g[t]; };
-    // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
-    const int nseg = (W + SG - 1) / SG;
-    for (int it = tid; it < H * nseg; it += kTailThreads) {
-        const int y = it % H, x0 = (it / H) * SG;
-        const float *src = in + y * kTP;
-        double acc[SG];
-#pragma unroll
-        for (int j = 0; j < SG; ++j) acc[j] = 0.0;
+    auto conv = [&](const float *p, int stride, double (&acc)[SG]) {
         if constexpr (NT > 0) {
-            if (x0 - R >= 0 && x0 + SG + R <= W) {
-                conv_seg<NT, SG>(src + x0 - R, 1, k, acc);
-            } else {
-#pragma unroll
-                for (int i = 0; i < SG + NT - 1; ++i) {
-                    const double v = (double)src[reflect_fast(x0 - R + i, W)];
-#pragma unroll
-                    for (int j = 0; j < SG; ++j) {
-                        const int t = i - j;
-                        if (t >= 0 && t < NT) acc[j] = fma(k[t], v, acc[j]);
-                    }
-                }
-            }
+            conv_seg<NT, SG>(p, stride, k, acc);
         } else {
+#pragma unroll
+            for (int j = 0; j < SG; ++j) acc[j] = 0.0;
             for (int i = 0; i < SG + n - 1; ++i) {
-                const double v = (double)src[reflect101(x0 - R + i, W)];
+                const double v = (double)p[i * stride];
 #pragma unroll
                 for (int j = 0; j < SG; ++j) {
                     const int t = i - j;
@@ -416,9 +405,30 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
                 }
             }
         }
+    };
+    // reflected columns
+    const int PW = W + 2 * R;
+    for (int i = tid; i < H * PW; i += kTailThreads) {
+        const int y = i / PW, c = i - (i / PW) * PW;
+        pad[y * kPP + c] = in[y * kTP + reflect101(c - R, W)];
+    }
+    __syncthreads();
+    // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
+    const int nseg = (W + SG - 1) / SG;
+    for (int it = tid; it < H * nseg; it += kTailThreads) {
+        const int y = it % H, x0 = (it / H) * SG;
+        double acc[SG];
+        conv(pad + y * kPP + x0, 1, acc);
 #pragma unroll
         for (int j = 0; j < SG; ++j)
-            if (x0 + j < W) rowt[y * kTP + x0 + j] = (float)acc[j];
+            if (x0 + j < W) rowt[(y + R) * kTP + x0 + j] = (float)acc[j];
+    }
+    __syncthreads();
+    // reflected rows of the row-pass output
+    for (int i = tid; i < 2 * R * W; i += kTailThreads) {
+        const int q = i / W, x = i - (i / W) * W;
+        const int ry = q < R ? q - R : H + (q - R);
+        rowt[(ry + R) * kTP + x] = rowt[(reflect101(ry, H) + R) * kTP + x];
     }
     __syncthreads();
     // column pass: item = (column x, segment of SG rows); lanes on consecutive columns
@@ -426,32 +436,7 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
     for (int it = tid; it < W * nrs; it += kTailThreads) {
         const int x = it % W, y0 = (it / W) * SG;
         double acc[SG];
-#pragma unroll
-        for (int j = 0; j < SG; ++j) acc[j] = 0.0;
-        if constexpr (NT > 0) {
-            if (y0 - R >= 0 && y0 + SG + R <= H) {
-                conv_seg<NT, SG>(rowt + (y0 - R) * kTP + x, kTP, k, acc);
-            } else {
-#pragma unroll
-                for (int i = 0; i < SG + NT - 1; ++i) {
-                    const double v = (double)rowt[reflect_fast(y0 - R + i, H) * kTP + x];
-#pragma unroll
-                    for (int j = 0; j < SG; ++j) {
-                        const int t = i - j;
-                        if (t >= 0 && t < NT) acc[j] = fma(k[t], v, acc[j]);
-                    }
-                }
-            }
-        } else {
-            for (int i = 0; i < SG + n - 1; ++i) {
-                const double v = (double)rowt[reflect101(y0 - R + i, H) * kTP + x];
-#pragma unroll
-                for (int j = 0; j < SG; ++j) {
-                    const int t = i - j;
-                    if (t >= 0 && t < n) acc[j] = fma(tap(t), v, acc[j]);
-                }
-            }
-        }
+        conv(rowt + y0 * kTP + x, kTP, acc);
 #pragma unroll
         for (int j = 0; j < SG; ++j) {
             const int y = y0 + j;
@@ -467,7 +452,8 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
 __global__ void __launch_bounds__(kTailThreads)
 blur_tail(TailArgs ta) {
     __shared__ float lv[3][kTailDim * kTP];      // current / next level, octave seed
-    __shared__ float rowt[kTailDim * kTP];
+    __shared__ float pad[kTailDim * kPP];         // level with reflected columns
+    __shared__ float rowt[kRowtRows * kTP];       // row-pass output with reflected rows
     // the tail is a latency chain of 18 workgroups running beside the extrema scan, which
     // fills every CU: raise its waves' issue priority so the chain is not starved
     __builtin_amdgcn_s_setprio(3);
@@ -504,12 +490,12 @@ blur_tail(TailArgs ta) {
             float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
             const double *tg = ta.taps + l * PANO_MAX_TAPS;
             switch (n) {   // the reference's kernel sizes; others take the runtime-count path
-                case 11: tail_level<11>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
-                case 13: tail_level<13>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
-                case 17: tail_level<17>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
-                case 21: tail_level<21>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
-                case 27: tail_level<27>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
-                default: tail_level<0>(lv[cur], lv[out], rowt, H, W, tg, n, g, d, tid); break;
+                case 11: tail_level<11>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
+                case 13: tail_level<13>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
+                case 17: tail_level<17>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
+                case 21: tail_level<21>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
+                case 27: tail_level<27>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
+                default: tail_level<0>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
             }
             __syncthreads();
             cur = out;
@@ -702,10 +688,30 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                                     ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
     }
-    // fork the small-octave tail onto the side stream as soon as its input exists
-    // (G[o_tail-1][nl-3]); only the last small blurs of that octave are then in flight, so
-    // its n workgroups get CUs before the extrema scan fills the GPU
-    auto fork_tail = [&]() -> int {
+    // The small octaves run on a high-priority side stream, beside the main stream's last
+    // large-octave levels and extrema scan: the last o_tail - o_side blur_fast octaves (their
+    // launches are one workgroup's latency each) and then the fused tail (octaves <= 64 x 64,
+    // blur_tail).  The fork comes as soon as the side's first input exists (G[o_side-1][nl-3]);
+    // keypoints split the extrema scan at o_side and join before the second part.
+    static const int side_oct = [] {
+        const char *e = getenv("PANO_SIDE_OCT");   // measured: 0 beats 1 and 2 (co-run contention)
+        return e ? atoi(e) : 0;
+    }();
+    const int o_side = o_tail < no ? std::max(1, o_tail - std::max(0, side_oct)) : no;
+    hipStream_t main_stream = ctx->stream;
+    auto fork = [&]() -> int {
+        if (!ctx->side) {
+            int lo_prio = 0, hi_prio = 0;   // numerically lower = higher priority
+            PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+            PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi_prio));
+            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+        }
+        PANO_HIP(ctx, hipEventRecord(ctx->ev_fork, main_stream));
+        PANO_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+        return PANO_OK;
+    };
+    auto launch_tail = [&]() -> int {
         // device copy of the level taps (uploaded only when they change)
         double th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
         TailArgs ta{};
@@ -736,15 +742,6 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
             for (int l = 0; l < nl; ++l) ta.G[oi][l] = G + ctx->gauss_off[o][l];
             for (int l = 0; l + 1 < nl; ++l) ta.D[oi][l] = D + ctx->dog_off[o][l];
         }
-        if (!ctx->side) {
-            int lo_prio = 0, hi_prio = 0;   // numerically lower = higher priority
-            PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-            PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi_prio));
-            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-        }
-        PANO_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
-        PANO_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
         {
             PanoProf prof_(ctx, PK_BLUR, ctx->side);
             blur_tail<<<n, kTailThreads, 0, ctx->side>>>(ta);
@@ -752,11 +749,12 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         PANO_LAUNCH_CHECK(ctx, "blur_tail");
         PANO_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
         ctx->tail_pending = true;
-        ctx->o_tail = o_tail;
+        ctx->o_tail = o_side;
         return PANO_OK;
     };
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
+        ctx->stream = o >= o_side ? ctx->side : main_stream;     // side-stream octaves
         for (int l = 1; l < nl; ++l) {
             float *out = G + ctx->gauss_off[o][l];
             float *dg = D + ctx->dog_off[o][l - 1];
@@ -776,12 +774,19 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                 rc = launch_blur<MODE_LEVEL>(ctx, la, (full || l < nl - 1) ? out : nullptr, dg, nullptr,
                                              n, H, W, tl[l]);
             }
-            if (rc) return rc;
-            if (o == o_tail - 1 && l == nl - 3 && o_tail < no) {
-                rc = fork_tail();
-                if (rc) return rc;
+            if (rc) { ctx->stream = main_stream; return rc; }
+            if (o == o_side - 1 && l == nl - 3 && o_tail < no) {
+                rc = fork();
+                if (rc) { ctx->stream = main_stream; return rc; }
             }
         }
+    }
+    ctx->stream = main_stream;
+    if (o_tail < no) {
+        rc = launch_tail();
+        if (rc) return rc;
+        static const bool tail_solo = getenv("PANO_TAIL_SOLO") != nullptr;   // diagnostics
+        if (tail_solo) sift_join_tail(ctx);
     }
     if (o_tail < no && !defer_tail) sift_join_tail(ctx);
     ctx->pyr_full = full;
