@@ -82,7 +82,6 @@ class Stitcher:
         self.canvas_cap = None           # (Hcap, Wcap) of the device-planned canvas; None: auto
         self._graph_mode = False
         self._fast = None                # (key, replay state) of run()'s graph fast path
-        self._memo = None                # (header bytes, canvas, parsed products) of the last run
         self._fast_key = None
 
     # ------------------------------------------------------------------ buffers
@@ -364,22 +363,11 @@ class Stitcher:
             if hdr[0] == _lib.PANO_E_NOMATCH:
                 raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
             if hdr[0] == _lib.PANO_OK:
-                # host-side products of the read-back header, memoised on its bytes (a replayed
-                # stitch of the same frames reads back the same header): the Python lists, the
-                # canvas view and the crop view
-                hb = head[:off_plan + 32].tobytes() + bytes([margin & 255])
-                memo = self._memo
-                if memo is not None and memo[0] == hb and memo[1] is canvas:
-                    shifts, best_pairs, view, pano, box = memo[2]
-                    t["total"] = tick() - t0
-                    return StitchResult(pano, view, list(shifts), list(best_pairs), recs, box, t)
                 shifts, best_pairs = self._shifts(recs)
                 H, W = int(hdr[1]), int(hdr[2])
-                view = canvas[:H * W * 3].view(H, W, 3)
+                view = canvas.as_strided((H, W, 3), (W * 3, 3, 1))
                 bb = head[off_bb:off_bb + 16].view(np.int32)
-                res = self._crop(view, bb, margin, shifts, best_pairs, recs, t, t0)
-                self._memo = (hb, canvas, (list(shifts), list(best_pairs), view, res.panorama, res.bbox))
-                return res
+                return self._crop(view, bb, margin, shifts, best_pairs, recs, t, t0)
             # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
             return self._finish(cyl, colnz, recs, margin, graph, t, t0)
         cyl, colnz, recs_dev = self.records(frames_dev, focals, graph)
@@ -421,6 +409,8 @@ class Stitcher:
             y0 = max(0, int(bb[0]) + margin)
             y1 = min(H - 1, int(bb[1]) - margin)
             x0, x1 = int(bb[2]), int(bb[3])
-            pano = canvas if (y0 > y1 or x0 > x1) else canvas[y0:y1 + 1, x0:x1 + 1]
+            pano = canvas if (y0 > y1 or x0 > x1) else canvas.as_strided(
+                (y1 + 1 - y0, x1 + 1 - x0, 3), canvas.stride(), canvas.storage_offset() +
+                y0 * canvas.stride(0) + x0 * 3)
         t["total"] = tick() - t0
         return StitchResult(pano, canvas, shifts, best_pairs, recs, (y0, y1, x0, x1), t)
