@@ -51,6 +51,25 @@ def test_cylindrical_bit_exact(gpu, setname, gold_json):
         assert np.array_equal(cz[i].astype(bool), (h[i] != 0).any(axis=(0, 2)))
 
 
+@pytest.mark.parametrize("focal", [6.0, 17.5, 40.0, 700.0])
+def test_cylindrical_inverse_map_strong_distortion(gpu, focal):
+    """The inverse-map kernels against the oracle's forward scatter where the map is far from
+    the identity (focal lengths comparable to the frame: several sources per destination,
+    destinations no source reaches), on odd sizes."""
+    from oracle import stitch as ostitch
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    rng = np.random.default_rng(7)
+    frames = rng.integers(0, 256, (3, 37, 53, 3), dtype=np.uint8)
+    frames[1, :, :5] = 0                                  # zero columns: colnz flags
+    st = Stitcher("sift")
+    cyl, colnz = st.cylindrical(st.upload(frames), [focal, focal * 1.5, focal])
+    h = cyl.cpu().numpy()
+    for i, f in enumerate([focal, focal * 1.5, focal]):
+        ref = ostitch.cylindrical(frames[i], f)
+        assert np.array_equal(h[i], ref), (i, f)
+        assert np.array_equal(colnz.cpu().numpy()[i].astype(bool), (ref != 0).any(axis=(0, 2)))
+
+
 # ------------------------------------------------------------------ S1..S4
 @pytest.mark.parametrize("api", ["pano_sift_pyramid", "pano_sift"])
 def test_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl, api):

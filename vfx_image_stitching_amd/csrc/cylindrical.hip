@@ -5,12 +5,18 @@
 // Python round = half-even), so for colliding destinations the last writer (largest
 // row-major source index) wins and unwritten pixels stay 0.
 //
-// gfx950 formulation: pass 1 scatters the source linear index with atomicMax into an
-// int32 winner map (one 4-byte atomic per source pixel), pass 2 gathers 3 bytes per
-// destination pixel and raises the per-column "any non-zero byte" flag the compositor
-// needs (blend_two_images counts non-zeros per column, :185-189).
-// Bytes per frame pixel: 3 read (scatter: none of the pixel data) + 4 atomic + 4 read +
-// 3 gathered + 3 written  ->  roofline unit C1 = 6 B/pixel algorithmic.
+// gfx950 formulation: the map is inverted instead of scattered.  Both coordinate maps are
+// monotone (x' in xd through atan, y' in yd for a fixed xd), so the sources that land on a
+// destination pixel form a small box of consecutive candidates around the inverse images
+// f tan(k/f) and k den/f; every candidate is re-checked with the forward formula itself
+// (the same f64 operations and rounding), and the winner is the candidate with the largest
+// row-major index -- the reference's last writer.  cyl_columns resolves the candidate
+// source columns of every destination column once per frame; cyl_inverse then writes every
+// destination pixel once (no winner map, no atomics, no memset) and raises the per-column
+// "any non-zero byte" flag the compositor needs (blend_two_images, :185-189).
+// Roofline unit C1 = 6 B/pixel algorithmic: 3 read + 3 written.
+// (The scatter form, cyl_scatter + cyl_gather over an atomicMax winner map, is kept as the
+// checked alternative: PANO_CYL_SCATTER=1.)
 #include "pano_internal.h"
 
 namespace {
@@ -61,6 +67,75 @@ cyl_gather(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
     if (colnz && (b | g | r)) colnz[(size_t)f * w + x] = 1;
 }
 
+// Source-column range [lo, hi] of destination column x' (inclusive; empty if lo > hi),
+// exact: every candidate of a conservative box around f tan((k +- 1/2)/f) is tested with
+// the forward map.  Also zeroes the column's non-zero flag (cyl_inverse raises it).
+__global__ void __launch_bounds__(256)
+cyl_columns(int w, FocalArg focal, int2 *__restrict__ cols, uint8_t *__restrict__ colnz) {
+    const int xp = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
+    if (xp >= w) return;
+    const double fl = focal.f[f];
+    const int cx = w / 2, k = xp - cx;
+    // inverse images of k -+ 1/2 (arguments kept inside the atan range; clamped to the frame)
+    const double lim = 1.5707963267948966 - 1e-12;
+    const double ta = fmax(fmin((k - 0.5) / fl, lim), -lim), tb = fmax(fmin((k + 0.5) / fl, lim), -lim);
+    const double a = fmax(fl * tan(ta), -cx - 2.0), b = fmin(fl * tan(tb), (double)(w - cx + 1));
+    const int c0 = (int)floor(a) - 1, c1 = (int)ceil(b) + 1;
+    int lo = 1, hi = 0;
+    for (int xd = c0; xd <= c1; ++xd) {
+        const int x = xd + cx;
+        if (x < 0 || x >= w) continue;
+        const int xm = (int)rint(fl * atan((double)xd / fl)) + cx;
+        if (xm != xp) continue;
+        if (lo > hi) lo = x;
+        hi = x;
+    }
+    cols[(size_t)f * w + xp] = make_int2(lo, hi);
+    if (colnz) colnz[(size_t)f * w + xp] = 0;
+}
+
+__global__ void __launch_bounds__(256)
+cyl_inverse(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 *__restrict__ cols,
+            uint8_t *__restrict__ colnz, int h, int w, FocalArg focal) {
+    const int xp = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int yp = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (xp >= w || yp >= h) return;
+    const double fl = focal.f[f];
+    const int cx = w / 2, cy = h / 2, k = yp - cy;
+    const int2 cr = cols[(size_t)f * w + xp];
+    long best = -1;                                   // largest row-major source index
+    for (int x = cr.x; x <= cr.y; ++x) {
+        const int xd = x - cx;
+        const double den = sqrt((double)xd * (double)xd + fl * fl);
+        const double s = den / fl;
+        // rows whose forward y' can be k: a box around [(k - 1/2) s, (k + 1/2) s], scanned
+        // from the top (the first hit is this column's largest row)
+        const int r1 = (int)ceil((k + 0.5) * s) + 1, r0 = (int)floor((k - 0.5) * s) - 1;
+        for (int yd = r1; yd >= r0; --yd) {
+            const int y = yd + cy;
+            if (y < 0 || y >= h) continue;
+            const int ym = (int)rint(fl * ((double)yd / den)) + cy;
+            if (ym != yp) continue;
+            const long li = (long)y * w + x;
+            if (li > best) best = li;
+            break;
+        }
+    }
+    uint8_t b = 0, g = 0, r = 0;
+    if (best >= 0) {
+        const uint8_t *p = src + ((size_t)f * h * w + (size_t)best) * 3;
+        b = p[0];
+        g = p[1];
+        r = p[2];
+    }
+    uint8_t *q = dst + (((size_t)f * h + yp) * w + xp) * 3;
+    q[0] = b;
+    q[1] = g;
+    q[2] = r;
+    if (colnz && (b | g | r)) colnz[(size_t)f * w + xp] = 1;
+}
+
 }  // namespace
 
 int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
@@ -69,6 +144,31 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
         return pano_fail(ctx, PANO_E_ARG, "pano_cylindrical: bad arguments");
     if ((long long)h * w >= (1LL << 31)) return pano_fail(ctx, PANO_E_ARG, "frame too large");
     const size_t plane = (size_t)h * w;
+    static const bool scatter_form = getenv("PANO_CYL_SCATTER") != nullptr;
+    if (!scatter_form) {
+        int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, (size_t)n * w * sizeof(int2));
+        if (rc) return rc;
+        int2 *cols = (int2 *)ctx->bscratch;
+        for (int f0 = 0; f0 < n; f0 += kFocalChunk) {
+            const int nf = n - f0 < kFocalChunk ? n - f0 : kFocalChunk;
+            FocalArg fa;
+            for (int i = 0; i < nf; ++i) fa.f[i] = h_focal[f0 + i];
+            {
+                PanoProf prof_(ctx, PK_CYL_SCATTER);
+                cyl_columns<<<dim3((w + 255) / 256, nf), 256, 0, ctx->stream>>>(
+                    w, fa, cols + (size_t)f0 * w, colnz ? colnz + (size_t)f0 * w : nullptr);
+            }
+            PANO_LAUNCH_CHECK(ctx, "cyl_columns");
+            {
+                PanoProf prof_(ctx, PK_CYL_GATHER);
+                cyl_inverse<<<dim3((w + 63) / 64, (h + 3) / 4, nf), 256, 0, ctx->stream>>>(
+                    src + f0 * plane * 3, dst + f0 * plane * 3, cols + (size_t)f0 * w,
+                    colnz ? colnz + (size_t)f0 * w : nullptr, h, w, fa);
+            }
+            PANO_LAUNCH_CHECK(ctx, "cyl_inverse");
+        }
+        return PANO_OK;
+    }
     const size_t need = plane * n * sizeof(int32_t);
     int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, need);
     if (rc) return rc;
