@@ -205,9 +205,12 @@ int pano_composite_sequential(pano_ctx *ctx, const uint8_t *d_frames, const uint
  * int32 {status, H, W, n, first_x, first_y}: status PANO_OK, PANO_E_NOMATCH (a pair had
  * no match: the reference fails there), or PANO_E_OVERFLOW (canvas above the capacity or a
  * column covered by three frames: use pano_plan_composite + pano_composite_bbox instead).
- * d_bbox as pano_composite_bbox's, except that no pixel above the threshold is reported
- * as d_bbox[1] < 0 with the other three entries unspecified (no fix-up launch).
+ * d_bbox: PANO_BBOX_SLOTS (64) partial boxes {ymin, ymax, xmin, xmax} (int32[256]); the
+ * crop box is their elementwise min / max, with ymax < 0 when no pixel passed the threshold
+ * (workgroups spread their atomics over the slots instead of serialising on one box).
  * Nothing is read back by either call (graph-capturable).  2 <= n <= 256. */
+#define PANO_BBOX_SLOTS 64   /* crop-box partials of pano_composite_planned (one box
+                                serialised every workgroup's atomics at L2: 48 us/stitch) */
 size_t pano_plan_device_bytes(void);
 int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *d_recs, int n, int h, int w,
                      int int_shifts, int Hcap, int Wcap, void *d_plan);

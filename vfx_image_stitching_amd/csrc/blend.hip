@@ -24,6 +24,18 @@ __device__ __forceinline__ uint8_t blend_px(float a32, float b32, uint8_t A, uin
     return (uint8_t)(int)v;   // astype(np.uint8) on a non-negative float: truncation
 }
 
+__device__ __forceinline__ void box_init_slot(int32_t *b) {
+    b[0] = 0x7fffffff; b[1] = -1; b[2] = 0x7fffffff; b[3] = -1;
+}
+// one workgroup's box into slot (workgroup id mod PANO_BBOX_SLOTS)
+__device__ __forceinline__ void box_commit(int32_t *slots, int ymin, int ymax, int xmin, int xmax) {
+    int32_t *b = slots + 4 * (linear_block_id() % PANO_BBOX_SLOTS);
+    atomicMin(&b[0], ymin);
+    atomicMax(&b[1], ymax);
+    atomicMin(&b[2], xmin);
+    atomicMax(&b[3], xmax);
+}
+
 __global__ void __launch_bounds__(256)
 place_first(const uint8_t *__restrict__ frame, const uint8_t *__restrict__ colnz, int h, int w,
             uint8_t *__restrict__ canvas, int W, int fy, int fx, uint8_t *__restrict__ F0,
@@ -153,9 +165,8 @@ template <bool DEV>
 __global__ void __launch_bounds__(256)
 composite_tables(const uint8_t *__restrict__ colnz, int w, SeqArg sa_arg, const DevPlan *__restrict__ dp,
                  uint8_t *__restrict__ mode, float2 *__restrict__ wgt, int32_t *__restrict__ bbox) {
-    if (DEV && bbox && blockIdx.x == 0 && threadIdx.x == 0) {   // crop box init (planned path)
-        bbox[0] = 0x7fffffff; bbox[1] = -1; bbox[2] = 0x7fffffff; bbox[3] = -1;
-    }
+    if (DEV && bbox && blockIdx.x == 0 && threadIdx.x < PANO_BBOX_SLOTS)   // crop-box slots init
+        box_init_slot(bbox + 4 * threadIdx.x);
     if (DEV && (dp->status != PANO_OK || (int)blockIdx.x >= dp->n)) return;
     const SeqArg &sa = DEV ? dp->sa : sa_arg;
     __shared__ int sh[256];
@@ -265,16 +276,22 @@ composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const ColInfo
         const uint8_t *fp = frames + (((size_t)max(ci.i, 0) * h) * w + ci.c) * 3;
         const uint8_t *mp = frames + (((size_t)max(ci.i - 1, 0) * h) * w + max(ci.cm, 0)) * 3;
         const bool blend = ci.i >= 0 && ci.mode == 2;
+        // every load is issued unconditionally from a clamped (in-frame) address and the
+        // out-of-frame bytes are zeroed afterwards: predicated loads compiled to a branch and
+        // a wait per byte, serialising the 48 loads of a thread
 #pragma unroll
         for (int k = 0; k < kCompRows; ++k) {
             const int y = y0 + k;
             const int fyl = y - ci.fy, ym = y - ci.fym;
             const bool fin = ci.i >= 0 && y < H && fyl >= 0 && fyl < h;
             const bool min_ = blend && y < H && ci.cm >= 0 && ym >= 0 && ym < h;
+            const size_t fo = (size_t)min(max(fyl, 0), h - 1) * w * 3;
+            const size_t mo = (size_t)min(max(ym, 0), h - 1) * w * 3;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                F[k][c] = fin ? fp[(size_t)fyl * w * 3 + c] : 0;
-                M[k][c] = min_ ? mp[(size_t)ym * w * 3 + c] : 0;
+                const uint8_t fv = fp[fo + c], mv = mp[mo + c];
+                F[k][c] = fin ? fv : 0;
+                M[k][c] = min_ ? mv : 0;
             }
         }
 #pragma unroll
@@ -307,12 +324,7 @@ composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const ColInfo
         }
         __syncthreads();
     }
-    if (tid == 0 && r[1][0] >= 0) {
-        atomicMin(&bbox[0], r[0][0]);
-        atomicMax(&bbox[1], r[1][0]);
-        atomicMin(&bbox[2], r[2][0]);
-        atomicMax(&bbox[3], r[3][0]);
-    }
+    if (tid == 0 && r[1][0] >= 0) box_commit(bbox, r[0][0], r[1][0], r[2][0], r[3][0]);
 }
 
 // ------------------------------------------------------------------ generic blend_two_images
@@ -390,9 +402,6 @@ blend_two(const uint8_t *__restrict__ A, int hA, int wA, int ayA, int axA,
 }
 
 // ------------------------------------------------------------------ rectangle_crop bbox
-__global__ void bbox_init(int32_t *bbox) {
-    bbox[0] = 0x7fffffff; bbox[1] = -1; bbox[2] = 0x7fffffff; bbox[3] = -1;
-}
 
 __global__ void __launch_bounds__(256)
 gray_bbox(const uint8_t *__restrict__ img, int H, int W, int thr, int32_t *__restrict__ bbox) {
@@ -418,16 +427,26 @@ gray_bbox(const uint8_t *__restrict__ img, int H, int W, int thr, int32_t *__res
         }
         __syncthreads();
     }
-    if (tid == 0 && r[1][0] >= 0) {
-        atomicMin(&bbox[0], r[0][0]);
-        atomicMax(&bbox[1], r[1][0]);
-        atomicMin(&bbox[2], r[2][0]);
-        atomicMax(&bbox[3], r[3][0]);
-    }
+    if (tid == 0 && r[1][0] >= 0) box_commit(bbox, r[0][0], r[1][0], r[2][0], r[3][0]);
 }
 
-__global__ void bbox_fix(int32_t *bbox) {
-    if (bbox[1] < 0) bbox[0] = bbox[1] = bbox[2] = bbox[3] = -1;
+__global__ void bbox_init(int32_t *slots) {   // PANO_BBOX_SLOTS threads
+    box_init_slot(slots + 4 * threadIdx.x);
+}
+
+// slots -> the 4-int box, -1s when no pixel passed (one wave)
+__global__ void bbox_fix(const int32_t *__restrict__ slots, int32_t *__restrict__ bbox) {
+    const int t = threadIdx.x;
+    int a = 0x7fffffff, b = -1, c = 0x7fffffff, d = -1;
+    if (t < PANO_BBOX_SLOTS) { a = slots[4 * t]; b = slots[4 * t + 1]; c = slots[4 * t + 2]; d = slots[4 * t + 3]; }
+    for (int o = 32; o > 0; o >>= 1) {
+        a = min(a, __shfl_xor(a, o)); b = max(b, __shfl_xor(b, o));
+        c = min(c, __shfl_xor(c, o)); d = max(d, __shfl_xor(d, o));
+    }
+    if (t == 0) {
+        if (b < 0) a = b = c = d = -1;
+        bbox[0] = a; bbox[1] = b; bbox[2] = c; bbox[3] = d;
+    }
 }
 
 }  // namespace
@@ -774,9 +793,13 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
     uint8_t *mode = ctx->flags + o_mode;
     float2 *wgt = (float2 *)(ctx->flags + o_w);
     ColInfo *info = (ColInfo *)(ctx->flags + o_own);
+    int32_t *slots = nullptr;
     if (bbox) {
+        rc = pano_grow(ctx, (void **)&ctx->boxslots, &ctx->boxslots_bytes, 4 * PANO_BBOX_SLOTS * sizeof(int32_t));
+        if (rc) return rc;
+        slots = ctx->boxslots;
         PanoProf prof_(ctx, PK_BBOX);
-        bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
+        bbox_init<<<1, PANO_BBOX_SLOTS, 0, ctx->stream>>>(slots);
     }
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
@@ -791,12 +814,12 @@ int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *c
     {
         dim3 grid((W + 63) / 64, (H + 4 * kCompRows - 1) / (4 * kCompRows));
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_pixels<false><<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, H, W, thr, bbox, nullptr);
+        composite_pixels<false><<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, H, W, thr, slots, nullptr);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_pixels");
     if (bbox) {
         PanoProf prof_(ctx, PK_BBOX);
-        bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
+        bbox_fix<<<1, 64, 0, ctx->stream>>>(slots, bbox);
     }
     return PANO_OK;
 }
@@ -847,15 +870,18 @@ int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint
 
 int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox) {
     if (!img || !bbox || H <= 0 || W <= 0) return pano_fail(ctx, PANO_E_ARG, "pano_gray_bbox");
-    bbox_init<<<1, 1, 0, ctx->stream>>>(bbox);
+    int rc = pano_grow(ctx, (void **)&ctx->boxslots, &ctx->boxslots_bytes, 4 * PANO_BBOX_SLOTS * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *slots = ctx->boxslots;
+    bbox_init<<<1, PANO_BBOX_SLOTS, 0, ctx->stream>>>(slots);
     const size_t total = (size_t)H * W;
     unsigned blocks = (unsigned)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     {
         PanoProf prof_(ctx, PK_BBOX);
-        gray_bbox<<<blocks, 256, 0, ctx->stream>>>(img, H, W, thr, bbox);
+        gray_bbox<<<blocks, 256, 0, ctx->stream>>>(img, H, W, thr, slots);
     }
-    bbox_fix<<<1, 1, 0, ctx->stream>>>(bbox);
+    bbox_fix<<<1, 64, 0, ctx->stream>>>(slots, bbox);
     PANO_LAUNCH_CHECK(ctx, "gray_bbox");
     return PANO_OK;
 }

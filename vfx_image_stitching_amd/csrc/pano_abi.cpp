@@ -101,7 +101,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
-                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted};
+                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted, ctx->boxslots};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);

@@ -87,6 +87,7 @@ struct pano_ctx {
     double taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // what *taps holds
     bool taps_valid = false;
     uint8_t *gray = nullptr; size_t gray_bytes = 0;   // u8 gray frames (base blur input)
+    int32_t *boxslots = nullptr; size_t boxslots_bytes = 0;   // crop-box partials (kBoxSlots x 4)
     // ---- match / ransac scratch
     void *mscratch = nullptr; size_t mscratch_bytes = 0;
     // ---- composite scratch

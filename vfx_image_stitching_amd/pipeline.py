@@ -31,6 +31,9 @@ from . import _lib
 from ._lib import PanoError, context, ptr
 
 
+BBOX_SLOTS = 64                         # include/pano.h PANO_BBOX_SLOTS
+
+
 @dataclass
 class StitchResult:
     panorama: "object"                 # torch uint8 [H', W', 3] on device (a view of canvas)
@@ -280,7 +283,7 @@ class Stitcher:
         P = n - 1
         lib, c = self.ctx.lib, self.ctx.h
         off_bb = P * 64
-        off_plan = (off_bb + 16 + 255) // 256 * 256
+        off_plan = (off_bb + 4 * BBOX_SLOTS * 4 + 255) // 256 * 256
         res = self._get("result", (off_plan + int(lib.pano_plan_device_bytes()),), T.uint8)
         # canvas capacity: every step pads by at most one frame width (|dx| <= w for real
         # overlaps) and the drift-corrected rows stay within one frame height; a plan above
@@ -303,7 +306,7 @@ class Stitcher:
                                                 Hcap, Wcap, ptr(res[off_plan:])))
             self.ctx.check(lib.pano_composite_planned(c, ptr(cyl), ptr(colnz), n, h, w,
                                                       ptr(res[off_plan:]), ptr(canvas), Hcap, Wcap, 0,
-                                                      ptr(res[off_bb:off_bb + 16])))
+                                                      ptr(res[off_bb:off_plan])))
             # the records, crop box and plan header to pinned host memory: the one host read
             self.ctx.check(lib.pano_copy_async(c, _lib._P(pin.data_ptr()), ptr(res), nhead))
             return cyl, colnz
@@ -366,7 +369,8 @@ class Stitcher:
                 shifts, best_pairs = self._shifts(recs)
                 H, W = int(hdr[1]), int(hdr[2])
                 view = canvas.as_strided((H, W, 3), (W * 3, 3, 1))
-                bb = head[off_bb:off_bb + 16].view(np.int32)
+                slots = head[off_bb:off_bb + 16 * BBOX_SLOTS].view(np.int32).reshape(BBOX_SLOTS, 4)
+                bb = (slots[:, 0].min(), slots[:, 1].max(), slots[:, 2].min(), slots[:, 3].max())
                 return self._crop(view, bb, margin, shifts, best_pairs, recs, t, t0)
             # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
             return self._finish(cyl, colnz, recs, margin, graph, t, t0)
