@@ -22,8 +22,10 @@ CLASSES = [
     (r"^(pair_shifts|pair_compact|pair_votes|pair_select)", "pair_shifts"),
     (r"^(composite|plan_device)", "composite_step"),
     (r"^(bbox_|gray_bbox)", "gray_bbox"),
-    (r"^cyl_scatter", "cyl_scatter"),
-    (r"^cyl_gather", "cyl_gather"),
+    # timing-class names of _lib.KERNELS: the inverse-map pair (cyl_columns, cyl_inverse)
+    # fills the slots the scatter pair (cyl_scatter, cyl_gather) named first
+    (r"^(cyl_scatter|cyl_columns)", "cyl_scatter"),
+    (r"^(cyl_gather|cyl_inverse)", "cyl_gather"),
 ]
 
 
@@ -47,8 +49,8 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
         rows += list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    # skip the first stitch: everything before the second cyl_scatter dispatch
-    starts = [i for i, r in enumerate(rows) if "cyl_scatter" in r["Kernel_Name"]]
+    # skip the first stitch: everything before the second projection dispatch
+    starts = [i for i, r in enumerate(rows) if cls(r["Kernel_Name"]) == "cyl_scatter"]
     for r in rows[starts[1] if len(starts) > 1 else 0:]:
         k = cls(r["Kernel_Name"])
         if k is None:
