@@ -70,7 +70,9 @@ typedef struct pano_pair_rec {
     int32_t n_matches;         /* matches passing the descriptor threshold               */
     int32_t votes;             /* inliers of the winner                                  */
     int32_t best;              /* index of the winning match in match order, -1 if none  */
-    int32_t status;            /* PANO_OK or PANO_E_NOMATCH                              */
+    int32_t status;            /* PANO_OK, PANO_E_NOMATCH, or PANO_E_OVERFLOW (a frame of
+                                  the pair has more keypoints than the capacity: rerun
+                                  with a larger cap -- its count is in d_counts)          */
 } pano_pair_rec;
 
 /* Placement of one compositing step in the final canvas (computed on the host from the
@@ -91,6 +93,10 @@ int pano_ctx_set_stream(pano_ctx *ctx, void *hip_stream);
 int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap);
 int pano_sync(pano_ctx *ctx);
 const char *pano_last_error(pano_ctx *ctx);
+/* Scratch generation: incremented whenever the context frees and re-allocates scratch
+ * (a call needing more than it has).  A hipGraph captured (pano_graph_begin/end) under an
+ * older generation references freed scratch and must be re-captured, not replayed. */
+uint64_t pano_ctx_generation(pano_ctx *ctx);
 const char *pano_version(void);
 void pano_sift_default_params(pano_sift_params *p);
 /* Host-only helpers (no GPU): the scalar plan of S1/S2 and the f32 Gaussian taps. */
@@ -202,8 +208,9 @@ int pano_composite_sequential(pano_ctx *ctx, const uint8_t *d_frames, const uint
  * correction and pano_plan_composite's geometry, and writes a plan of pano_plan_device_bytes()
  * bytes to d_plan; pano_composite_planned then composites into d_canvas, a buffer of
  * Hcap x Wcap x 3 bytes laid out as [H][W][3] with the planned H, W.  The plan starts with
- * int32 {status, H, W, n, first_x, first_y}: status PANO_OK, PANO_E_NOMATCH (a pair had
- * no match: the reference fails there), or PANO_E_OVERFLOW (canvas above the capacity or a
+ * int32 {status, H, W, n, first_x, first_y}: status PANO_OK, PANO_E_NOMATCH (a pair record
+ * is not PANO_OK: no match -- the reference fails there -- or a keypoint-capacity overflow,
+ * which the record's own status tells apart), or PANO_E_OVERFLOW (canvas above the capacity or a
  * column covered by three frames: use pano_plan_composite + pano_composite_bbox instead).
  * d_bbox: PANO_BBOX_SLOTS (64) partial boxes {ymin, ymax, xmin, xmax} (int32[256]); the
  * crop box is their elementwise min / max, with ymax < 0 when no pixel passed the threshold

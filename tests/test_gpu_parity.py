@@ -510,3 +510,103 @@ def test_device_plan_matches_host_plan(gpu, method, setname, gold_json):
     assert np.array_equal(res.panorama.cpu().numpy(), h_pano)
     assert digest(h_pano) == gold_json(f"{method}_{setname}.json")["pano_digest"]
     st.release_graphs()
+
+
+# ------------------------------------------------------------------ Lowe ratio (north_star M1)
+@pytest.mark.parametrize("ratio", [0.7, 0.8])
+def test_lowe_ratio_filter_vs_exact_knn2(gpu, gold_npz, ratio):
+    """pano_match (kNN-2: d1, d2) + pano_pair_shifts with ratio > 0 on the reference's own
+    prtn00 / prtn01 keypoints and descriptors, against the oracle's exact brute-force kNN-2:
+    match i is kept iff d1 < desc_thresh and m.distance < ratio * n.distance
+    (sift_visualizeUI.py:252-257 on exact -- not FLANN -- neighbours; the kernel compares the
+    squared distances, d1 < ratio^2 d2, which is the same decision for these exact integer
+    distances), and the translation vote runs on the survivors."""
+    import torch
+    from vfx_image_stitching_amd import _lib
+    g = gold_npz("sift_pair.npz")
+    dA = g["prtn00_desc"].astype(np.float32)
+    dB = g["prtn01_desc"].astype(np.float32)
+    cap = 2048
+    d = np.zeros((2, cap, 128), np.float32)
+    d[0, :len(dA)], d[1, :len(dB)] = dA, dB
+    kp = np.zeros((2, cap), _lib.KP_NP)
+    for f, name in enumerate(("prtn00", "prtn01")):
+        n = len(g[f"{name}_kp_x"])
+        for k in ("x", "y", "size", "angle", "response", "octave"):
+            kp[f, :n][k] = g[f"{name}_kp_{k}"]
+    ctx = gpu
+    desc = torch.from_numpy(d).cuda()
+    kps = torch.from_numpy(kp.view(np.int32).reshape(2, cap, 6).copy()).cuda()
+    counts = torch.tensor([len(dA), len(dB)], dtype=torch.int32).cuda()
+    best = torch.empty((1, cap), dtype=torch.int32).cuda()
+    d1 = torch.empty((1, cap)).cuda()
+    d2 = torch.empty((1, cap)).cuda()
+    recs = torch.empty((1, 64), dtype=torch.uint8).cuda()
+    hp = np.array([0, 1], np.int32)
+    ctx.check(ctx.lib.pano_match(ctx.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), 1, 2,
+                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2)))
+    ctx.check(ctx.lib.pano_pair_shifts(ctx.h, _lib.ptr(kps), None, _lib.ptr(counts), cap, _lib.i32p(hp), 1,
+                                       _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2), 25000.0, ratio, 3.0,
+                                       _lib.ptr(recs)))
+    r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
+    # oracle: exact kNN-2 over the full distance matrix (exact integers in f64)
+    A, B = dA.astype(np.float64), dB.astype(np.float64)
+    full = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2 * A @ B.T
+    order = np.argsort(full, axis=1, kind="stable")
+    m1, m2 = full[np.arange(len(A)), order[:, 0]], full[np.arange(len(A)), order[:, 1]]
+    keep = (m1 < 25000) & (np.sqrt(m1) < ratio * np.sqrt(m2))
+    assert np.array_equal(keep, (m1 < 25000) & (m1 < ratio * ratio * m2))
+    matches = [((float(kp[0, i]["x"]), float(kp[0, i]["y"])),
+                (float(kp[1, order[i, 0]]["x"]), float(kp[1, order[i, 0]]["y"])))
+               for i in np.nonzero(keep)[0]]
+    move, pair = ostitch.ransac(matches, 3)
+    assert r["status"] == _lib.PANO_OK and r["n_matches"] == len(matches)
+    assert (r["dx"], r["dy"]) == tuple(move)
+    assert ((r["xA"], r["yA"]), (r["xB"], r["yB"])) == pair
+    if ratio == 0.7:
+        assert len(matches) == 86                         # SURVEY 8(a) M1: both filters: 86
+
+
+# ------------------------------------------------------------------ config 5 at full size
+def test_synthetic_1080p_vs_oracle_golden(gpu, gold_json, gold_npz):
+    """BASELINE config 5 frame size (1920 x 1080, ~25k keypoints per frame) against the
+    oracle's golden for frames 0..2 (tests/golden/make_golden_1080p.py): cylindrical digest,
+    every keypoint (the _compare_features bars), every 4th descriptor row, the full
+    descriptor digest where no angle flipped, and both pairs' match count and ransac move."""
+    from vfx_image_stitching_amd import _lib, data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    meta = gold_json("synthetic_1080p.json")
+    z = gold_npz("synthetic_1080p.npz")
+    nf = meta["frames"]
+    frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920, start=0, count=nf)
+    st = Stitcher("sift", cap=32768)
+    cyl, _ = st.cylindrical(st.upload(frames), focals)
+    cyl_h = cyl.cpu().numpy()
+    kps, desc, counts = st.features(cyl)
+    n = counts.cpu().numpy()
+    sub = meta["sub"]
+    for i in range(nf):
+        pf = meta["per_frame"][i]
+        assert digest(cyl_h[i]) == pf["cyl_digest"]
+        assert n[i] == pf["count"], (i, n[i], pf["count"])
+        rec = kps[i, :n[i]].cpu().numpy().view(_lib.KP_NP).reshape(-1)
+        d = desc[i, :n[i]].cpu().numpy()
+        g = {k: z[f"f{i}_{k}"] for k in ("x", "y", "size", "angle", "response", "octave")}
+        sel = np.arange(0, n[i], sub)
+        gsub = {k: v[sel] for k, v in g.items()}
+        # keypoint table in full (exact fields, size ulp, angle-flip bar), descriptors on the
+        # stored rows
+        for k in ("x", "y", "response", "octave"):
+            np.testing.assert_array_equal(rec[k], g[k].astype(rec[k].dtype), err_msg=k)
+        np.testing.assert_allclose(rec["size"], g["size"], rtol=3e-7, atol=0)
+        da = np.abs(rec["angle"].astype(np.float64) - g["angle"])
+        da = np.minimum(da, 360 - da)
+        assert (da > 2e-3).mean() <= 1e-3 and da.max() < 1.0
+        _compare_features(rec[sel], d[sel], gsub, z[f"f{i}_desc_sub"])
+    recs, _ = st.pair_records((kps, desc, counts), [(i, i + 1) for i in range(nf - 1)])
+    r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)
+    for p, want in enumerate(meta["pairs"]):
+        assert r[p]["status"] == _lib.PANO_OK
+        assert abs(int(r[p]["n_matches"]) - want["n_matches"]) <= max(2, want["n_matches"] // 1000)
+        assert abs(r[p]["dx"] - want["move"][0]) <= 1e-3 and abs(r[p]["dy"] - want["move"][1]) <= 1e-3, \
+            (p, r[p], want)

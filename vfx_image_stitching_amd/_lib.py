@@ -87,6 +87,7 @@ SIGNATURES = {
     "pano_ctx_reserve": (_I, [_P, _I, _I, _I, _I]),
     "pano_sync": (_I, [_P]),
     "pano_last_error": (ctypes.c_char_p, [_P]),
+    "pano_ctx_generation": (ctypes.c_uint64, [_P]),
     "pano_version": (ctypes.c_char_p, []),
     "pano_sift_default_params": (None, [ctypes.POINTER(SiftParams)]),
     "pano_sift_plan": (_I, [ctypes.POINTER(SiftParams), _I, _I, _PI32, _PI32, _PD, _PD]),
@@ -187,6 +188,11 @@ class Context:
 
     def sync(self):
         self.check(self.lib.pano_sync(self.h))
+
+    def generation(self) -> int:
+        """Scratch generation (include/pano.h): changes when the context re-allocates scratch,
+        which invalidates every hipGraph captured before."""
+        return int(self.lib.pano_ctx_generation(self.h))
 
     def prof_enable(self, kernel):
         k = kernel if isinstance(kernel, int) else (K_ALL if kernel == "all" else KERNELS.index(kernel))

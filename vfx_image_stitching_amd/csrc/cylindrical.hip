@@ -79,7 +79,10 @@ cyl_columns(int w, FocalArg focal, int2 *__restrict__ cols, uint8_t *__restrict_
     // inverse images of k -+ 1/2 (arguments kept inside the atan range; clamped to the frame)
     const double lim = 1.5707963267948966 - 1e-12;
     const double ta = fmax(fmin((k - 0.5) / fl, lim), -lim), tb = fmax(fmin((k + 0.5) / fl, lim), -lim);
-    const double a = fmax(fl * tan(ta), -cx - 2.0), b = fmin(fl * tan(tb), (double)(w - cx + 1));
+    // both ends clamped to the frame's column range before the integer conversion (near the
+    // atan limit fl * tan() reaches ~fl * 1e12, outside int)
+    const double lo_c = -cx - 2.0, hi_c = (double)(w - cx + 1);
+    const double a = fmin(fmax(fl * tan(ta), lo_c), hi_c), b = fmin(fmax(fl * tan(tb), lo_c), hi_c);
     const int c0 = (int)floor(a) - 1, c1 = (int)ceil(b) + 1;
     int lo = 1, hi = 0;
     for (int xd = c0; xd <= c1; ++xd) {

@@ -36,6 +36,7 @@ int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need) {
         (void)hipFree(*p);
         *p = nullptr;
         *have = 0;
+        ++ctx->generation;               // graphs captured before this point are stale
     }
     size_t sz = need + need / 4 + 4096;
     hipError_t e = hipMalloc(p, sz);
@@ -136,6 +137,8 @@ int pano_sync(pano_ctx *ctx) {
 }
 
 const char *pano_last_error(pano_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+uint64_t pano_ctx_generation(pano_ctx *ctx) { return ctx ? ctx->generation : 0; }
 
 int pano_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
                      const double *focal, uint8_t *colnz) {

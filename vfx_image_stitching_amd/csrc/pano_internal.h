@@ -106,6 +106,9 @@ struct pano_ctx {
     // ---- hipGraph capture (pano_graph_begin / end)
     bool capturing = false;
     size_t cap_prof_start = 0;           // first profiler event of the capture
+    // bumped whenever scratch is freed and re-allocated (pano_grow): a graph captured under
+    // an older generation holds dangling scratch pointers (pano_ctx_generation)
+    uint64_t generation = 1;
     // ---- live profiler
     ProfState prof;
 };

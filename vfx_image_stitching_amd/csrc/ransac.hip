@@ -157,7 +157,8 @@ pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount
 }
 
 __global__ void __launch_bounds__(RB)
-pair_select(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy, int cap, PairArg pairs,
+pair_select(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
+            const int32_t *__restrict__ counts, int cap, PairArg pairs,
             const int32_t *__restrict__ best, const double2 *__restrict__ moves,
             const int32_t *__restrict__ midx, const int32_t *__restrict__ kcount,
             const int32_t *__restrict__ votes, pano_pair_rec *__restrict__ recs) {
@@ -170,6 +171,18 @@ pair_select(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy, int
     const int32_t *mi = midx + (size_t)p * cap;
     pano_pair_rec r{};
     r.n_matches = K;
+    // a frame with more keypoints than the capacity (count > cap) or whose keypoint stages
+    // overflowed (count -1) was matched on a truncated set: the pair's result is not the
+    // reference's, so the record says so instead of carrying a silently different shift
+    const int ca = counts[fa], cb = counts[fb];
+    if (ca < 0 || cb < 0 || ca > cap || cb > cap) {
+        if (tid == 0) {
+            r.best = -1;
+            r.status = PANO_E_OVERFLOW;
+            recs[p] = r;
+        }
+        return;
+    }
     if (K == 0) {
         if (tid == 0) {
             r.best = -1;
@@ -273,7 +286,7 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
         PANO_LAUNCH_CHECK(ctx, "pair_votes");
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
-            pair_select<<<np, RB, 0, ctx->stream>>>(kps, xy_i32, cap, pa, best + o, moves + o, midx + o,
+            pair_select<<<np, RB, 0, ctx->stream>>>(kps, xy_i32, counts, cap, pa, best + o, moves + o, midx + o,
                                                    kcount + p0, votes + o, recs + p0);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_select");

@@ -690,7 +690,10 @@ emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cn
         }
         ++pos;
     }
-    if (tid == 1023) counts[f] = scan[1023];
+    if (tid == 1023) {
+        counts[f] = scan[1023];                  // the true count, even above cap
+        if (scan[1023] > cap) err[0] = PANO_E_OVERFLOW;   // keypoints past cap were dropped
+    }
 }
 
 // ------------------------------------------------------------------ S9

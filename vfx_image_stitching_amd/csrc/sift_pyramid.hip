@@ -631,11 +631,8 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
     ctx->n_lvl = nl;
     const size_t need = (goff + doff) * sizeof(float);
     if (need > ctx->pyr_bytes) {
-        if (ctx->pyr) (void)hipFree(ctx->pyr);
-        ctx->pyr = nullptr;
-        ctx->pyr_bytes = 0;
-        PANO_HIP(ctx, hipMalloc((void **)&ctx->pyr, need));
-        ctx->pyr_bytes = need;
+        const int rc = pano_grow(ctx, (void **)&ctx->pyr, &ctx->pyr_bytes, need);
+        if (rc) return rc;
     }
     ctx->dog = ctx->pyr + goff;
     ctx->n = n;

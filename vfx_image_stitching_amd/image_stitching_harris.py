@@ -62,7 +62,8 @@ def compute_shift_harris(imgA, imgB, ransac_thr, desc_thresh):
     st = _stitcher(200)
     st.ransac_thr = float(ransac_thr)
     st.desc_thresh = float(desc_thresh)
-    feats = st.features(st.upload(np.stack([np.asarray(imgA, np.uint8), np.asarray(imgB, np.uint8)])))
+    # frames may differ in shape (each frame's corners are its own: :277-278)
+    feats = st.features_of([np.asarray(imgA, np.uint8), np.asarray(imgB, np.uint8)])
     recs, _ = st.pair_records(feats, [(0, 1)])
     r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
     if r["status"] != _lib.PANO_OK:

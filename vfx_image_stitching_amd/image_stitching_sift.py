@@ -17,16 +17,17 @@ from .stitching import run_panorama as _run
 
 
 def compute_shift_sift(imgA, imgB, ransac_thr=3, desc_thresh=25000):
+    """Frames may differ in shape: the reference extracts each frame's features on its own
+    (image_stitching_sift.py:59-60); so does features_of."""
     from .sift_impl import _as_bgr_u8, _stitcher
-    a, b = _as_bgr_u8(imgA), _as_bgr_u8(imgB)
-    if a.shape != b.shape:
-        raise ValueError("compute_shift_sift: frames must have the same shape (run_panorama pads)")
     st = _stitcher(1.6, 3, 0.5, 5)
     st.ransac_thr = float(ransac_thr)
     st.desc_thresh = float(desc_thresh)
-    feats = st.features(st.upload(np.stack([a, b])))
+    feats = st.features_of([_as_bgr_u8(imgA), _as_bgr_u8(imgB)])
     recs, _ = st.pair_records(feats, [(0, 1)])
     r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
+    if r["status"] == _lib.PANO_E_OVERFLOW:
+        raise _lib.PanoError(_lib.PANO_E_OVERFLOW, "keypoint capacity exceeded")
     if r["status"] != _lib.PANO_OK:
         return (0, 0), None
     return (float(r["dx"]), float(r["dy"])), ((float(r["xA"]), float(r["yA"])),

@@ -91,6 +91,9 @@ class Stitcher:
     def _get(self, name, shape, dtype):
         t = self._buf.get(name)
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            if t is not None and self._graphs:
+                # captured graphs hold the old buffer's address: re-capture, never replay them
+                self.release_graphs()
             t = self.torch.empty(shape, dtype=dtype, device=self.device)
             self._buf[name] = t
         return t
@@ -129,6 +132,42 @@ class Stitcher:
         self.ctx.check(self.ctx.lib.pano_harris(self.ctx.h, ptr(frames_dev), n, h, w,
                                                 self.max_points, ptr(xy), ptr(desc), ptr(counts)))
         return xy, desc, counts
+
+    def features_fit(self, frames_dev):
+        """features() with the SIFT keypoint capacity grown until every frame's keypoints
+        fit (the reference has no limit; one host read of the counts per call)."""
+        while True:
+            feats = self.features(frames_dev)
+            if self.method != "sift":
+                return feats
+            c = feats[2].cpu().numpy()
+            if (c < 0).any():
+                raise PanoError(_lib.PANO_E_OVERFLOW, "SIFT extrema exceeded the internal capacity")
+            if c.max(initial=0) <= self.cap:
+                return feats
+            self.cap = 1 << int(np.ceil(np.log2(int(c.max()))))
+
+    def features_of(self, images):
+        """Features of host frames that may differ in shape (the reference computes each
+        frame on its own: image_stitching_sift.py:59-60): equal shapes run as one batch,
+        otherwise frame by frame, gathered into one [n][cap] feature set for pair_records."""
+        T = self.torch
+        imgs = [np.ascontiguousarray(i, np.uint8) for i in images]
+        if len({i.shape for i in imgs}) == 1:
+            return self.features_fit(self.upload(np.stack(imgs)))
+        parts = []
+        for img in imgs:
+            pts, desc, counts = self.features_fit(self.upload(img[None]))
+            parts.append((pts.clone(), desc.clone(), counts.clone()))
+        cap = max(p[1].shape[1] for p in parts)
+        n = len(parts)
+        pts = T.zeros((n, cap) + tuple(parts[0][0].shape[2:]), dtype=parts[0][0].dtype, device=self.device)
+        desc = T.zeros((n, cap, 128), dtype=T.float32, device=self.device)
+        counts = T.cat([p[2] for p in parts])
+        for i, (p, d, _) in enumerate(parts):
+            pts[i, :p.shape[1]] = p[0]
+            desc[i, :d.shape[1]] = d[0]
+        return pts, desc, counts
 
     def pair_records(self, feats, pairs, out=None):
         T = self.torch
@@ -214,7 +253,7 @@ class Stitcher:
             with T.cuda.stream(self._gstream):
                 self.ctx.bind_stream()
                 dbg = os.environ.get("PANO_DEBUG_SYNC") == "1"
-                ent = self._graphs.get(key)
+                ent = self._graph_entry(key)
                 if ent is None:
                     fn()
                     if dbg:
@@ -231,10 +270,9 @@ class Stitcher:
                         raise
                     g = self.ctx.graph_end()
                     if len(self._graphs) >= 16:
-                        old = next(iter(self._graphs))
-                        self._fast = None
-                        self.ctx.graph_destroy(self._graphs.pop(old)[0])
-                    ent = self._graphs[key] = (g, out)
+                        self._drop_graph(next(iter(self._graphs)))
+                    # the scratch generation the graph's pointers belong to (pano_ctx_generation)
+                    ent = self._graphs[key] = (g, out, self.ctx.generation())
                 self.ctx.graph_launch(ent[0])
                 self.last_graphs.append(ent[0])
                 if dbg:
@@ -245,10 +283,26 @@ class Stitcher:
             self.ctx.bind_stream()
         return ent[1]
 
+    def _graph_entry(self, key):
+        """The cached graph of key if it is still valid: a graph captured before the context
+        re-allocated its scratch (another call needed more, on this or another Stitcher of
+        the same device) references freed memory and is dropped here, to be re-captured."""
+        ent = self._graphs.get(key)
+        if ent is not None and ent[2] != self.ctx.generation():
+            self._drop_graph(key)
+            ent = None
+        return ent
+
+    def _drop_graph(self, key):
+        g = self._graphs.pop(key)[0]
+        if self._fast is not None and self._fast[1][0] is g:
+            self._fast = None
+        self.ctx.graph_destroy(g)
+
     def release_graphs(self):
         self._fast = None
-        for g, _ in self._graphs.values():
-            self.ctx.graph_destroy(g)
+        for ent in self._graphs.values():
+            self.ctx.graph_destroy(ent[0])
         self._graphs.clear()
 
     def records(self, frames_dev, focals, graph: bool = False):
@@ -316,14 +370,14 @@ class Stitcher:
             tuple(float(f) for f in np.asarray(focals, np.float64)), self.method, self.match,
             bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh,
             self.ratio, res.data_ptr(), canvas.data_ptr())
-        ent = self._graphs.get(key) if self._graph_mode else None
+        ent = self._graph_entry(key) if self._graph_mode else None
         if ent is not None:       # replay on the caller's stream and wait: one library call
             cur = T.cuda.current_stream(self.device).cuda_stream
             self.ctx.check(lib.pano_graph_launch_sync(c, ent[0], _lib._P(cur)))
             self.last_graphs.append(ent[0])
             cyl, colnz = ent[1]
             # the next identical call skips all of the above (run()'s fast path)
-            self._fast = (self._fast_key, (ent[0], cyl, colnz, off_bb, off_plan, nhead, canvas))
+            self._fast = (self._fast_key, (ent[0], cyl, colnz, off_bb, off_plan, nhead, canvas, ent[2]))
         elif self._graph_mode:
             cyl, colnz = self._replay(key, seg)
             T.cuda.current_stream(self.device).synchronize()
@@ -338,7 +392,37 @@ class Stitcher:
             graph: bool = False, device_plan: bool = True) -> StitchResult:
         """run_panorama's numeric body.  device_plan (default): one launch chain and one host
         read per stitch; the host-planned form (two reads) runs when the plan reports a
-        canvas above capacity or a column covered by three frames, or with device_plan=False."""
+        canvas above capacity or a column covered by three frames, or with device_plan=False.
+
+        The reference has no keypoint limit: a frame with more keypoints than the capacity
+        (the pair records say PANO_E_OVERFLOW) re-runs the stitch once with the capacity grown
+        to fit, and the Stitcher keeps the larger capacity.  The returned panorama and canvas
+        are views of buffers the next run() on this Stitcher reuses: clone them to keep them."""
+        try:
+            return self._run(frames_dev, focals, margin, graph, device_plan)
+        except PanoError as e:
+            if e.code != _lib.PANO_E_OVERFLOW or self.method != "sift":
+                raise
+            need = self.grown_cap()
+            if need is None:
+                raise
+            self.cap = need
+            self.release_graphs()
+            return self._run(frames_dev, focals, margin, graph, device_plan)
+
+    def grown_cap(self):
+        """The capacity the last SIFT features call needed (power of two >= the largest frame
+        count), or None when no count exceeded the capacity (an internal-stage overflow, which
+        a larger keypoint capacity does not fix)."""
+        counts = self._buf.get("counts")
+        if counts is None:
+            return None
+        c = counts.cpu().numpy()
+        if (c < 0).any() or c.max() <= self.cap:
+            return None
+        return 1 << int(np.ceil(np.log2(int(c.max()))))
+
+    def _run(self, frames_dev, focals, margin, graph, device_plan):
         t = {}
         tick = time.perf_counter
         t0 = tick()
@@ -348,11 +432,12 @@ class Stitcher:
             self._graph_mode = graph
             # replay fast path: same frames buffer, focals and settings as the last replay
             fk = (frames_dev.data_ptr(), tuple(frames_dev.shape),
-                  np.asarray(focals, np.float64).tobytes(), self.canvas_cap, self.match, self.ratio,
-                  self.desc_thresh, self.ransac_thr, bytes(self.params)) if graph else None
+                  np.asarray(focals, np.float64).tobytes(), self.canvas_cap, self.method, self.match,
+                  self.ratio, self.desc_thresh, self.ransac_thr, bytes(self.params), self.cap,
+                  self.max_points) if graph else None
             fast = self._fast
-            if fast is not None and fast[0] == fk:
-                g, cyl, colnz, off_bb, off_plan, nhead, canvas = fast[1]
+            if fast is not None and fast[0] == fk and fast[1][7] == self.ctx.generation():
+                g, cyl, colnz, off_bb, off_plan, nhead, canvas, _ = fast[1]
                 cur = self.torch.cuda.current_stream(self.device).cuda_stream
                 self.ctx.check(self.ctx.lib.pano_graph_launch_sync(self.ctx.h, g, _lib._P(cur)))
                 self.last_graphs.append(g)
@@ -363,6 +448,7 @@ class Stitcher:
             recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1).copy()
             hdr = head[off_plan:off_plan + 32].view(np.int32)
             t["features_match_ransac"] = tick() - t0
+            self._check_records(recs)
             if hdr[0] == _lib.PANO_E_NOMATCH:
                 raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
             if hdr[0] == _lib.PANO_OK:
@@ -377,7 +463,15 @@ class Stitcher:
         cyl, colnz, recs_dev = self.records(frames_dev, focals, graph)
         recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)   # sync point 1
         t["features_match_ransac"] = tick() - t0
+        self._check_records(recs)
         return self._finish(cyl, colnz, recs, margin, graph, t, t0)
+
+    @staticmethod
+    def _check_records(recs):
+        bad = np.nonzero(recs["status"] == _lib.PANO_E_OVERFLOW)[0]
+        if len(bad):
+            raise PanoError(_lib.PANO_E_OVERFLOW,
+                            f"pairs {bad.tolist()}: a frame has more keypoints than the capacity")
 
     def _shifts(self, recs):
         """Per-pair moves and best pairs as the reference's Python values: floats of the

@@ -22,12 +22,13 @@ _stitchers: dict = {}
 _last_pyramid: dict = {}
 
 
-def _stitcher(sigma, num_intervals, assumed_blur, border, cap=4096):
+def _stitcher(sigma, num_intervals, assumed_blur, border):
+    """One Stitcher per parameter set; its keypoint capacity grows on demand (features_fit)."""
     from .pipeline import Stitcher
-    key = (sigma, num_intervals, assumed_blur, border, cap)
+    key = (sigma, num_intervals, assumed_blur, border)
     st = _stitchers.get(key)
     if st is None:
-        st = Stitcher("sift", cap=cap, sift_params=dict(
+        st = Stitcher("sift", cap=4096, sift_params=dict(
             sigma=sigma, num_intervals=num_intervals, assumed_blur=assumed_blur, border=border))
         _stitchers[key] = st
     return st
@@ -51,17 +52,9 @@ def _as_bgr_u8(image) -> np.ndarray:
 def compute_keypoints_and_descriptors(image, sigma=1.6, num_intervals=3, assumed_blur=0.5,
                                       image_border_width=5):
     bgr = _as_bgr_u8(image)
-    cap = 4096
-    while True:
-        st = _stitcher(sigma, num_intervals, assumed_blur, image_border_width, cap)
-        dev = st.upload(bgr[None])
-        kps, desc, counts = st.features(dev)
-        n = int(counts.cpu()[0])
-        if n < 0:
-            raise _lib.PanoError(_lib.PANO_E_OVERFLOW, "more raw keypoints than the sort capacity")
-        if n <= cap:
-            break
-        cap = 1 << int(np.ceil(np.log2(n)))
+    st = _stitcher(sigma, num_intervals, assumed_blur, image_border_width)
+    kps, desc, counts = st.features_fit(st.upload(bgr[None]))
+    n = int(counts.cpu()[0])
     st.ctx.sync()
     rec = kps[0, :n].cpu().numpy().view(_lib.KP_NP).reshape(-1)
     d = desc[0, :n].cpu().numpy().astype(np.float32)
