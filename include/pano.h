@@ -120,6 +120,13 @@ int pano_sift(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
               const pano_sift_params *params, pano_kp *d_kps, float *d_desc, int cap,
               int32_t *d_counts);
 
+/* pano_sift with the descriptors as bytes (the batched Stitcher's form, what the distance GEMM
+ * reads): d_desc_u8 [n][cap][128] uint8 (the same integer values) and d_norms [n][cap] int32
+ * squared norms (exact).  A quarter of the f32 form's bytes; no repacking before matching. */
+int pano_sift_u8(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
+                 const pano_sift_params *params, pano_kp *d_kps, uint8_t *d_desc_u8,
+                 int32_t *d_norms, int cap, int32_t *d_counts);
+
 /* Stage access for the GUI-facing stage functions (sift_impl.py:45-111):
  * after pano_sift_pyramid the Gaussian / DoG pyramid of frame `frame` stays in the
  * context: level 0..num_intervals+2 (Gaussian) / 0..num_intervals+1 (DoG).  After pano_sift

@@ -129,7 +129,9 @@ def _compare_features(rec, desc, gold_rec, gold_desc):
     assert flip.mean() <= 1e-3 and da.max() < 1.0, (int(flip.sum()), float(da.max()))
     d = np.abs(desc - gold_desc.astype(np.float32))[~flip]
     if d.size:
-        assert d.max() <= 1, "descriptor element off by more than 1 LSB"
+        bad = np.nonzero(d.max(1) > 1)[0]
+        assert d.max() <= 1, ("descriptor element off by more than 1 LSB", d.max(), len(bad),
+                              np.nonzero(~flip)[0][bad[:4]].tolist())
         assert (d > 0).mean() < 1e-3, "more than 0.1 % of descriptor elements differ"
 
 

@@ -94,6 +94,7 @@ SIGNATURES = {
     "pano_sift_taps": (_I, [_D, _PD, _PI32]),
     "pano_cylindrical": (_I, [_P, _P, _P, _I, _I, _I, _PD, _P]),
     "pano_sift": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P, _P, _I, _P]),
+    "pano_sift_u8": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P, _P, _P, _I, _P]),
     "pano_sift_pyramid": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams)]),
     "pano_sift_level_shape": (_I, [_P, _I, _PI32, _PI32, _PI32]),
     "pano_sift_copy_level": (_I, [_P, _I, _I, _I, _I, _P]),

@@ -161,8 +161,21 @@ int pano_sift(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     pano_sift_params p;
     if (params) p = *params; else pano_sift_default_params(&p);
     int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
-    if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, desc, cap, counts);
+    if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, desc, nullptr, nullptr, cap, counts);
     sift_join_tail(ctx);                  // no-op unless an error left the tail unjoined
+    return rc;
+}
+
+int pano_sift_u8(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
+                 const pano_sift_params *params, pano_kp *kps, uint8_t *desc_u8, int32_t *norms,
+                 int cap, int32_t *counts) {
+    if (!ctx) return PANO_E_ARG;
+    if (!desc_u8 || !norms) return pano_fail(ctx, PANO_E_ARG, "pano_sift_u8: bad outputs");
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
+    if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, nullptr, desc_u8, norms, cap, counts);
+    sift_join_tail(ctx);
     return rc;
 }
 

@@ -17,6 +17,7 @@
 #define PANO_MAX_OCTAVES 16
 #define PANO_MAX_LEVELS 8      // num_intervals + 3 <= 8  -> num_intervals <= 5
 #define PANO_MAX_TAPS 64
+#define PANO_MAX_FRAMES 1024   // frames per pano_sift batch
 // SIFT per-frame counters: one 128-byte line each (no false sharing between frames).
 // Layout of pano_ctx::counters: [err] [cand f=0..n) [raw f] [ext f], kCntStride ints apiece.
 constexpr int kCntStride = 32;
@@ -173,8 +174,9 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
 // the top level (only its DoG is used).
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                         const pano_sift_params *p, bool defer_tail = false, bool full = true);
+// desc: f32 [n][cap][128] (drop-in form) or, when NULL, desc_u8 [n][cap][128] + norms [n][cap]
 int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
-                          int cap, int32_t *counts);
+                          uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts);
 int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int max_points,
                   int32_t *xy, float *desc, int32_t *counts);
 int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,

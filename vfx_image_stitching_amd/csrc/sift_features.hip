@@ -7,8 +7,8 @@
 //   bucket_*          compare_keypoints :299-316 (rank = sorted slot: counting sort on x)
 //   emit_keypoints    remove_duplicate_keypoints :319-327 + convert_keypoints_to_input_image_size
 //                     :333-343 (workgroup per frame)
-//   descriptor        unpack_octave :349-358 + generate_descriptors :361-526
-//                     (workgroup per keypoint)
+//   descriptor_wave   unpack_octave :349-358 + generate_descriptors :361-526
+//                     (persistent waves, one keypoint per wave at a time)
 //
 // Parity notes (DESIGN.md "Parity"):
 //  * extrema decisions are exact f32 comparisons; the cube / gradient / Hessian are the
@@ -32,7 +32,6 @@ namespace {
 constexpr float kRad2DegF32 = 180.0f / 3.14159265358979323846f;   // numpy f32 rad2deg
 constexpr double kHistScale = 1099511627776.0;                    // 2^40 fixed point
 constexpr double kHistInv = 1.0 / 1099511627776.0;
-constexpr double kDescScale = 1099511627776.0;
 
 // a / b correctly rounded from y = RN(1 / b) (Markstein): q = RN(a y) is within one ulp, the
 // remainder a - b q is exact under fma, and RN(q + r y) is the correctly rounded quotient
@@ -50,7 +49,6 @@ __device__ __forceinline__ unsigned long long rint_fix(double x) {
     const double magic = 6755399441055744.0;
     return (unsigned long long)(__double_as_longlong(x + magic) - __double_as_longlong(magic));
 }
-constexpr double kDescInv = 1.0 / 1099511627776.0;
 // Per-frame scratch capacities scale with the pyramid: raw DoG extrema <= sum(Po) / 32
 // (32768 at 512 x 384, 345k at 1080p), localised candidates and oriented keypoints <= 1/4
 // of that.  Every count is checked against its capacity (PANO_E_OVERFLOW), never clamped
@@ -747,258 +745,348 @@ __device__ __forceinline__ float sdot_skx_wave128(float lo, float hi) {
     return (float)((double)kern + 0.0);
 }
 
-// Descriptors, one WAVE per keypoint (4 keypoints per workgroup, no block barriers): the
-// wave derives, per patch column, the row interval inside the rotated square and the image
-// (conservative; `sample` applies the exact bin test), scans the interval lengths into a
-// dense sample index, and each lane walks its own run of that index, spreading into the
-// wave's 2^40 fixed-point histogram (integer sums: order independent).  The normalisation
-// is the reference's, with np.linalg.norm in OpenBLAS's sdot order across the lanes.
-constexpr int kDescCols = 256;   // patch sides up to this use the dense index
+// atan2(y, x) in units of pi/4 ("octants", (-4, 4]): octant reduction to a = min/max in
+// [0, 1] and an odd minimax polynomial of degree 15 (f32 Horner, |error| < 2.1e-7 octant).
+// The descriptor only uses the angle through the continuous trilinear weights, so a few
+// ulps here move each contribution by ~1e-7 relative -- the size of the reference's own f32
+// np.add.at rounding (sift_impl.py:499-500); atan2(0, 0) = 0 as numpy's.
+__device__ __forceinline__ float atan2_oct(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    // v_rcp_f32 flushes a subnormal argument (0 * inf = NaN): gradients that small (flat
+    // black borders of the cylindrical frames after the cascaded blurs) have magnitude 0 in
+    // f32 anyway, so their angle is taken as 0, numpy's atan2(0, 0)
+    const float a = mx >= 1.17549435e-38f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float t = a * a;
+    float p = -0.005166319198906422f;
+    p = fmaf(p, t, 0.027850419282913208f);
+    p = fmaf(p, t, -0.07120880484580994f);
+    p = fmaf(p, t, 0.1227816641330719f);
+    p = fmaf(p, t, -0.1770951747894287f);
+    p = fmaf(p, t, 0.2539685070514679f);
+    p = fmaf(p, t, -0.42436903715133667f);
+    p = fmaf(p, t, 1.2732386589050293f);
+    float r = p * a;                               // atan(a) / (pi / 4), in [0, 1]
+    r = ay > ax ? 2.0f - r : r;
+    r = x < 0.0f ? 4.0f - r : r;
+    return y < 0.0f ? -r : r;
+}
 
-__global__ void __launch_bounds__(256)
+// Descriptors, one WAVE per keypoint, persistent: waves stride over the keypoints of the
+// whole batch (no workgroups for empty capacity slots).  Per keypoint the wave derives, per
+// patch column, the row interval inside the rotated square and the image (conservative; the
+// exact bin test is per sample), scans the interval lengths into a dense sample index, and
+// each lane walks its own run of that index down patch columns (the gradient taps come from
+// a sliding window of row triples: one 12-byte load per sample, the next one in flight while
+// the current sample is binned; neighbouring lanes are Q samples apart: different cells /
+// orientations, few same-address LDS atomics).  Each sample is spread trilinearly into the
+// wave's 6 x 6 x 8 histogram (padding bins included: no bounds branches) as 2^22 fixed-point
+// u64 LDS atomics -- integer sums, deterministic and order independent (LDS f32 atomics
+// measured 5x slower on gfx950).  The normalisation is the reference's, np.linalg.norm in
+// OpenBLAS's sdot order across the lanes.
+//
+// Arithmetic (generate_descriptors :361-526): every per-sample quantity is f32.  Everything
+// the reference computes in float64 (rotation, bins, weights) enters only through continuous
+// trilinear weights: a sample moving across a bin edge hands its weight over continuously, so
+// f32 rounding moves each contribution by ~1e-7 relative -- the size of the reference's own
+// float32 np.add.at accumulation (measured on the parrington goldens: 6e-6 of the integer
+// elements 1 LSB off, vs 2e-6 for an exact-sum form; the bar is 1e-3).
+//
+// OUT_U8: the Stitcher's form -- integer descriptors as bytes [n][cap][128] plus their
+// squared norms (exact integers) [n][cap], what the distance GEMM consumes; otherwise the
+// drop-in form, f32 [n][cap][128].
+constexpr int kDescWaves = 4;         // waves (keypoints in flight) per workgroup
+constexpr int kDescCols = 128;        // patch sides up to this use the dense index (default
+                                      // parameters: side <= 73)
+constexpr int kHist = 6 * 6 * 8;      // padded histogram (reference: tensor of (ww+2, ww+2, nb))
+constexpr float kFix = 4194304.0f;    // 2^22: contributions <= 255 sqrt(2) fit a u32
+#ifndef PANO_DESC_ABL
+#define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS)
+#endif
+
+// Frame of dense keypoint index gk (frames' keypoints back to back, counts clamped to
+// [0, cap]): chunked wave scan of the counts; false when gk is past the last keypoint.
+__device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ counts, int n_frames,
+                                                int cap, int gk, int &f, int &k) {
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    for (int f0 = 0; f0 < n_frames; f0 += 64) {
+        int c = f0 + lane < n_frames ? counts[f0 + lane] : 0;
+        c = c < 0 ? 0 : (c < cap ? c : cap);
+        int incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int tot = __shfl(incl, 63);
+        if (gk < base + tot) {
+            const int j = __popcll(__ballot(base + incl <= gk));   // frames wholly before gk
+            f = f0 + j;
+            k = gk - base - (__shfl(incl, j) - __shfl(c, j));
+            return true;
+        }
+        base += tot;
+    }
+    return false;
+}
+
+template <bool OUT_U8>
+__global__ void __launch_bounds__(64 * kDescWaves, 5)
 descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
-                const int32_t *__restrict__ counts, int cap, float *__restrict__ desc) {
-    __shared__ unsigned long long acc[4][128];
-    __shared__ int col_lo[4][kDescCols], col_pre[4][kDescCols + 1];
-    __shared__ double gwt[4][kDescCols / 2 + 1];          // separable Gaussian weight by |offset|
+                const int32_t *__restrict__ counts, int n_frames, int cap, int32_t *__restrict__ work,
+                float *__restrict__ desc, uint8_t *__restrict__ desc_u8, int32_t *__restrict__ norms) {
+    __shared__ unsigned long long hist[kDescWaves][kHist];
+    __shared__ int col_lo[kDescWaves][kDescCols], col_pre[kDescWaves][kDescCols + 1];
+    __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const unsigned tb = xcd_swizzle_chunked<16>(linear_block_id(), gridDim.x * gridDim.y);
-    const int f = (int)(tb / gridDim.x);
-    const int k = (int)(tb % gridDim.x) * 4 + wv;
-    int cnt = counts[f];
-    cnt = cnt < cap ? cnt : cap;
-    if (k >= cnt) return;                                  // whole wave
-    unsigned long long *wacc = acc[wv];
-    wacc[lane] = 0ull;
-    wacc[64 + lane] = 0ull;
-    const pano_kp kp = kps[(size_t)f * cap + k];
-    int oct = kp.octave & 255;
-    if (oct >= 128) oct |= -128;
-    const int lyr = (kp.octave >> 8) & 255;
-    const float scl = oct >= 0 ? 1.0f / (float)(1 << oct) : (float)(1 << -oct);
-    const int O = oct + 1;
-    const int rows = pa.H[O], cols = pa.W[O];
-    const float *img = pa.gauss[O][lyr] + (size_t)f * rows * cols;
-    const int px = (int)rint((double)scl * (double)kp.x);
-    const int py = (int)rint((double)scl * (double)kp.y);
-    const double angle = 360.0 - (double)kp.angle;
-    const double rad = angle * (3.141592653589793 / 180.0);
-    const double cos_a = cos(rad), sin_a = sin(rad);
-    const float hw = (dp.hw_mult * scl) * kp.size;
-    const double hwd = (double)hw;
-    int half = (int)rint(hwd * 1.4142135623730951 * 5.0 * 0.5);
-    const int diag = (int)sqrt((double)(rows * rows + cols * cols));
-    half = half < diag ? half : diag;
-    const int side = 2 * half + 1;
-    const float angle_f = (float)angle;
-    const float bins_per_deg = (float)(8.0 / 360.0);
-    const double inv_hwd = 1.0 / hwd;
-    const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hwd < 2.5 with slack
-    // The reference's weight exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) has (rrot, crot) a rotation
-    // of (xs, ys), so it equals exp(-xs^2/(8hw^2)) * exp(-ys^2/(8hw^2)): one table of side/2+1
-    // entries per keypoint replaces an f64 exp per sample.  The two forms differ by a few f64
-    // ulps (~1e-15 relative), below the 2^-40 quantum of the fixed-point histogram and far
-    // below the f32 rounding of the reference's own np.add.at accumulation.
-    const bool use_tab = side <= kDescCols;
-    // gradient taps of the in-image sample (xi, yi): gx = q[1] - q[-1], gy = q[-cols] - q[cols]
-    auto taps = [&](int xi, int yi, float (&g)[4]) {
-        const float *q = img + (size_t)(py + yi - half) * cols + (px + xi - half);
-        g[0] = q[1];
-        g[1] = q[-1];
-        g[2] = q[-cols];
-        g[3] = q[cols];
-    };
-    // (x-1, x, x+1) of patch row yi at patch column xi
-    auto trip = [&](int xi, int yi, float (&T)[3]) {
-        const float *q = img + (size_t)(py + yi - half) * cols + (px + xi - half) - 1;
-        T[0] = q[0];
-        T[1] = q[1];
-        T[2] = q[2];
-    };
-    auto sample = [&](int xi, int yi, const float (&g)[4]) {
-        const int xs = xi - half, ys = yi - half;
-        const double rrot = (double)xs * sin_a + (double)ys * cos_a;
-        const double crot = (double)xs * cos_a - (double)ys * sin_a;
-        const double rq = div_rn(rrot, hwd, inv_hwd), cq = div_rn(crot, hwd, inv_hwd);
-        const double rbin = (rq + 2.0) - 0.5;
-        const double cbin = (cq + 2.0) - 0.5;
-        if (!(rbin > -1.0 && rbin < 4.0 && cbin > -1.0 && cbin < 4.0)) return;
-        const float gx = g[0] - g[1];
-        const float gy = g[2] - g[3];
-        const float mag = sqrtf(gx * gx + gy * gy);
-        const float ori = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
-        const double w = use_tab ? gwt[wv][abs(xs)] * gwt[wv][abs(ys)]
-                                 : exp(-0.125 * (rq * rq + cq * cq));
-        const double wm = (w * (double)mag) * kDescScale;   // 2^40 fixed point, exact scaling
-        const float ob = np_remainder_pos_f((ori - angle_f) * bins_per_deg, 8.0f);
-        const int r0 = (int)floor(rbin), c0 = (int)floor(cbin);
-        const int o0 = ((int)floorf(ob)) % 8;
-        const double rf = rbin - r0, cf = cbin - c0;
-        const double of = (double)ob - (double)o0;
-        const double c1 = wm * rf;
-        const double c0w = wm - c1;
-        const double part[4] = {c0w * (1 - cf), c0w * cf, c1 * (1 - cf), c1 * cf};
+    unsigned long long *h = hist[wv];
+    int *clo = col_lo[wv], *cpre = col_pre[wv];
+    float *cbr = col_br[wv], *cbc = col_bc[wv];
+    // XCD-aware split (workgroup b runs on XCD b % 8): each XCD takes one contiguous eighth of
+    // the keypoints (x-sorted per frame: neighbouring windows), its waves striding over it, so
+    // a window's pyramid rows are fetched into one XCD's L2, not eight
+    int total = 0;
+    for (int f0 = 0; f0 < n_frames; f0 += 64) {
+        int c = f0 + lane < n_frames ? counts[f0 + lane] : 0;
+        c = c < 0 ? 0 : (c < cap ? c : cap);
 #pragma unroll
-        for (int qd = 0; qd < 4; ++qd) {
-            const int rb = r0 + 1 + (qd >> 1), cb = c0 + 1 + (qd & 1);
-            if (rb < 1 || rb > 4 || cb < 1 || cb > 4) continue;
-            const int base = ((rb - 1) * 4 + (cb - 1)) * 8;
-            const double v0 = part[qd] * (1 - of);
-            const double v1 = part[qd] * of;
-            atomicAdd(&wacc[base + o0], rint_fix(v0));
-            atomicAdd(&wacc[base + ((o0 + 1) & 7)], rint_fix(v1));
-        }
-    };
-    if (use_tab) {
-        for (int a = lane; a <= half; a += 64) {
-            const double q = (double)a / hwd;
-            gwt[wv][a] = exp(-0.125 * (q * q));
-        }
-        int *clo = col_lo[wv], *cpre = col_pre[wv];
-        int run = 0;                                       // wave-wide running total
+        for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+        total += c;
+    }
+    const int xcd = blockIdx.x & 7, nx = gridDim.x >> 3;           // gridDim.x % 8 == 0
+    const int lo_k = (int)((long long)total * xcd / 8), hi_k = (int)((long long)total * (xcd + 1) / 8);
+    // dynamic: a wave takes the XCD's next keypoint from the XCD's own counter (window sizes
+    // vary ~3x; static striding left waves idle); one 128-byte line per counter
+    int32_t *wq = work + xcd * kCntStride;
+    unsigned long long abl_sink = 0;
+    (void)nx;
+    int f = 0, k = 0;
+    for (;;) {
+        int gk = 0;
+        if (lane == 0) gk = atomicAdd(wq, 1);
+        gk = lo_k + __shfl(gk, 0);
+        if (gk >= hi_k || !locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
+        for (int i = lane; i < kHist; i += 64) h[i] = 0ull;
+        const pano_kp kp = kps[(size_t)f * cap + k];
+        int oct = kp.octave & 255;
+        if (oct >= 128) oct |= -128;
+        const int lyr = (kp.octave >> 8) & 255;
+        const float scl = oct >= 0 ? 1.0f / (float)(1 << oct) : (float)(1 << -oct);
+        const int O = oct + 1;
+        const int rows = pa.H[O], cols = pa.W[O];
+        const float *img = pa.gauss[O][lyr] + (size_t)f * rows * cols;
+        const int px = (int)rint((double)scl * (double)kp.x);
+        const int py = (int)rint((double)scl * (double)kp.y);
+        const double angle = 360.0 - (double)kp.angle;
+        const double rad = angle * (3.141592653589793 / 180.0);
+        const double cos_a = cos(rad), sin_a = sin(rad);
+        const float hw = (dp.hw_mult * scl) * kp.size;
+        const double hwd = (double)hw, inv_hw = 1.0 / hwd;
+        int half = (int)rint(hwd * 1.4142135623730951 * 5.0 * 0.5);
+        const int diag = (int)sqrt((double)(rows * rows + cols * cols));
+        half = half < diag ? half : diag;
+        const int side = 2 * half + 1;
+        // ob = remainder((ori - angle) * 8 / 360, 8): one bin is one octant (45 deg), so with
+        // the gradient angle in octants ob = ori8 - angle * 8 / 360 (mod 8)
+        const float a8 = (float)(angle * (8.0 / 360.0));
+        // rbin = ys (cos / hw) + (xs sin / hw + 1.5), cbin = ys (-sin / hw) + (xs cos / hw + 1.5)
+        const double sr = sin_a * inv_hw, cr = cos_a * inv_hw;
+        const float ar = (float)cr, ac = (float)-sr;
+        auto sample = [&](float gx, float gy, float rbin, float cbin, float w) {
+            if (!(rbin > -1.0f && rbin < 4.0f && cbin > -1.0f && cbin < 4.0f)) return;
+            const float mag = __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
+            float ob = atan2_oct(gy, gx) - a8;               // (-12, 4]
+            ob = ob < 0.0f ? ob + 8.0f : ob;
+            ob = ob < 0.0f ? ob + 8.0f : ob;
+            const float wm = w * mag;
+            const float fr = floorf(rbin), fc = floorf(cbin), fo = floorf(ob);
+            const float rf = rbin - fr, cf = cbin - fc, of = ob - fo;
+            const int o0 = (int)fo & 7, o1 = (o0 + 1) & 7;
+            const int base = ((int)fr + 1) * 48 + ((int)fc + 1) * 8;   // (r0 + 1, c0 + 1) bin
+            const float c1 = wm * rf, c0w = wm - c1;
+            const float v00 = c0w * (1.0f - cf), v01 = c0w * cf, v10 = c1 * (1.0f - cf), v11 = c1 * cf;
+            const float nof = 1.0f - of;
+            auto fix = [](float v) { return (unsigned long long)(uint32_t)fmaf(v, kFix, 0.5f); };
+            unsigned long long *hA = h + base + o0, *hB = h + base + o1;
+#if PANO_DESC_ABL == 0
+            atomicAdd(hA, fix(v00 * nof));      atomicAdd(hB, fix(v00 * of));
+            atomicAdd(hA + 8, fix(v01 * nof));  atomicAdd(hB + 8, fix(v01 * of));
+            atomicAdd(hA + 48, fix(v10 * nof)); atomicAdd(hB + 48, fix(v10 * of));
+            atomicAdd(hA + 56, fix(v11 * nof)); atomicAdd(hB + 56, fix(v11 * of));
+#elif PANO_DESC_ABL == 1
+            hA[0] = fix(v00 * nof);  hB[0] = fix(v00 * of);
+            hA[8] = fix(v01 * nof);  hB[8] = fix(v01 * of);
+            hA[48] = fix(v10 * nof); hB[48] = fix(v10 * of);
+            hA[56] = fix(v11 * nof); hB[56] = fix(v11 * of);
+#else
+            abl_sink += fix(v00 * nof) + fix(v00 * of) + fix(v01 * nof) + fix(v01 * of) + fix(v10 * nof) +
+                        fix(v10 * of) + fix(v11 * nof) + fix(v11 * of) + (unsigned long long)(base + o0 + o1);
+#endif
+        };
+        if (side <= kDescCols) {
+            const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hw < 2.5 with slack
+            // |a ys + b| < lim -> ys in an interval (rrot: a = cos, b = xs sin; crot: a = -sin,
+            // b = xs cos); conservative: widened by 1e-6, so approximate quotients are fine
+            const double ia_r = fabs(cos_a) < 1e-12 ? 0.0 : 1.0 / cos_a;
+            const double ia_c = fabs(sin_a) < 1e-12 ? 0.0 : -1.0 / sin_a;
+            const float kq = (float)(-0.125 * 1.4426950408889634 * inv_hw * inv_hw);
+            int run = 0;                                   // wave-wide running total
+            for (int c4 = 0; c4 < side; c4 += 64) {
+                const int c = c4 + lane;
+                int lo = 1, hi = 0;
+                if (c < side) {
+                    const int xs = c - half, cc = px + xs;
+                    cbr[c] = (float)((double)xs * sr) + 1.5f;
+                    cbc[c] = (float)((double)xs * cr) + 1.5f;
+                    if (cc > 0 && cc < cols - 1) {
+                        lo = max(-half, 1 - py);
+                        hi = min(half, rows - 2 - py);
+                        const double bvs[2] = {xs * sin_a, xs * cos_a};
+                        const double ias[2] = {ia_r, ia_c};
 #pragma unroll
-        for (int c4 = 0; c4 < kDescCols; c4 += 64) {
-            if (c4 >= side) break;
-            const int c = c4 + lane;
-            int lo = 1, hi = 0;
-            if (c < side) {
-                const int xs = c - half, cc = px + xs;
-                if (cc > 0 && cc < cols - 1) {
-                    lo = max(-half, 1 - py);
-                    hi = min(half, rows - 2 - py);
-                    // |a ys + b| < lim  ->  ys in an interval (rrot: a = cos, b = xs sin;
-                    // crot: a = -sin, b = xs cos), widened by 1e-6 and clipped before rounding
-                    const double ab[2][2] = {{cos_a, xs * sin_a}, {-sin_a, xs * cos_a}};
-#pragma unroll
-                    for (int qd = 0; qd < 2; ++qd) {
-                        const double av = ab[qd][0], bv = ab[qd][1];
-                        if (fabs(av) < 1e-12) {
-                            if (!(fabs(bv) < lim)) hi = lo - 1;
-                            continue;
+                        for (int qd = 0; qd < 2; ++qd) {
+                            const double bv = bvs[qd], ia = ias[qd];
+                            if (ia == 0.0) {
+                                if (!(fabs(bv) < lim)) hi = lo - 1;
+                                continue;
+                            }
+                            const double t1 = (-lim - bv) * ia, t2 = (lim - bv) * ia;
+                            const double l = fmax(fmin(t1, t2) - 1e-6, -half - 1.0);
+                            const double u = fmin(fmax(t1, t2) + 1e-6, half + 1.0);
+                            lo = max(lo, (int)ceil(l));
+                            hi = min(hi, (int)floor(u));
                         }
-                        const double t1 = (-lim - bv) / av, t2 = (lim - bv) / av;
-                        const double l = fmax(fmin(t1, t2) - 1e-6, -half - 1.0);
-                        const double u = fmin(fmax(t1, t2) + 1e-6, half + 1.0);
-                        lo = max(lo, (int)ceil(l));
-                        hi = min(hi, (int)floor(u));
                     }
                 }
-            }
-            const int n_c = hi >= lo ? hi - lo + 1 : 0;
-            int incl = n_c;
+                const int n_c = hi >= lo ? hi - lo + 1 : 0;
+                int incl = n_c;
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int t = __shfl_up(incl, d);
-                if (lane >= d) incl += t;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int t = __shfl_up(incl, d);
+                    if (lane >= d) incl += t;
+                }
+                if (c < side) {
+                    clo[c] = lo;
+                    cpre[c] = run + incl - n_c;
+                }
+                run += __shfl(incl, 63);
             }
-            if (c < side) {
-                clo[c] = lo;
-                cpre[c] = run + incl - n_c;
+            if (lane == 0) cpre[side] = run;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int nsamp = run;
+            const int Q = (nsamp + 63) >> 6;
+            int t = lane * Q;
+            const int tend = min(t + Q, nsamp);
+            if (t < tend) {
+                int c = 0, c1 = side - 1;                  // largest c with cpre[c] <= t
+                while (c < c1) {
+                    const int mid = (c + c1 + 1) >> 1;
+                    if (cpre[mid] <= t) c = mid;
+                    else c1 = mid - 1;
+                }
+                int ys = clo[c] + (t - cpre[c]);
+                int yend = clo[c] + (cpre[c + 1] - cpre[c]);
+                // (x-1, x, x+1) of image row py + y at patch column cc
+                auto trip = [&](int cc, int y, float (&T)[3]) {
+                    const float *q = img + (size_t)(py + y) * cols + (px + cc - half) - 1;
+                    T[0] = q[0];
+                    T[1] = q[1];
+                    T[2] = q[2];
+                };
+                float br = cbr[c], bc = cbc[c], xs2 = (float)((c - half) * (c - half));
+                float Tm[3], T0[3], Tp[3];
+                trip(c, ys - 1, Tm);
+                trip(c, ys, T0);
+                trip(c, ys + 1, Tp);
+                for (int j = t; j < tend; ++j) {
+                    // the next sample's position (this column, or the next non-empty one),
+                    // its taps loaded while this sample is binned
+                    int cn = c, yn = ys + 1;
+                    const bool more = j + 1 < tend;
+                    const bool newcol = more && yn >= yend;
+                    if (newcol) {
+                        do { ++cn; } while (cpre[cn + 1] == cpre[cn]);
+                        yn = clo[cn];
+                    }
+                    float N0[3], N1[3], N2[3];
+                    if (newcol) {
+                        trip(cn, yn - 1, N0);
+                        trip(cn, yn, N1);
+                    }
+                    if (more) trip(cn, yn + 1, N2);
+                    const float ysf = (float)ys;
+                    // exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) = exp2(kq (xs^2 + ys^2)): a rotation
+                    // keeps the radius (no LDS read on the sample path)
+                    sample(T0[2] - T0[0], Tm[1] - Tp[1], fmaf(ysf, ar, br), fmaf(ysf, ac, bc),
+                           __builtin_amdgcn_exp2f(kq * fmaf(ysf, ysf, xs2)));
+                    if (newcol) {
+                        c = cn;
+                        yend = clo[c] + (cpre[c + 1] - cpre[c]);
+                        br = cbr[c];
+                        bc = cbc[c];
+                        xs2 = (float)((c - half) * (c - half));
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) { Tm[i] = N0[i]; T0[i] = N1[i]; Tp[i] = N2[i]; }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; Tp[i] = N2[i]; }
+                    }
+                    ys = yn;
+                }
             }
-            run += __shfl(incl, 63);
+        } else {
+            // very large patches (non-default parameters): every sample of the square
+            const int S = side * side;
+            for (int j = lane; j < S; j += 64) {
+                const int xi = j / side, yi = j - (j / side) * side;
+                const int xs = xi - half, ys = yi - half;
+                const int rr = py + ys, cc = px + xs;
+                if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
+                const double rq = ((double)xs * sin_a + (double)ys * cos_a) * inv_hw;
+                const double cq = ((double)xs * cos_a - (double)ys * sin_a) * inv_hw;
+                if (!(fabs(rq) < 2.5 + 1e-6 && fabs(cq) < 2.5 + 1e-6)) continue;
+                const float *q = img + (size_t)rr * cols + cc;
+                sample(q[1] - q[-1], q[-cols] - q[cols], (float)rq + 1.5f, (float)cq + 1.5f,
+                       (float)exp(-0.125 * (rq * rq + cq * cq)));
+            }
         }
-        if (lane == 0) cpre[side] = run;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // lane L takes the run [L Q, L Q + Q) of the dense index: one binary search, then a
-        // column-by-column walk (neighbouring lanes are Q samples apart: different cells /
-        // orientations, few same-address LDS atomics)
-        const int total = run;
-        const int Q = (total + 63) >> 6;
-        int t = lane * Q;
-        const int tend = min(t + Q, total);
-        if (t < tend) {
-            int c = 0, c1 = side - 1;                      // largest c with cpre[c] <= t
-            while (c < c1) {
-                const int mid = (c + c1 + 1) >> 1;
-                if (cpre[mid] <= t) c = mid;
-                else c1 = mid - 1;
-            }
-            int r = t - cpre[c];
-            int ncol = cpre[c + 1] - cpre[c];
-            // A lane's run walks down patch columns, so its taps come from a sliding window
-            // of three row triples (x-1, x, x+1) at rows y-1, y, y+1: one 12-byte load per
-            // sample (three at a column change) instead of four scattered dword loads -- the
-            // lanes are far apart, so every load instruction costs one L1 tag lookup per lane
-            // and the tap count, not the arithmetic, bounded this kernel.  The next sample's
-            // triple is in flight while the current one is binned.
-            while (r >= ncol) {
-                r -= ncol;
-                ++c;
-                ncol = cpre[c + 1] - cpre[c];
-            }
-            int xi = c, yi = clo[c] + r + half;
-            float Tm[3], T0[3], Tp[3];
-            trip(xi, yi - 1, Tm);
-            trip(xi, yi, T0);
-            trip(xi, yi + 1, Tp);
-            for (++t, ++r; t < tend; ++t, ++r) {
-                bool newcol = false;
-                while (r >= ncol) {
-                    r -= ncol;
-                    ++c;
-                    ncol = cpre[c + 1] - cpre[c];
-                    newcol = true;
-                }
-                const int xn = c, yn = clo[c] + r + half;
-                float N0[3], N1[3], N2[3];
-                if (newcol) {
-                    trip(xn, yn - 1, N0);
-                    trip(xn, yn, N1);
-                }
-                trip(xn, yn + 1, N2);
-                {
-                    const float g[4] = {T0[2], T0[0], Tm[1], Tp[1]};
-                    sample(xi, yi, g);
-                }
+        // crop the padding: element i = (r, c, o) of the 4 x 4 x 8 block
+        auto interior = [&](int i) {
+            const unsigned long long v = h[((i >> 5) + 1) * 48 + (((i >> 3) & 3) + 1) * 8 + (i & 7)];
+            return (float)((double)v * (1.0 / 4194304.0));
+        };
+        float lo = interior(lane), hi = interior(64 + lane);
+        if (PANO_DESC_ABL == 2) lo += (float)abl_sink;
+        const float thr = sqrtf(sdot_skx_wave128(lo, hi)) * dp.max_value;
+        lo = lo > thr ? thr : lo;
+        hi = hi > thr ? thr : hi;
+        float nv = sqrtf(sdot_skx_wave128(lo, hi));
+        if (nv < 1e-7f) nv = 1e-7f;
+        float dlo = rintf(512.0f * (lo / nv)), dhi = rintf(512.0f * (hi / nv));
+        dlo = dlo < 0.0f ? 0.0f : (dlo > 255.0f ? 255.0f : dlo);
+        dhi = dhi < 0.0f ? 0.0f : (dhi > 255.0f ? 255.0f : dhi);
+        const size_t row = (size_t)f * cap + k;
+        if constexpr (OUT_U8) {
+            desc_u8[row * PANO_DESC_DIM + lane] = (uint8_t)dlo;
+            desc_u8[row * PANO_DESC_DIM + 64 + lane] = (uint8_t)dhi;
+            int sq = (int)dlo * (int)dlo + (int)dhi * (int)dhi;
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    Tm[i] = newcol ? N0[i] : T0[i];
-                    T0[i] = newcol ? N1[i] : Tp[i];
-                    Tp[i] = N2[i];
-                }
-                xi = xn;
-                yi = yn;
-            }
-            {
-                const float g[4] = {T0[2], T0[0], Tm[1], Tp[1]};
-                sample(xi, yi, g);
-            }
+            for (int d = 32; d > 0; d >>= 1) sq += __shfl_xor(sq, d);
+            if (lane == 0) norms[row] = sq;
+        } else {
+            desc[row * PANO_DESC_DIM + lane] = dlo;
+            desc[row * PANO_DESC_DIM + 64 + lane] = dhi;
         }
-    } else {
-        // very large patches: every sample of the (side x side) square, cheap range test first
-        const int S = side * side;
-        for (int j = lane; j < S; j += 64) {
-            const int xi = j / side, yi = j - (j / side) * side;
-            const int xs = xi - half, ys = yi - half;
-            const int rr = py + ys, cc = px + xs;
-            if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
-            const double rrot = (double)xs * sin_a + (double)ys * cos_a;
-            const double crot = (double)xs * cos_a - (double)ys * sin_a;
-            if (fabs(rrot) < lim && fabs(crot) < lim) {
-                float g[4];
-                taps(xi, yi, g);
-                sample(xi, yi, g);
-            }
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();                   // h / column tables reused next
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float lo = (float)((double)(long long)wacc[lane] * kDescInv);
-    float hi = (float)((double)(long long)wacc[64 + lane] * kDescInv);
-    const float thr = sqrtf(sdot_skx_wave128(lo, hi)) * dp.max_value;
-    lo = lo > thr ? thr : lo;
-    hi = hi > thr ? thr : hi;
-    float nv = sqrtf(sdot_skx_wave128(lo, hi));
-    if (nv < 1e-7f) nv = 1e-7f;
-    float dlo = rintf(512.0f * (lo / nv)), dhi = rintf(512.0f * (hi / nv));
-    dlo = dlo < 0.0f ? 0.0f : (dlo > 255.0f ? 255.0f : dlo);
-    dhi = dhi < 0.0f ? 0.0f : (dhi > 255.0f ? 255.0f : dhi);
-    float *out = desc + ((size_t)f * cap + k) * PANO_DESC_DIM;
-    out[lane] = dlo;
-    out[64 + lane] = dhi;
 }
 
 }  // namespace
@@ -1006,9 +1094,11 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
 int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p);
 
 int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
-                          int cap, int32_t *counts) {
+                          uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts) {
     const int n = ctx->n, no = ctx->n_oct, nl = ctx->n_lvl, ni = p->num_intervals;
-    if (cap <= 0 || !kps || !desc || !counts) return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
+    if (cap <= 0 || !kps || !counts || (!desc && !(desc_u8 && norms)))
+        return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
+    if (n > PANO_MAX_FRAMES) return pano_fail(ctx, PANO_E_ARG, "pano_sift: more than PANO_MAX_FRAMES frames");
     // per-frame candidate / raw capacities, scaled with the pyramid (see kExtMin)
     size_t spo = 0;
     for (int o = 0; o < no; ++o) spo += (size_t)ctx->oct_h[o] * ctx->oct_w[o];
@@ -1022,13 +1112,15 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint32_t));
     if (rc) return rc;
     uint32_t *raw_ext = (uint32_t *)ctx->frame_off;
-    const size_t cnt_ints = (3 * (size_t)n + 1) * kCntStride;
+    // [err] [cand f] [raw f] [ext f] [descriptor work queue per XCD x 8], one line apiece
+    const size_t cnt_ints = (3 * (size_t)n + 1 + 8) * kCntStride;
     rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, cnt_ints * sizeof(int32_t));
     if (rc) return rc;
     int32_t *err = ctx->counters;
     int32_t *cand_cnt = err + kCntStride;
     int32_t *raw_cnt = cand_cnt + (size_t)n * kCntStride;
     int32_t *ext_cnt = raw_cnt + (size_t)n * kCntStride;
+    int32_t *desc_work = ext_cnt + (size_t)n * kCntStride;
     rc = launch_fill(ctx, ctx->counters, 0, cnt_ints * sizeof(int32_t));
     if (rc) return rc;
 
@@ -1148,10 +1240,27 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     }
     {
         DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
-        dim3 grid((cap + 3) / 4, n);
+        // persistent waves over the batch's keypoints: exactly the workgroups that are
+        // resident at once (a second partial round would leave the first round's CUs idle)
+        static int resident = 0;
+        if (!resident) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, descriptor_wave<true>, 64 * kDescWaves, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+                per_cu <= 0 || cus <= 0)
+                per_cu = 4, cus = 256;
+            resident = per_cu * cus;
+        }
+        const size_t slots = ((size_t)n * cap + kDescWaves - 1) / kDescWaves;
+        const unsigned blocks = (unsigned)std::min<size_t>((slots + 7) & ~size_t(7), (size_t)resident & ~size_t(7));
         {
             PanoProf prof_(ctx, PK_DESC);
-            descriptor_wave<<<grid, 256, 0, ctx->stream>>>(pa, dp, kps, counts, cap, desc);
+            if (desc_u8)
+                descriptor_wave<true><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                    pa, dp, kps, counts, n, cap, desc_work, nullptr, desc_u8, norms);
+            else
+                descriptor_wave<false><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                    pa, dp, kps, counts, n, cap, desc_work, desc, nullptr, nullptr);
         }
         PANO_LAUNCH_CHECK(ctx, "descriptor");
     }
