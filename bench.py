@@ -92,7 +92,7 @@ def parse():
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=0, help="frames of the CPU sample (0 = all)")
-    ap.add_argument("--match", default=None, choices=["f32", "bf16"])
+    ap.add_argument("--match", default=None, choices=["u8", "bf16", "f32"])
     ap.add_argument("--cap", type=int, default=0, help="keypoint capacity per frame (0 = auto)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch eagerly instead of replaying captured hipGraphs")
@@ -291,9 +291,9 @@ def main():
         pairs = [(i, i + 1) for i in range(len(cnt) - 1)]
         fl = sum(2.0 * cnt[a] * cnt[b] * 128 for a, b in pairs)
         ms = per_kernel["dist_mfma"]["total_ms"]
-        pk = MFMA_BF16_PEAK_TFLOPS if st.match == "bf16" else MFMA_F32_PEAK_TFLOPS
+        pk = MFMA_F32_PEAK_TFLOPS if st.match == "f32" else MFMA_BF16_PEAK_TFLOPS
         tf = fl / (ms * 1e-3) / 1e12
-        roof_match = {"bound": "mfma", "kernel": "dist_mfma", "dtype": st.match,
+        roof_match = {"bound": "mfma", "kernel": "dist_mfma", "dtype": "f32" if st.match == "f32" else "bf16", "descriptors": st.match,
                       "achieved": round(tf, 2), "peak": pk, "unit": "TFLOP/s",
                       "frac": round(tf / pk, 5), "flop_per_step": fl,
                       "mean_keypoints": round(float(cnt.mean()), 1),
@@ -315,7 +315,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": ("u8 frames; f32 pyramid (fp64-accumulated blur); match " +
-                  ("bf16 MFMA, exact for integer descriptors" if st.match == "bf16" else "f32 MFMA")
+                  ("f32 MFMA" if st.match == "f32" else "bf16 MFMA, exact for integer descriptors")
                   if args.method == "sift" else "u8 frames; f64 Harris response; f32 descriptors"),
         "data": "reference parrington JPEGs (packed under data/), decoded, resident in HBM"
         if args.workload != "synthetic" else "synthetic 1080p sequence (SURVEY 8d config 5)",

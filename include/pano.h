@@ -165,6 +165,15 @@ int pano_match(pano_ctx *ctx, const float *d_desc, const int32_t *d_counts, int 
                const int32_t *h_pairs, int n_pairs, int exact_int,
                int32_t *d_best, float *d_d1, float *d_d2);
 
+/* pano_match on byte descriptors (pano_sift_u8 output): d_desc_u8 [frames][cap][128] and
+ * d_norms [frames][cap] their exact squared norms.  bf16 MFMA distance GEMM with each 128-row
+ * candidate tile converted once into LDS for 256 query rows; results bit-identical to
+ * exact_int 1 / 2 (integers <= 255 exact in bf16, exact f32 accumulation).  d_d2 may be NULL
+ * (second-best not computed). */
+int pano_match_u8(pano_ctx *ctx, const uint8_t *d_desc_u8, const int32_t *d_norms,
+                  const int32_t *d_counts, int cap, const int32_t *h_pairs, int n_pairs,
+                  int32_t *d_best, float *d_d1, float *d_d2);
+
 /* ---------------------------------------------------------------- R1
  * Match filter (distance < desc_thresh, optional Lowe ratio d1 < ratio*d2 when ratio > 0;
  * d_d2 is read only then and may be NULL otherwise)

@@ -181,7 +181,26 @@ def test_sift_blank_and_tiny_inputs(gpu):
 
 
 # ------------------------------------------------------------------ M1 + R1
-@pytest.mark.parametrize("mode", [1, 2])
+def _pano_match(ctx, d, counts_h, pairs, mode, best, d1, d2):
+    """pano_match (modes 0-2, f32 descriptors) or, for mode 3, pano_match_u8 on the same
+    integer descriptors as bytes with their exact squared norms."""
+    import torch
+    from vfx_image_stitching_amd import _lib
+    hp = np.array(pairs, np.int32).reshape(-1)
+    counts = torch.tensor(counts_h, dtype=torch.int32).cuda()
+    d2p = _lib.ptr(d2) if d2 is not None else None
+    if mode == 3:
+        du8 = torch.from_numpy(d.astype(np.uint8)).cuda()
+        norms = torch.from_numpy((d.astype(np.int64) ** 2).sum(-1).astype(np.int32)).cuda()
+        ctx.check(ctx.lib.pano_match_u8(ctx.h, _lib.ptr(du8), _lib.ptr(norms), _lib.ptr(counts), d.shape[1],
+                                        _lib.i32p(hp), len(pairs), _lib.ptr(best), _lib.ptr(d1), d2p))
+    else:
+        desc = torch.from_numpy(d).cuda()
+        ctx.check(ctx.lib.pano_match(ctx.h, _lib.ptr(desc), _lib.ptr(counts), d.shape[1], _lib.i32p(hp),
+                                     len(pairs), mode, _lib.ptr(best), _lib.ptr(d1), d2p))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_match_exact_on_golden_descriptors(gpu, gold_npz, mode):
     """Feed the reference's own descriptors: NN indices and distances are exact."""
     import torch
@@ -193,15 +212,10 @@ def test_match_exact_on_golden_descriptors(gpu, gold_npz, mode):
     d = np.zeros((2, cap, 128), np.float32)
     d[0, :len(dA)] = dA
     d[1, :len(dB)] = dB
-    ctx = gpu
-    desc = torch.from_numpy(d).cuda()
-    counts = torch.tensor([len(dA), len(dB)], dtype=torch.int32).cuda()
     best = torch.empty((1, cap), dtype=torch.int32).cuda()
     d1 = torch.empty((1, cap)).cuda()
     d2 = torch.empty((1, cap)).cuda()
-    hp = np.array([0, 1], np.int32)
-    ctx.check(ctx.lib.pano_match(ctx.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), 1, mode,
-                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2)))
+    _pano_match(gpu, d, [len(dA), len(dB)], [(0, 1)], mode, best, d1, d2)
     b = best.cpu().numpy()[0][:len(dA)]
     np.testing.assert_array_equal(b, g["match_prtn00_prtn01_idx"])
     np.testing.assert_array_equal(d1.cpu().numpy()[0][:len(dA)], g["match_prtn00_prtn01_dist"].astype(np.float32))
@@ -210,31 +224,27 @@ def test_match_exact_on_golden_descriptors(gpu, gold_npz, mode):
     np.testing.assert_array_equal(d2.cpu().numpy()[0][:len(dA)], np.sort(full, axis=1)[:, 1].astype(np.float32))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_match_ties_pick_first_index(gpu, mode):
     import torch
-    from vfx_image_stitching_amd import _lib
     rng = np.random.default_rng(7)
     cap = 300
     A = rng.integers(0, 256, (cap, 128)).astype(np.float32)
     B = np.repeat(rng.integers(0, 256, (cap // 3, 128)), 3, axis=0).astype(np.float32)  # triplets
     d = np.stack([A, B])
-    desc = torch.from_numpy(d).cuda()
-    counts = torch.tensor([cap, cap], dtype=torch.int32).cuda()
     best = torch.empty((1, cap), dtype=torch.int32).cuda()
     d1 = torch.empty((1, cap)).cuda()
     d2 = torch.empty((1, cap)).cuda()
-    hp = np.array([0, 1], np.int32)
-    gpu.check(gpu.lib.pano_match(gpu.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), 1, mode,
-                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2)))
+    _pano_match(gpu, d, [cap, cap], [(0, 1)], mode, best, d1, d2)
     j, dist = ostitch.nn_match_sift(A, B)
     np.testing.assert_array_equal(best.cpu().numpy()[0], j)
     assert (best.cpu().numpy()[0] % 3 == 0).all()          # first of each tied triplet
     np.testing.assert_array_equal(d2.cpu().numpy()[0], d1.cpu().numpy()[0])
 
 
+@pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("with_d2", [True, False])
-def test_match_bf16_multi_pair_ragged(gpu, with_d2):
+def test_match_bf16_multi_pair_ragged(gpu, with_d2, mode):
     """bf16 MFMA path over several pairs with ragged counts (0, 1, a partial tile, many
     tiles so workgroups walk several candidate tiles), a capacity that is not a multiple of
     the 128-row tile, and heavy ties: indices, d1 and d2 equal the exact integer distances
@@ -249,15 +259,11 @@ def test_match_bf16_multi_pair_ragged(gpu, with_d2):
     for f, c in enumerate(counts_h):
         d[f, :c] = pool[rng.integers(0, len(pool), c)] if f % 2 == 0 else rng.integers(0, 256, (c, 128))
     pairs = [(0, 4), (4, 0), (3, 1), (1, 3), (0, 2), (2, 3), (3, 3)]
-    desc = torch.from_numpy(d).cuda()
-    counts = torch.tensor(counts_h, dtype=torch.int32).cuda()
     P = len(pairs)
     best = torch.full((P, cap), -7, dtype=torch.int32).cuda()
     d1 = torch.empty((P, cap)).cuda()
     d2 = torch.empty((P, cap)).cuda() if with_d2 else None
-    hp = np.array(pairs, np.int32).reshape(-1)
-    gpu.check(gpu.lib.pano_match(gpu.h, _lib.ptr(desc), _lib.ptr(counts), cap, _lib.i32p(hp), P, 2,
-                                 _lib.ptr(best), _lib.ptr(d1), _lib.ptr(d2) if with_d2 else None))
+    _pano_match(gpu, d, counts_h, pairs, mode, best, d1, d2)
     b_h, d1_h = best.cpu().numpy(), d1.cpu().numpy()
     d2_h = d2.cpu().numpy() if with_d2 else None
     for p, (fa, fb) in enumerate(pairs):

@@ -100,6 +100,7 @@ SIGNATURES = {
     "pano_sift_copy_level": (_I, [_P, _I, _I, _I, _I, _P]),
     "pano_harris": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "pano_match": (_I, [_P, _P, _P, _I, _PI32, _I, _I, _P, _P, _P]),
+    "pano_match_u8": (_I, [_P, _P, _P, _P, _I, _PI32, _I, _P, _P, _P]),
     "pano_pair_shifts": (_I, [_P, _P, _P, _P, _I, _PI32, _I, _P, _P, _P, _D, _D, _D, _P]),
     "pano_ransac_translate": (_I, [_P, _P, _I, _D, _P]),
     "pano_plan_composite": (_I, [_PD, _PD, _I, _I, _I, ctypes.POINTER(Step), _PI32, _PI32]),

@@ -329,6 +329,194 @@ dist_bf16(const unsigned short *__restrict__ pa, const unsigned short *__restric
     }
 }
 
+// ---------------------------------------------------------------- u8 path (the Stitcher's)
+// Descriptors as bytes [frames][cap][128] with exact squared norms (pano_sift_u8), so nothing
+// is repacked between the descriptor kernel and the GEMM.  Workgroup = 256 query rows
+// (8 waves: 4 row groups of 64 x 2 candidate halves of 64); every 128-row candidate tile is
+// converted ONCE into LDS as the augmented bf16 row [b | c2, c1, c0, 0...] and read by all
+// 256 query rows (the register-fragment form re-streamed each candidate row from L2 once per
+// 128 query rows).  The next tile's bytes are in flight in registers while the current tile
+// is multiplied.  Query fragments [-2 a | 65536, 256, 1, 0...] (|2a| <= 510: 8 significant
+// bits, exact in bf16) are converted from bytes once, in registers, so C = ||b||^2 - 2 a.b
+// exactly, as in dist_bf16.  Per element the fold is one min (the index is searched only
+// when a 16-element block beats the running best), or compare / select with min / max when
+// the second-best distance is wanted.
+constexpr int QT = 256;              // query rows per workgroup
+constexpr int BT = 128;              // candidate rows per LDS tile
+constexpr int BKP = KA + 8;          // LDS row pitch (bf16): 304 B, rows 12 banks apart
+
+__device__ __forceinline__ unsigned int bf16x2_of_ints(int v0, int v1) {
+    // bf16 of small integers (8 significant bits): their f32 bits >> 16, exact
+    return (__float_as_uint((float)v0) >> 16) | (__float_as_uint((float)v1) & 0xffff0000u);
+}
+// the four bytes of x as two dwords of bf16 pairs (v_cvt_f32_ubyte0..3 + two byte permutes)
+__device__ __forceinline__ void bf16x4_of_u8x4(unsigned int x, unsigned int &lo, unsigned int &hi) {
+    const float f0 = (float)(x & 255u), f1 = (float)((x >> 8) & 255u);     // v_cvt_f32_ubyte*
+    const float f2 = (float)((x >> 16) & 255u), f3 = (float)(x >> 24);
+    // selector 0x07060302: bytes 2, 3 of the second operand, then bytes 2, 3 of the first
+    lo = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+    hi = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+}
+
+template <bool SECOND>
+__global__ void __launch_bounds__(512, 2)
+dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
+        const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
+        int n_split) {
+    __shared__ __attribute__((aligned(16))) unsigned short Bs[BT * BKP];
+    __shared__ Part red[2][QT];
+    const int p = blockIdx.z;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    int NA = counts[fa], NB = counts[fb];
+    NA = min(max(NA, 0), cap);
+    NB = min(max(NB, 0), cap);
+    const int i0 = blockIdx.y * QT;
+    const int n_jt = (NB + BT - 1) / BT;
+    if (i0 >= NA || (int)blockIdx.x >= n_jt) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wi = wv & 3, wj = wv >> 2;
+    const int lr = lane & 31, lh = lane >> 5;
+    const uint8_t *dA = desc + (size_t)fa * cap * PANO_DESC_DIM;
+    const uint8_t *dB = desc + (size_t)fb * cap * PANO_DESC_DIM;
+    // ---- query fragments, converted once: rows i0 + wi 64 + m 32 + lr, K step k holds
+    // elements 16 k + 8 lh .. + 8
+    bf16x8 fi[2][KS];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int row = i0 + wi * 64 + m * 32 + lr;
+        const bool live = row < NA;
+#pragma unroll
+        for (int k = 0; k < KS - 1; ++k) {
+            uint2 v = make_uint2(0u, 0u);
+            if (live) v = *(const uint2 *)(dA + (size_t)row * PANO_DESC_DIM + 16 * k + 8 * lh);
+            const unsigned int w[4] = {bf16x2_of_ints(-2 * (int)(v.x & 255), -2 * (int)((v.x >> 8) & 255)),
+                                       bf16x2_of_ints(-2 * (int)((v.x >> 16) & 255), -2 * (int)(v.x >> 24)),
+                                       bf16x2_of_ints(-2 * (int)(v.y & 255), -2 * (int)((v.y >> 8) & 255)),
+                                       bf16x2_of_ints(-2 * (int)((v.y >> 16) & 255), -2 * (int)(v.y >> 24))};
+            fi[m][k] = *(const bf16x8 *)w;
+        }
+        // augmentation [65536, 256, 1, 0, ...] on the lh = 0 half of the last K step
+        const unsigned int a0 = (__float_as_uint(65536.0f) >> 16) | (__float_as_uint(256.0f) & 0xffff0000u);
+        const unsigned int a1 = __float_as_uint(1.0f) >> 16;
+        const unsigned int w[4] = {lh ? 0u : a0, lh ? 0u : a1, 0u, 0u};
+        fi[m][KS - 1] = *(const bf16x8 *)w;
+    }
+    // ---- candidate tile staging: thread t converts row t % 128, bytes 32 (t / 128) .. + 32
+    // (a wave writes 64 consecutive rows at one offset: rows 12 banks apart, conflict free)
+    const int sr = tid & (BT - 1), sp = tid / BT;
+    uint4 pre[2];
+    int pre_norm = 0;
+    auto fetch = [&](int jt) {
+        const int row = jt * BT + sr;
+        pre[0] = pre[1] = make_uint4(0u, 0u, 0u, 0u);
+        pre_norm = (int)kPadNorm;               // past the count: never a best (reduce_parts)
+        if (row < NB) {
+            const uint4 *src = (const uint4 *)(dB + (size_t)row * PANO_DESC_DIM + 32 * sp);
+            pre[0] = src[0];
+            pre[1] = src[1];
+            pre_norm = norms[(size_t)fb * cap + row];
+        }
+    };
+    auto store = [&]() {
+        unsigned short *dst = Bs + sr * BKP + 32 * sp;
+        const unsigned int *u = (const unsigned int *)pre;
+        unsigned int o[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bf16x4_of_u8x4(u[q], o[2 * q], o[2 * q + 1]);
+        uint4 *d4 = (uint4 *)dst;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        if (sp == 0) {
+            const int nb = pre_norm;                // ||b||^2 = c2 65536 + c1 256 + c0
+            const unsigned int t0 = bf16x2_of_ints(nb >> 16, (nb >> 8) & 255);
+            const unsigned int t1 = bf16x2_of_ints(nb & 255, 0);
+            uint4 *aug = (uint4 *)(Bs + sr * BKP + 128);
+            aug[0] = make_uint4(t0, t1, 0u, 0u);
+            aug[1] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    float best[2] = {INFINITY, INFINITY}, second[2] = {INFINITY, INFINITY};
+    int bj[2] = {0x7fffffff, 0x7fffffff};
+    int jt = blockIdx.x;
+    fetch(jt);
+    for (; jt < n_jt; jt += n_split) {
+        __syncthreads();                            // every wave is done with the last tile
+        store();
+        __syncthreads();
+        if (jt + n_split < n_jt) fetch(jt + n_split);   // in flight during the MFMAs
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            bf16x8 fj[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                fj[a] = *(const bf16x8 *)(Bs + (wj * 64 + a * 32 + lr) * BKP + 16 * k + 8 * lh);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a], fi[b][k], acc[a][b], 0, 0, 0);
+        }
+        const int jb = jt * BT + wj * 64 + 4 * lh;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                if (SECOND) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {   // j increasing within the lane: strict <
+                        const float d = acc[a][b][r];
+                        second[b] = fminf(second[b], fmaxf(best[b], d));
+                        const bool lt = d < best[b];
+                        bj[b] = lt ? jb + a * 32 + (r & 3) + 8 * (r >> 2) : bj[b];
+                        best[b] = lt ? d : best[b];
+                    }
+                } else {
+                    // the block's minimum first (one op per element); its index only when it
+                    // beats the running best, which happens ~ln(#blocks) times per row
+                    float m = acc[a][b][0];
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) m = fminf(m, acc[a][b][r]);
+                    if (m < best[b]) {
+                        int ri = 15;
+#pragma unroll
+                        for (int r = 14; r >= 0; --r) ri = acc[a][b][r] == m ? r : ri;   // first r
+                        best[b] = m;
+                        bj[b] = jb + a * 32 + (ri & 3) + 8 * (ri >> 2);
+                    }
+                }
+            }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const float ob = __shfl_xor(best[b], 32);
+        const int oj = __shfl_xor(bj[b], 32);
+        const float os = __shfl_xor(second[b], 32);
+        merge(best[b], bj[b], second[b], ob, oj, os);
+        const int il = wi * 64 + b * 32 + lr;
+        if (lh == 0) red[wj][il] = Part{best[b], bj[b], second[b]};
+    }
+    __syncthreads();
+    if (tid < QT) {
+        Part x = red[0][tid];
+        const Part y = red[1][tid];
+        float bb = x.best, ss = x.second;
+        int jj = x.idx;
+        merge(bb, jj, ss, y.best, y.idx, y.second);
+        const int gi = i0 + tid;
+        if (gi < NA) {
+            const float na = (float)norms[(size_t)fa * cap + gi];
+            parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{na + bb, jj, na + ss};
+        }
+    }
+}
+
 __global__ void reduce_parts(const Part *__restrict__ parts, const int32_t *__restrict__ counts,
                              int cap, PairArg pairs, int n_jt, int32_t *__restrict__ best,
                              float *__restrict__ d1, float *__restrict__ d2) {
@@ -426,6 +614,46 @@ dist_direct(const float *__restrict__ desc, const int32_t *__restrict__ counts, 
 }  // namespace
 
 int match_set_attributes(pano_ctx *) { return PANO_OK; }
+
+int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, const int32_t *counts,
+                    int cap, const int32_t *h_pairs, int n_pairs, int32_t *best, float *d1, float *d2) {
+    if (cap <= 0 || n_pairs <= 0 || !desc || !norms || !counts || !best || !d1)
+        return pano_fail(ctx, PANO_E_ARG, "pano_match_u8: bad arguments");
+    const int n_qt = (cap + QT - 1) / QT, n_bt = (cap + BT - 1) / BT;
+    for (int p0 = 0; p0 < n_pairs; p0 += 256) {
+        const int np = n_pairs - p0 < 256 ? n_pairs - p0 : 256;
+        PairArg pa;
+        for (int q = 0; q < np; ++q) {
+            pa.a[q] = h_pairs[2 * (p0 + q)];
+            pa.b[q] = h_pairs[2 * (p0 + q) + 1];
+        }
+        // query tiles x candidate splits x pairs: at least ~2 workgroups per CU even when
+        // each pair is small (parrington); large pairs walk their candidate tiles in-kernel
+        const int n_split = std::max(1, std::min(n_bt, (1024 + n_qt * np - 1) / (n_qt * np)));
+        const size_t part_bytes = ((size_t)np * n_split * cap * sizeof(Part) + 255) & ~size_t(255);
+        int rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes, part_bytes);
+        if (rc) return rc;
+        Part *parts = (Part *)ctx->mscratch;
+        int32_t *bp = best + (size_t)p0 * cap;
+        float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 ? d2 + (size_t)p0 * cap : nullptr;
+        dim3 grid(n_split, n_qt, np);
+        {
+            PanoProf prof_(ctx, PK_DIST_MFMA);
+            if (p2)
+                dist_u8<true><<<grid, 512, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_split);
+            else
+                dist_u8<false><<<grid, 512, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_split);
+        }
+        PANO_LAUNCH_CHECK(ctx, "dist_u8");
+        dim3 g2((cap + 255) / 256, np);
+        {
+            PanoProf prof_(ctx, PK_REDUCE);
+            reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_split, bp, p1, p2);
+        }
+        PANO_LAUNCH_CHECK(ctx, "reduce_parts");
+    }
+    return PANO_OK;
+}
 
 int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
                  const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,

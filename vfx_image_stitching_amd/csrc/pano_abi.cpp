@@ -215,6 +215,12 @@ int pano_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
     return launch_match(ctx, desc, counts, cap, pairs, n_pairs, exact_int, best, d1, d2);
 }
 
+int pano_match_u8(pano_ctx *ctx, const uint8_t *desc_u8, const int32_t *norms, const int32_t *counts,
+                  int cap, const int32_t *pairs, int n_pairs, int32_t *best, float *d1, float *d2) {
+    if (!ctx || !pairs) return PANO_E_ARG;
+    return launch_match_u8(ctx, desc_u8, norms, counts, cap, pairs, n_pairs, best, d1, d2);
+}
+
 int pano_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
                      const int32_t *counts, int cap, const int32_t *pairs, int n_pairs,
                      const int32_t *best, const float *d1, const float *d2, double desc_thresh,

@@ -182,6 +182,8 @@ int launch_harris(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w, int ma
 int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int cap,
                  const int32_t *h_pairs, int n_pairs, int exact_int, int32_t *best, float *d1,
                  float *d2);
+int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, const int32_t *counts,
+                    int cap, const int32_t *h_pairs, int n_pairs, int32_t *best, float *d1, float *d2);
 int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
                        const int32_t *counts, int cap, const int32_t *h_pairs, int n_pairs,
                        const int32_t *best, const float *d1, const float *d2,

@@ -34,6 +34,16 @@ from ._lib import PanoError, context, ptr
 BBOX_SLOTS = 64                         # include/pano.h PANO_BBOX_SLOTS
 
 
+class Features(tuple):
+    """(keypoints, descriptors, counts) of a batch, plus the descriptors' squared norms when
+    they are bytes (pano_sift_u8): what pano_match_u8 reads."""
+
+    def __new__(cls, feats, norms):
+        t = super().__new__(cls, feats)
+        t.norms = norms
+        return t
+
+
 @dataclass
 class StitchResult:
     panorama: "object"                 # torch uint8 [H', W', 3] on device (a view of canvas)
@@ -76,8 +86,10 @@ class Stitcher:
         # Lowe ratio test (0 = off, as the reference's stitcher; the visualiser uses 0.7 with
         # FLANN, sift_visualizeUI.py:252-257)
         self.ratio = float(ratio)
-        # SIFT distance GEMM: "bf16" (exact for integer descriptors, 16x MFMA rate) or "f32"
-        self.match = match or os.environ.get("PANO_MATCH", "bf16")
+        # SIFT descriptors + distance GEMM: "u8" (bytes from the descriptor kernel straight into
+        # the LDS-staged bf16 GEMM, pano_sift_u8 + pano_match_u8), "bf16" (f32 descriptors
+        # packed to bf16 rows) or "f32" (f32 MFMA); all exact for integer descriptors
+        self.match = match or os.environ.get("PANO_MATCH", "u8")
         self._buf = {}
         self._graphs = {}                # key -> (pano_graph, outputs of the captured call)
         self._gstream = None             # private stream for capture / replay
@@ -120,8 +132,15 @@ class Stitcher:
         T = self.torch
         if self.method == "sift":
             kps = self._get("kps", (n, self.cap, 6), T.int32)
-            desc = self._get("desc", (n, self.cap, 128), T.float32)
             counts = self._get("counts", (n,), T.int32)
+            if self.match == "u8":
+                desc = self._get("desc_u8", (n, self.cap, 128), T.uint8)
+                norms = self._get("norms", (n, self.cap), T.int32)
+                self.ctx.check(self.ctx.lib.pano_sift_u8(self.ctx.h, ptr(frames_dev), n, h, w,
+                                                         ctypes.byref(self.params), ptr(kps), ptr(desc),
+                                                         ptr(norms), self.cap, ptr(counts)))
+                return Features((kps, desc, counts), norms)
+            desc = self._get("desc", (n, self.cap, 128), T.float32)
             self.ctx.check(self.ctx.lib.pano_sift(self.ctx.h, ptr(frames_dev), n, h, w,
                                                   ctypes.byref(self.params), ptr(kps), ptr(desc),
                                                   self.cap, ptr(counts)))
@@ -162,11 +181,13 @@ class Stitcher:
         cap = max(p[1].shape[1] for p in parts)
         n = len(parts)
         pts = T.zeros((n, cap) + tuple(parts[0][0].shape[2:]), dtype=parts[0][0].dtype, device=self.device)
-        desc = T.zeros((n, cap, 128), dtype=T.float32, device=self.device)
+        desc = T.zeros((n, cap, 128), dtype=parts[0][1].dtype, device=self.device)
         counts = T.cat([p[2] for p in parts])
         for i, (p, d, _) in enumerate(parts):
             pts[i, :p.shape[1]] = p[0]
             desc[i, :d.shape[1]] = d[0]
+        if desc.dtype == T.uint8:
+            return Features((pts, desc, counts), (desc.int() ** 2).sum(-1, dtype=T.int32))
         return pts, desc, counts
 
     def pair_records(self, feats, pairs, out=None):
@@ -179,11 +200,18 @@ class Stitcher:
         d1 = self._get("d1", (P, cap), T.float32)
         # the second-best distance is only computed when the Lowe ratio test needs it (the
         # reference's stitcher has none: image_stitching_sift.py:63-79)
-        exact = (2 if self.match == "bf16" else 1) if self.method == "sift" else 0
+        exact = (1 if self.match == "f32" else 2) if self.method == "sift" else 0
         d2 = self._get("d2", (P, cap), T.float32) if (self.ratio > 0 or exact != 2) else None
         d2p = ptr(d2) if d2 is not None else None
-        self.ctx.check(self.ctx.lib.pano_match(self.ctx.h, ptr(desc), ptr(counts), cap,
-                                               _lib.i32p(hp), P, exact, ptr(best), ptr(d1), d2p))
+        if desc.dtype == T.uint8:
+            norms = getattr(feats, "norms", None)
+            if norms is None:
+                norms = (desc.int() ** 2).sum(-1, dtype=T.int32)
+            self.ctx.check(self.ctx.lib.pano_match_u8(self.ctx.h, ptr(desc), ptr(norms), ptr(counts), cap,
+                                                      _lib.i32p(hp), P, ptr(best), ptr(d1), d2p))
+        else:
+            self.ctx.check(self.ctx.lib.pano_match(self.ctx.h, ptr(desc), ptr(counts), cap,
+                                                   _lib.i32p(hp), P, exact, ptr(best), ptr(d1), d2p))
         recs = out if out is not None else self._get("recs", (P, 64), T.uint8)
         kps_p = ptr(pts) if self.method == "sift" else None
         xy_p = None if self.method == "sift" else ptr(pts)
