@@ -241,6 +241,18 @@ int pano_composite_planned(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t
                            int h, int w, const void *d_plan, uint8_t *d_canvas, int Hcap,
                            int Wcap, int black_threshold, int32_t *d_bbox);
 
+/* One rank's band of a sharded stitch from the GLOBAL plan of pano_plan_device
+ * (built from every rank's gathered records): the rank holds frames f0 .. f0 + n_local - 1
+ * (its pairs plus the boundary frame f0) and owns the canvas columns whose last covering
+ * frame is one of its frames after f0 (plus frame 0's on the first band).  Writes a local
+ * plan (pano_plan_device_bytes) whose canvas is the owned column range -- pass it with the
+ * rank's frames to pano_composite_planned, canvas capacity Hcap x Wcap -- and d_band[4] =
+ * {status, own_lo, own_hi, global W}: PANO_OK, the global plan's status, PANO_E_UNSUPPORTED
+ * (owned columns not contiguous) or PANO_E_OVERFLOW (band wider than Wcap).  Device-only,
+ * graph-capturable. */
+int pano_band_plan(pano_ctx *ctx, const void *d_plan, int f0, int n_local, int w, int Wcap,
+                   void *d_local_plan, int32_t *d_band);
+
 /* blend_two_images(shift_vec, ref_match, imgA, imgB) for arbitrary inputs
  * image_stitching_sift.py:156-202.  Geometry comes from pano_blend_geometry. */
 int pano_blend_geometry(double dx, double dy, const double *h_ref4, int hA, int wA, int hB,

@@ -116,7 +116,16 @@ def _worker(rank, world, port, gold, q):
             (xa, ya), (xb, yb) = pairs[s0 + k]
             local[k]["xA"], local[k]["yA"], local[k]["xB"], local[k]["yB"] = xa, ya, xb, yb
         t = torch.from_numpy(local.view(np.uint8).reshape(c, 64).copy())
-        recs = D.gather_records(t, [cc for _, cc in shards])
+        counts = [cc for _, cc in shards]
+        recs = D.gather_records(t, counts)
+        # the device path's form: zero-padded [pmax, 64] blocks, one all_gather_into_tensor,
+        # compacted by the block layout -- the same global records
+        pmax, starts = D.block_layout(counts)
+        blk = torch.zeros((pmax, 64), dtype=torch.uint8)
+        blk[:c] = t
+        comp = D.compact_blocks(D.gather_blocks(blk), counts)
+        assert list(starts) == [0] + list(np.cumsum(counts))
+        assert np.array_equal(comp.numpy(), recs.view(np.uint8).reshape(-1, 64))
         # 2. every rank replays the same global plan and derives its band
         got_shifts, got_pairs = D.records_to_shifts(recs)
         steps, first, (H, W) = D.global_plan(drift_correct(got_shifts), got_pairs,

@@ -470,6 +470,66 @@ def test_bands_assemble_to_single_gpu_canvas(gpu, method, setname):
         assert np.array_equal(got, canvas), world
 
 
+@pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("harris", "grail")])
+def test_device_band_path_assembles_to_single_gpu_canvas(gpu, method, setname):
+    """The N>1 step (distributed.run_rank's segments: rank_records -> all_gather -> rank_band
+    with pano_plan_device + pano_band_plan + pano_composite_planned) simulated for world 2, 3
+    and 8 in one process (the gather is a concatenation of the ranks' record blocks): every
+    rank's global records equal the single-GPU records, the owned bands tile the single-GPU
+    canvas byte for byte, and the crop boxes reduce to the single-GPU box."""
+    import torch
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd import distributed as D
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = data.load_set(setname)
+    st = Stitcher(method)
+    dev = st.upload(frames)
+    full = st.run(dev, focals, margin=margin)
+    canvas = full.canvas.cpu().numpy()
+    for world in (2, 3, 8):
+        shards = D.shard_ranges(len(frames) - 1, world)
+        counts = [cnt for _, cnt in shards]
+        pmax = max(counts)
+        blocks, locs = [], []
+        for s, cnt in shards:
+            block, cyl, colnz = D.rank_records(st, dev[s:s + cnt + 1], focals[s:s + cnt + 1], pmax)
+            blocks.append(block.clone())
+            locs.append((s, cyl.clone(), colnz.clone()))
+        gathered = torch.cat(blocks)
+        got = np.full_like(canvas, 7)
+        boxes = []
+        for s, cyl, colnz in locs:
+            recs, owned, lo, (H, W), box = D.rank_band(st, cyl, colnz, gathered, counts, s, margin)
+            assert np.array_equal(recs.view(np.uint8), full.records.view(np.uint8))
+            assert (H, W) == canvas.shape[:2]
+            got[:, lo:lo + owned.shape[1]] = owned.cpu().numpy()
+            boxes.append(box)
+        assert np.array_equal(got, canvas), world
+        y0 = min(b[0] for b in boxes); y1 = max(b[1] for b in boxes)
+        x0 = min(b[2] for b in boxes); x1 = max(b[3] for b in boxes)
+        assert (max(0, y0 + margin), min(canvas.shape[0] - 1, y1 - margin), x0, x1) == full.bbox
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_run_rank_world1_is_the_single_gpu_stitch(gpu, parrington, graph):
+    """At N=1 distributed.run_rank (no process group) is Stitcher.run's device-planned stitch:
+    same records, canvas bytes and crop box (the N>1 path is the N=1 path plus the gather)."""
+    from vfx_image_stitching_amd import distributed as D
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = parrington
+    st = Stitcher("sift")
+    dev = st.upload(frames)
+    full = st.run(dev, focals, margin=margin)
+    canvas = full.canvas.cpu().numpy()
+    for _ in range(2 if graph else 1):
+        out = D.run_rank(st, dev, focals, 0, [len(frames) - 1], margin=margin, graph=graph)
+        assert np.array_equal(out["records"].view(np.uint8), full.records.view(np.uint8))
+        assert out["x_offset"] == 0 and out["canvas_hw"] == canvas.shape[:2]
+        assert np.array_equal(out["band"].cpu().numpy(), canvas)
+        assert out["bbox"] == full.bbox
+    st.release_graphs()
+
+
 # ------------------------------------------------------------------ hipGraph replay
 @pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("harris", "grail")])
 def test_graph_replay_matches_eager(gpu, method, setname, gold_json):

@@ -653,7 +653,88 @@ plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int
     }
 }
 
+// One rank's band of a sharded stitch, from the GLOBAL device plan: the rank holds
+// frames f0 .. f0 + n_local - 1 (its pairs plus the boundary frame f0) and owns the canvas
+// columns whose last covering frame is one of its frames after f0 (plus frame 0's columns on
+// the first band).  With no column covered by three frames -- which plan_device checks: its
+// status is PANO_OK only then -- a column's final value depends on its last covering frame
+// and that frame's predecessor, both held by the owning band, so the band composites exactly
+// like the whole canvas.  Writes a LOCAL plan over the band's frames whose canvas is the
+// owned column range (frame positions shifted by its first column, possibly negative), for
+// pano_composite_planned, and band = {status, own_lo, own_hi, global W}.
+__global__ void band_plan(const DevPlan *__restrict__ g, int f0, int n_local, int w, int Wcap,
+                          DevPlan *__restrict__ l, int32_t *__restrict__ band) {
+    __shared__ int32_t hdr[3];
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        int st = g->status, lo = 0, hi = 0;
+        const int n = g->n;
+        if (st == PANO_OK && (f0 < 0 || n_local < 1 || f0 + n_local > n)) st = PANO_E_ARG;
+        if (st == PANO_OK) {
+            // owned pieces: last_cover(i) = frame i's span minus frame i+1's span (at most two
+            // pieces each; disjoint across frames because frame i+2 never meets frame i), so
+            // their union is one interval iff its span equals their total length
+            lo = 0x7fffffff;
+            hi = -0x7fffffff;
+            long long total = 0;
+            const int i0 = f0 == 0 ? 0 : f0 + 1;
+            for (int i = i0; i <= f0 + n_local - 1; ++i) {
+                const int a = g->sa.fx[i], b = a + w;
+                int pc[2][2] = {{a, b}, {0, 0}};
+                if (i + 1 < n) {
+                    const int na = g->sa.fx[i + 1], nb = na + w;
+                    pc[0][1] = min(b, na);
+                    pc[1][0] = max(a, nb);
+                    pc[1][1] = b;
+                }
+                for (int q = 0; q < 2; ++q)
+                    if (pc[q][0] < pc[q][1]) {
+                        lo = min(lo, pc[q][0]);
+                        hi = max(hi, pc[q][1]);
+                        total += pc[q][1] - pc[q][0];
+                    }
+            }
+            if (lo > hi) { lo = 0; hi = 0; }
+            else if (total != (long long)(hi - lo)) st = PANO_E_UNSUPPORTED;
+            if (st == PANO_OK && hi - lo > Wcap) st = PANO_E_OVERFLOW;
+        }
+        hdr[0] = st; hdr[1] = lo; hdr[2] = hi;
+    }
+    __syncthreads();
+    const int st = hdr[0], lo = hdr[1], hi = hdr[2];
+    for (int k = tid; k < n_local && st == PANO_OK; k += blockDim.x) {
+        l->sa.fx[k] = g->sa.fx[f0 + k] - lo;
+        l->sa.fy[k] = g->sa.fy[f0 + k];
+        l->sa.is_a[k] = k == 0 ? 0 : g->sa.is_a[f0 + k];
+        l->sa.overlap[k] = k == 0 ? 0.0 : g->sa.overlap[f0 + k];
+    }
+    if (tid == 0) {
+        l->status = st;
+        l->n = n_local;
+        l->H = st == PANO_OK ? g->H : 0;
+        l->W = st == PANO_OK ? hi - lo : 0;
+        l->first_x = l->first_y = 0;
+        band[0] = st;
+        band[1] = lo;
+        band[2] = hi;
+        band[3] = g->W;
+    }
+}
+
 }  // namespace
+
+int launch_band_plan(pano_ctx *ctx, const void *plan, int f0, int n_local, int w, int Wcap,
+                     void *local_plan, int32_t *band) {
+    if (!plan || !local_plan || !band || n_local < 1 || n_local > kMaxSeq || f0 < 0 || w <= 0)
+        return pano_fail(ctx, PANO_E_ARG, "pano_band_plan: bad arguments");
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        band_plan<<<1, 256, 0, ctx->stream>>>((const DevPlan *)plan, f0, n_local, w, Wcap,
+                                             (DevPlan *)local_plan, band);
+    }
+    PANO_LAUNCH_CHECK(ctx, "band_plan");
+    return PANO_OK;
+}
 
 size_t plan_device_bytes() { return sizeof(DevPlan); }
 

@@ -258,6 +258,12 @@ int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, int
     return launch_plan_device(ctx, recs, n, h, w, int_shifts, Hcap, Wcap, plan);
 }
 
+int pano_band_plan(pano_ctx *ctx, const void *plan, int f0, int n_local, int w, int Wcap,
+                   void *local_plan, int32_t *band) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_band_plan(ctx, plan, f0, n_local, w, Wcap, local_plan, band);
+}
+
 int pano_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
                            int w, const void *plan, uint8_t *canvas, int Hcap, int Wcap,
                            int black_threshold, int32_t *bbox) {

@@ -212,31 +212,155 @@ def global_bbox(local_bbox, group=None):
     return int(-v[0]), int(v[1]), int(-v[2]), int(v[3])
 
 
-def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15,
-             graph=False):
-    """One rank's share of a sharded stitch (frames_dev = its pair range + boundary frame).
+def rank_records(stitcher, frames_dev, focals, pmax, graph=False):
+    """Segment 1 of a rank's step (the single-GPU launch chain up to the pair records):
+    cylindrical projection, features, matching and RANSAC of the rank's frames, the records
+    written into a zero-padded [pmax, 64] uint8 device block (what the all_gather moves).
+    Returns (block, cyl, colnz)."""
+    import torch
+    st = stitcher
+    n_local = frames_dev.shape[0]
+    block = st._get("recs_block", (pmax, 64), torch.uint8)
 
-    Returns dict(records=global PAIR_NP, band=device canvas of the owned band,
-    bbox=global crop box, x_offset=band's first column in the final canvas).
-    """
+    def seg():
+        cyl, colnz = st.cylindrical(frames_dev, focals)
+        feats = st.features(cyl)
+        st.pair_records(feats, [(i, i + 1) for i in range(n_local - 1)], out=block[:n_local - 1])
+        return cyl, colnz
+
+    if not graph:
+        block.zero_()
+        cyl, colnz = seg()
+        return block, cyl, colnz
+    key = ("rank_records", frames_dev.data_ptr(), tuple(frames_dev.shape),
+           np.asarray(focals, np.float64).tobytes(), pmax, st.method, st.match, bytes(st.params),
+           st.cap, st.max_points, st.ransac_thr, st.desc_thresh, st.ratio)
+    if st._graph_entry(key) is None:
+        block.zero_()                      # padding rows stay zero in every replay
+    cyl, colnz = st._replay(key, seg)
+    return block, cyl, colnz
+
+
+def gather_blocks(block, group=None):
+    """THE collective of a sharded stitch: all_gather_into_tensor of every rank's [pmax, 64]
+    record block, device to device (RCCL over xGMI for backend "nccl"; gloo on CPU tensors)."""
     import torch
     import torch.distributed as dist
-    stitcher.last_graphs = []
-    recs_dev, cyl, colnz = local_records(stitcher, frames_dev, focals, graph)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world > 1:
-        recs = gather_records(recs_dev, pair_counts, group)
+    if world == 1:
+        return block
+    out = torch.empty((world * block.shape[0], 64), dtype=torch.uint8, device=block.device)
+    dist.all_gather_into_tensor(out, block, group=group)
+    return out
+
+
+def block_layout(pair_counts):
+    """Where each rank's records sit: rank r's block of the gathered [world * pmax, 64] array
+    starts at row r * pmax and its records land at global pair starts[r] (pair order)."""
+    pmax = max(pair_counts)
+    starts = np.concatenate([[0], np.cumsum(pair_counts)]).astype(np.int64)
+    return pmax, starts
+
+
+def compact_blocks(gathered, pair_counts):
+    """The global [P, 64] record array from gathered blocks (torch; rank_band does the same
+    with device copies inside its launch chain)."""
+    import torch
+    pmax, _ = block_layout(pair_counts)
+    return torch.cat([gathered[r * pmax:r * pmax + c] for r, c in enumerate(pair_counts)])
+
+
+def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=False):
+    """Segment 2 (device-planned, one host read): compact the gathered blocks into the global
+    record array, pano_plan_device over the WHOLE sequence (drift correction + geometry),
+    pano_band_plan for this rank's frames f0 .. f0 + n_local - 1, pano_composite_planned of its
+    band, and one pinned copy of {records, crop-box partials, band info, plan header}.
+    Returns (records PAIR_NP, band view [H, own_hi - own_lo, 3] on device, own_lo, (H, W),
+    local crop box (ymin, ymax, xmin, xmax) in global columns or NO_BOX)."""
+    import torch
+    from .pipeline import BBOX_SLOTS
+    st = stitcher
+    lib, c = st.ctx.lib, st.ctx.h
+    n_local, h, w = cyl.shape[0], cyl.shape[1], cyl.shape[2]
+    pmax, starts = block_layout(pair_counts)
+    P = int(starts[-1])
+    plan_bytes = int(lib.pano_plan_device_bytes())
+    off_bb = P * 64
+    off_band = off_bb + 16 * BBOX_SLOTS
+    off_gp = (off_band + 16 + 255) // 256 * 256
+    off_lp = off_gp + (plan_bytes + 255) // 256 * 256
+    res = st._get("band_result", (off_lp + plan_bytes,), torch.uint8)
+    Hcap, Wcap = st.canvas_cap or (2 * h, (n_local + 2) * w)
+    canvas = st._get("band_canvas", (Hcap * Wcap * 3,), torch.uint8)
+    nhead = off_gp + 32
+    pin = st._buf.get("band_pin")
+    if pin is None or pin.numel() < nhead:
+        pin = torch.empty(max(nhead, 4096), dtype=torch.uint8, pin_memory=True)
+        st._buf["band_pin"] = pin
+
+    def seg():
+        for r, cnt in enumerate(pair_counts):
+            if cnt:
+                st.ctx.check(lib.pano_copy_async(c, _lib._P(res.data_ptr() + int(starts[r]) * 64),
+                                                 _lib._P(gathered.data_ptr() + r * pmax * 64), cnt * 64))
+        st.ctx.check(lib.pano_plan_device(c, _lib.ptr(res[:off_bb]), P + 1, h, w,
+                                          int(st.method != "sift"), Hcap, 1 << 30,
+                                          _lib.ptr(res[off_gp:off_lp])))
+        st.ctx.check(lib.pano_band_plan(c, _lib.ptr(res[off_gp:off_lp]), f0, n_local, w, Wcap,
+                                        _lib.ptr(res[off_lp:]), _lib.ptr(res[off_band:off_gp])))
+        st.ctx.check(lib.pano_composite_planned(c, _lib.ptr(cyl), _lib.ptr(colnz), n_local, h, w,
+                                                _lib.ptr(res[off_lp:]), _lib.ptr(canvas), Hcap, Wcap, 0,
+                                                _lib.ptr(res[off_bb:off_band])))
+        st.ctx.check(lib.pano_copy_async(c, _lib._P(pin.data_ptr()), _lib.ptr(res), nhead))
+
+    if graph:
+        key = ("rank_band", cyl.data_ptr(), colnz.data_ptr(), tuple(cyl.shape), gathered.data_ptr(),
+               tuple(pair_counts), f0, st.method, Hcap, Wcap, res.data_ptr(), canvas.data_ptr())
+        st._replay(key, seg)
     else:
-        recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)
-    owned, own_lo, (H, W) = composite_band(stitcher, cyl, colnz, recs, pair_start,
-                                           check=world > 1)
-    if owned.shape[1] > 0:
-        bb = stitcher.bbox(owned.contiguous()).to(torch.int64)
-        lo = torch.where(bb[1] >= 0, bb, torch.tensor(NO_BOX, device=bb.device))
-        lo[2:] = torch.where(lo[3] >= 0, lo[2:] + own_lo, lo[2:])
-    else:
-        lo = torch.tensor(NO_BOX, dtype=torch.int64, device=owned.device)
-    g = global_bbox(lo, group)
+        seg()
+    torch.cuda.current_stream(st.device).synchronize()           # the one host read
+    head = pin.numpy()[:nhead]
+    recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1).copy()
+    st._check_records(recs)
+    band = head[off_band:off_band + 16].view(np.int32)
+    gst = head[off_gp:off_gp + 32].view(np.int32)
+    if gst[0] == _lib.PANO_E_NOMATCH:
+        raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+    if band[0] != _lib.PANO_OK:
+        raise BandError(f"device band plan refused the band (status {int(band[0])}): columns "
+                        "covered by three frames, a non-contiguous band or a band wider than the "
+                        "canvas capacity")
+    H, W, own_lo, own_hi = int(gst[1]), int(gst[2]), int(band[1]), int(band[2])
+    bw = own_hi - own_lo
+    view = canvas[:H * bw * 3].view(H, bw, 3)
+    slots = head[off_bb:off_band].view(np.int32).reshape(BBOX_SLOTS, 4)
+    box = (int(slots[:, 0].min()), int(slots[:, 1].max()), int(slots[:, 2].min()), int(slots[:, 3].max()))
+    box = NO_BOX if box[1] < 0 else (box[0], box[1], box[2] + own_lo, box[3] + own_lo)
+    return recs, view, own_lo, (H, W), box
+
+
+def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15,
+             graph=False):
+    """One rank's share of a sharded stitch (frames_dev = its pair range + boundary frame):
+    the single-GPU launch chain (rank_records, rank_band: device planning, one host read)
+    split around ONE all_gather of the 64-byte pair records, plus the crop box's 4-int
+    all_reduce.  At world 1 it is Stitcher.run's device-planned stitch over the whole canvas.
+
+    Returns dict(records=global PAIR_NP, band=device canvas of the owned band,
+    bbox=global crop box, x_offset=band's first column in the final canvas)."""
+    import torch
+    import torch.distributed as dist
+    st = stitcher
+    st.last_graphs = []
+    st._graph_mode = graph
+    pmax = max(pair_counts)
+    block, cyl, colnz = rank_records(st, frames_dev, focals, pmax, graph)
+    gathered = gather_blocks(block, group)
+    recs, owned, own_lo, (H, W), box = rank_band(st, cyl, colnz, gathered, pair_counts, pair_start,
+                                                 margin, graph)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    g = box if world == 1 else global_bbox(torch.tensor(box, dtype=torch.int64, device=owned.device), group)
     if g[1] >= 0:
         y0, y1 = max(0, g[0] + margin), min(H - 1, g[1] - margin)
     else:
