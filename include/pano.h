@@ -186,6 +186,33 @@ int pano_pair_shifts(pano_ctx *ctx, const pano_kp *d_kps, const int32_t *d_xy_i3
                      double desc_thresh, double ratio, double ransac_thr,
                      pano_pair_rec *d_recs);
 
+/* ---------------------------------------------------------------- f3
+ * The visualiser's matching + homography (sift_visualizeUI.py:247-266): good matches by the
+ * Lowe ratio test on the exact kNN-2 of pano_match / pano_match_u8 (d1 < ratio^2 d2 on the
+ * squared distances; FLANN's approximate neighbours are not reproduced) and, optionally,
+ * d1 < desc_thresh (<= 0: no threshold); then, for a pair with more than min_good good
+ * matches (the visualiser's MIN_MATCH_COUNT = 10), a deterministic homography RANSAC:
+ * n_hyp 4-point hypotheses drawn by a counter-based hash of (seed, pair, hypothesis),
+ * degenerate samples rejected as cv2's checkSubset does, each scored by the matches whose
+ * squared reprojection error is <= reproj_thr^2 (cv2.findHomography(..., cv2.RANSAC, 5.0)),
+ * the first best refitted by Hartley-normalised least squares over its inliers.
+ * d_recs[n_pairs]; d_mask [n_pairs][cap] (optional) flags the refit's inliers among the pair's
+ * good matches, in match order. */
+typedef struct pano_homography_rec {
+    double H[9];               /* row-major, H[8] = 1 (zeros when status != PANO_OK)        */
+    int32_t n_matches;         /* good matches                                              */
+    int32_t inliers;           /* inliers of the refitted H                                 */
+    int32_t hyp_inliers;       /* inliers of the best hypothesis                            */
+    int32_t status;            /* PANO_OK, PANO_E_NOMATCH (too few matches / no model) or
+                                  PANO_E_OVERFLOW (a frame's count exceeded cap)             */
+} pano_homography_rec;
+
+int pano_pair_homography(pano_ctx *ctx, const pano_kp *d_kps, const int32_t *d_counts, int cap,
+                         const int32_t *h_pairs, int n_pairs, const int32_t *d_best,
+                         const float *d_d1, const float *d_d2, double desc_thresh, double ratio,
+                         double reproj_thr, int n_hyp, uint64_t seed, int min_good,
+                         pano_homography_rec *d_recs, uint8_t *d_mask);
+
 /* ransac(matches) on an explicit move list (drop-in for the Python function):
  * d_moves [k][2] double (dx, dy).  d_out[0] = best index (-1 if k == 0), d_out[1] = votes. */
 int pano_ransac_translate(pano_ctx *ctx, const double *d_moves, int k, double thr,

@@ -65,6 +65,16 @@ PAIR_NP = np.dtype([("dx", "<f8"), ("dy", "<f8"), ("xA", "<f8"), ("yA", "<f8"),
                     ("best", "<i4"), ("status", "<i4")])
 
 
+class HomographyRec(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_double * 9), ("n_matches", ctypes.c_int32),
+                ("inliers", ctypes.c_int32), ("hyp_inliers", ctypes.c_int32),
+                ("status", ctypes.c_int32)]
+
+
+HOMOGRAPHY_NP = np.dtype([("H", "<f8", (9,)), ("n_matches", "<i4"), ("inliers", "<i4"),
+                          ("hyp_inliers", "<i4"), ("status", "<i4")])
+
+
 class Step(ctypes.Structure):
     _fields_ = [("frame_x", ctypes.c_int32), ("frame_y", ctypes.c_int32),
                 ("canvas_x", ctypes.c_int32), ("canvas_y", ctypes.c_int32),
@@ -103,6 +113,8 @@ SIGNATURES = {
     "pano_match_u8": (_I, [_P, _P, _P, _P, _I, _PI32, _I, _P, _P, _P]),
     "pano_pair_shifts": (_I, [_P, _P, _P, _P, _I, _PI32, _I, _P, _P, _P, _D, _D, _D, _P]),
     "pano_ransac_translate": (_I, [_P, _P, _I, _D, _P]),
+    "pano_pair_homography": (_I, [_P, _P, _P, _I, _PI32, _I, _P, _P, _P, _D, _D, _D, _I,
+                                  ctypes.c_uint64, _I, _P, _P]),
     "pano_plan_composite": (_I, [_PD, _PD, _I, _I, _I, ctypes.POINTER(Step), _PI32, _PI32]),
     "pano_composite": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I]),
     "pano_composite_bbox": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P, _I, _I,

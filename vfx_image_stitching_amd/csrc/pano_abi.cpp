@@ -102,7 +102,8 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
-                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted, ctx->boxslots};
+                    ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
+                    ctx->boxslots, ctx->hmscratch};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
@@ -228,6 +229,15 @@ int pano_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
     if (!ctx || !pairs) return PANO_E_ARG;
     return launch_pair_shifts(ctx, kps, xy_i32, counts, cap, pairs, n_pairs, best, d1, d2,
                               desc_thresh, ratio, ransac_thr, recs);
+}
+
+int pano_pair_homography(pano_ctx *ctx, const pano_kp *kps, const int32_t *counts, int cap,
+                         const int32_t *pairs, int n_pairs, const int32_t *best, const float *d1,
+                         const float *d2, double desc_thresh, double ratio, double reproj_thr, int n_hyp,
+                         uint64_t seed, int min_good, pano_homography_rec *recs, uint8_t *mask) {
+    if (!ctx || !pairs) return PANO_E_ARG;
+    return launch_pair_homography(ctx, kps, counts, cap, pairs, n_pairs, best, d1, d2, desc_thresh, ratio,
+                                  reproj_thr, n_hyp, seed, min_good, recs, mask);
 }
 
 int pano_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr, int32_t *out) {

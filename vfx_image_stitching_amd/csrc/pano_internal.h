@@ -91,6 +91,8 @@ struct pano_ctx {
     int32_t *boxslots = nullptr; size_t boxslots_bytes = 0;   // crop-box partials (kBoxSlots x 4)
     // ---- match / ransac scratch
     void *mscratch = nullptr; size_t mscratch_bytes = 0;
+    // ---- homography scratch
+    void *hmscratch = nullptr; size_t hmscratch_bytes = 0;
     // ---- composite scratch
     uint8_t *flags = nullptr; size_t flags_bytes = 0;
     // ---- harris scratch
@@ -190,6 +192,15 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
                        double desc_thresh, double ratio, double thr, pano_pair_rec *recs);
 int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr,
                             int32_t *out);
+int launch_match_compact(pano_ctx *ctx, const pano_kp *kps, const int32_t *counts, int cap,
+                         const int32_t *fa, const int32_t *fb, int np, const int32_t *best,
+                         const float *d1, const float *d2, double desc_thresh, double ratio,
+                         void *moves, int32_t *midx, int32_t *kcount);
+int launch_pair_homography(pano_ctx *ctx, const pano_kp *kps, const int32_t *counts, int cap,
+                           const int32_t *h_pairs, int n_pairs, const int32_t *best, const float *d1,
+                           const float *d2, double desc_thresh, double ratio, double reproj_thr,
+                           int n_hyp, unsigned long long seed, int min_good,
+                           pano_homography_rec *recs, uint8_t *mask);
 int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
                      int w, const pano_step *steps, const int32_t *first_xy, uint8_t *canvas,
                      int H, int W);

@@ -294,6 +294,29 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
     return PANO_OK;
 }
 
+// Ordered compaction of the accepted matches of np pairs (desc_thresh, optional Lowe ratio):
+// moves / midx [np][cap], kcount [np].  Shared with the homography path.
+int launch_match_compact(pano_ctx *ctx, const pano_kp *kps, const int32_t *counts, int cap,
+                         const int32_t *fa, const int32_t *fb, int np, const int32_t *best,
+                         const float *d1, const float *d2, double desc_thresh, double ratio,
+                         void *moves, int32_t *midx, int32_t *kcount) {
+    if (np < 1 || np > 256) return pano_fail(ctx, PANO_E_ARG, "match compaction: 1..256 pairs");
+    PairArg pa;
+    for (int q = 0; q < np; ++q) {
+        pa.a[q] = fa[q];
+        pa.b[q] = fb[q];
+    }
+    {
+        PanoProf prof_(ctx, PK_PAIR_SHIFTS);
+        pair_compact<<<np, RB, 0, ctx->stream>>>(kps, nullptr, counts, cap, pa, best, d1, d2,
+                                                desc_thresh > 0 ? (float)desc_thresh : INFINITY,
+                                                ratio > 0 ? ratio * ratio : 0.0,
+                                                (double2 *)moves, midx, kcount);
+    }
+    PANO_LAUNCH_CHECK(ctx, "pair_compact");
+    return PANO_OK;
+}
+
 int launch_ransac_translate(pano_ctx *ctx, const double *moves, int k, double thr,
                             int32_t *out) {
     if (k < 0 || (k > 0 && !moves) || !out) return pano_fail(ctx, PANO_E_ARG, "pano_ransac_translate");
