@@ -316,6 +316,13 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     constexpr bool CENTER = MODE != MODE_BASE;
     static_assert((TY + 2 * R) * (TX / SR) <= 512 && TX * (TY / SC) <= 512, "one item per thread");
     extern __shared__ __attribute__((aligned(16))) float tin[];   // [TY + 2R][IWP]
+#ifdef PANO_BLUR_STAGGER
+    {   // probe: offset the odd residency slots of the first dispatch round
+        const unsigned lb = linear_block_id();
+        if (lb < 1024 && ((lb >> 8) & 1))
+            for (int i = 0; i < PANO_BLUR_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
     const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TY;
     const int f = (int)(tb / (gridDim.x * gridDim.y));
