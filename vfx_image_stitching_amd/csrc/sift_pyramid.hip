@@ -206,11 +206,19 @@ gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t 
 // Register-blocked sliding window: SEG consecutive outputs of one row (or column) from
 // SEG + NT - 1 staged inputs; output j receives taps t = 0..NT-1 in order (the oracle's
 // sequential sum), all index arithmetic compile-time after unrolling.
+#ifndef PANO_BLUR_ABL
+#define PANO_BLUR_ABL 0     // timing ablations of blur_fast only: bit 1 no FMAs, 2 no stores, 4 no loads
+#endif
 template <int NT, int SEG>
 __device__ __forceinline__ void conv_seg(const float *__restrict__ p, int stride,
                                          const double *__restrict__ k, double (&acc)[SEG]) {
 #pragma unroll
     for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
+    if constexpr ((PANO_BLUR_ABL & 1) != 0) {
+#pragma unroll
+        for (int j = 0; j < SEG; ++j) acc[j] = (double)p[(j + NT / 2) * stride];
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < SEG + NT - 1; ++i) {
         const double v = (double)p[i * stride];
@@ -329,7 +337,9 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     const int tw = min(TX, W - x0), th = min(TY, H - y0);
     const int tid = threadIdx.x;
     const int ih = th + 2 * R, iw = tw + 2 * R;
-    if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TX + R <= W && y0 + TY + R <= H)
+    if constexpr ((PANO_BLUR_ABL & 4) != 0) {
+        for (int i = tid; i < (TY + 2 * R) * IWP; i += 512) tin[i] = (float)(i & 255);
+    } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TX + R <= W && y0 + TY + R <= H)
         stage_interior<R, 512>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
     else
         stage_tile<MODE, 8, (TY + 2 * R + 7) / 8>(la, f, H, W, x0, y0, R, ih, iw, IWP, tin);
@@ -369,6 +379,10 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         if (ty >= th) break;
         const float o = (float)acc[j];
         const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + cxp;
+        if constexpr ((PANO_BLUR_ABL & 2) != 0) {
+            if (o == -1.2345f) out[gi] = o + cen[j];          // never true: keeps the work live
+            continue;
+        }
         if (out) out[gi] = o;
         if constexpr (CENTER) {
             if (dog) dog[gi] = o - cen[j];
