@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(256) conv_loop(float *out, Taps taps, int iter
     float s = 0.f;
     for (int it = 0; it < iters; ++it) {
         double acc[SEG];
-        conv_seg<NT, SEG>(p, STRIDE, taps.k, acc);
+        conv_seg<NT, SEG>(p + ((it * 7) & 15) * (STRIDE == 1 ? 97 : 1), STRIDE, taps.k, acc);
 #pragma unroll
         for (int j = 0; j < SEG; ++j) s += (float)acc[j];
     }

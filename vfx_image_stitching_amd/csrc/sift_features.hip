@@ -292,6 +292,131 @@ extrema_scan(DogArgs a, int border, double thresh, uint32_t *__restrict__ raw,
     }
 }
 
+// Streaming form of the same test: one WAVE per item = a 62-column strip of XSR output rows
+// of one octave of one frame.  Lane = column (lanes 0 and 63 are the 1-px halo); the wave
+// walks down the rows with the NL DoG values of PD rows prefetched in registers, forms the
+// horizontal 3-max/min of each level with two lane shifts, keeps the last three rows of those
+// in registers for the vertical 3-max/min, and tests the row behind.  No LDS tile, no block
+// barrier: each wave streams its rows as a chain of coalesced 256-byte loads.  Hits (rare)
+// are gathered in a per-wave LDS buffer and appended with one atomic per flush.
+constexpr int XSW = 62;          // output columns per strip
+constexpr int XSR = 32;          // output rows per item (default; PANO_EXTREMA_XSR=16 halves it)
+constexpr int XPD = 3;           // rows prefetched ahead
+
+struct XArgs {
+    const float *dog[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
+    int H[PANO_MAX_OCTAVES], W[PANO_MAX_OCTAVES];
+    int strips_x[PANO_MAX_OCTAVES];
+    int item_start[PANO_MAX_OCTAVES + 1];
+    int n_oct;
+};
+
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+__device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
+
+template <int NL, int SR>
+__global__ void __launch_bounds__(256)
+extrema_stream(XArgs a, int border, double thresh, uint32_t *__restrict__ raw,
+               int32_t *__restrict__ raw_cnt, int raw_cap, int item_base, int item_end) {
+    constexpr int ni = NL - 2;
+    constexpr int BUF = 64;
+    __shared__ uint32_t kbuf[4][BUF];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int f = blockIdx.y;
+    int t = item_base + (int)blockIdx.x * 4 + wv;
+    if (t >= item_end) return;                                     // whole wave
+    int o = 0;
+    while (o + 1 < a.n_oct && t >= a.item_start[o + 1]) ++o;
+    t -= a.item_start[o];
+    const int H = a.H[o], W = a.W[o];
+    const int x0 = border + (t % a.strips_x[o]) * XSW;
+    const int y0 = border + (t / a.strips_x[o]) * SR;
+    const int yend = min(y0 + SR, H - border);                     // last input row (inclusive)
+    const int x = x0 - 1 + lane;
+    const int gx = min(x, W - 1);
+    const bool out_lane = lane >= 1 && lane <= XSW && x < W - border;
+    const float *p[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) p[l] = a.dog[o][l] + (size_t)f * H * W + gx;
+    int nbuf = 0;                                                   // wave-uniform
+    auto flush = [&]() {
+        if (nbuf == 0) return;
+        __builtin_amdgcn_wave_barrier();
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&raw_cnt[f * kCntStride], nbuf);
+        base = __shfl(base, 0);
+        for (int i = lane; i < nbuf; i += 64)
+            if (base + i < raw_cap) raw[(size_t)f * raw_cap + base + i] = kbuf[wv][i];
+        __builtin_amdgcn_wave_barrier();
+        nbuf = 0;
+    };
+    float nx[XPD][NL];                                              // prefetched rows
+#pragma unroll
+    for (int k = 0; k < XPD; ++k) {
+        const int r = y0 - 1 + k;
+        if (r <= yend) {
+#pragma unroll
+            for (int l = 0; l < NL; ++l) nx[k][l] = p[l][(size_t)r * W];
+        }
+    }
+    float hxA[NL], hnA[NL], hxB[NL], hnB[NL], cB[NL];               // rows r-2 (A), r-1 (B)
+    for (int r0 = y0 - 1; r0 <= yend; r0 += XPD) {
+#pragma unroll
+        for (int k = 0; k < XPD; ++k) {
+            const int r = r0 + k;
+            if (r > yend) break;
+            float c[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) c[l] = nx[k][l];
+            if (r + XPD <= yend) {
+#pragma unroll
+                for (int l = 0; l < NL; ++l) nx[k][l] = p[l][(size_t)(r + XPD) * W];
+            }
+            float hxC[NL], hnC[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                const float lf = __shfl_up(c[l], 1), rt = __shfl_down(c[l], 1);
+                hxC[l] = max3f(lf, c[l], rt);
+                hnC[l] = min3f(lf, c[l], rt);
+            }
+            if (r >= y0 + 1) {                                      // test output row r - 1
+                float vx[NL], vn[NL];
+#pragma unroll
+                for (int l = 0; l < NL; ++l) {
+                    vx[l] = max3f(hxA[l], hxB[l], hxC[l]);
+                    vn[l] = min3f(hnA[l], hnB[l], hnC[l]);
+                }
+#pragma unroll
+                for (int L = 1; L <= ni; ++L) {
+                    const float v = cB[L];
+                    bool ext = false;
+                    if (out_lane && (double)fabsf(v) > thresh)
+                        ext = v > 0 ? v >= max3f(vx[L - 1], vx[L], vx[L + 1])
+                                    : v <= min3f(vn[L - 1], vn[L], vn[L + 1]);
+                    const unsigned long long m = __ballot(ext);
+                    if (m) {                                        // wave-uniform
+                        const int k2 = __popcll(m);
+                        if (nbuf + k2 > BUF) flush();
+                        if (ext) {
+                            const int pos = nbuf + __popcll(m & ((1ull << lane) - 1));
+                            kbuf[wv][pos] = scan_key(o, L, r - 1, x);
+                        }
+                        nbuf += k2;
+                    }
+                }
+            }
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                hxA[l] = hxB[l]; hnA[l] = hnB[l];
+                hxB[l] = hxC[l]; hnB[l] = hnC[l];
+                cB[l] = c[l];
+            }
+        }
+    }
+    flush();
+}
+
 __device__ __forceinline__ float dog_at(const DogArgs &a, int o, int lvl, int f, int y, int x) {
     return a.dog[o][lvl][((size_t)f * a.H[o] + y) * a.W[o] + x];
 }
@@ -1149,14 +1274,59 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     da.tile_start[no] = tiles;
     if (ctx->h * 2 > 4095 || ctx->w * 2 > 4095)
         return pano_fail(ctx, PANO_E_UNSUPPORTED, "frames above 2047 px need a wider scan key");
+    // Extrema: the streaming kernel for the large octaves (a wave walks 32 rows of a strip),
+    // the LDS-tiled scan for the small ones (few rows: more, shorter workgroups win); the
+    // octaves of a pending blur tail are scanned after the join.
+    static const int xsr = [] {
+        const char *e = getenv("PANO_EXTREMA_XSR");
+        return e && atoi(e) == 16 ? 16 : XSR;
+    }();
+    static const int xmin_h = [] {
+        const char *e = getenv("PANO_EXTREMA_STREAM_MIN_H");   // 0 disables the streaming kernel
+        return e ? atoi(e) : 192;
+    }();
     if (tiles > 0) {
-        // large octaves first (overlapping a pending blur tail on the side stream), then
-        // join and scan the tail octaves
-        const int split = ctx->tail_pending ? da.tile_start[ctx->o_tail] : tiles;
-        for (int part = 0; part < 2; ++part) {
-            const int t0 = part == 0 ? 0 : split, t1 = part == 0 ? split : tiles;
-            if (part == 1) sift_join_tail(ctx);
-            if (t1 <= t0) continue;
+        XArgs xa{};
+        int items = 0;
+        xa.n_oct = no;
+        for (int o = 0; o < no; ++o) {
+            xa.H[o] = da.H[o];
+            xa.W[o] = da.W[o];
+            for (int l = 0; l < nl - 1; ++l) xa.dog[o][l] = da.dog[o][l];
+            const int iw = da.W[o] - 2 * p->border, ih = da.H[o] - 2 * p->border;
+            xa.item_start[o] = items;
+            xa.strips_x[o] = iw > 0 ? (iw + XSW - 1) / XSW : 1;
+            if (iw > 0 && ih > 0) items += xa.strips_x[o] * ((ih + xsr - 1) / xsr);
+        }
+        xa.item_start[no] = items;
+        const int o_split = ctx->tail_pending ? ctx->o_tail : no;
+        int o_s = 0;
+        while (xmin_h > 0 && o_s < o_split && da.H[o_s] >= xmin_h) ++o_s;
+        auto launch_stream = [&](int t0, int t1) -> int {
+            if (t1 <= t0) return PANO_OK;
+            dim3 grid((unsigned)((t1 - t0 + 3) / 4), n);
+            {
+                PanoProf prof_(ctx, PK_EXTREMA);
+#define PANO_EXTREMA(NLV)                                                                          \
+    (xsr == 16 ? extrema_stream<NLV, 16><<<grid, 256, 0, ctx->stream>>>(xa, p->border, lp.thresh, raw_ext, \
+                                                                      ext_cnt, (int)ext_cap, t0, t1)  \
+               : extrema_stream<NLV, XSR><<<grid, 256, 0, ctx->stream>>>(xa, p->border, lp.thresh, raw_ext, \
+                                                                       ext_cnt, (int)ext_cap, t0, t1))
+                switch (ni + 2) {
+                    case 3: PANO_EXTREMA(3); break;
+                    case 4: PANO_EXTREMA(4); break;
+                    case 5: PANO_EXTREMA(5); break;
+                    case 6: PANO_EXTREMA(6); break;
+                    case 7: PANO_EXTREMA(7); break;
+                    default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "num_intervals above 5");
+                }
+#undef PANO_EXTREMA
+            }
+            PANO_LAUNCH_CHECK(ctx, "extrema_stream");
+            return PANO_OK;
+        };
+        auto launch_scan = [&](int t0, int t1) -> int {
+            if (t1 <= t0) return PANO_OK;
             dim3 grid(t1 - t0, n);
             {
                 PanoProf prof_(ctx, PK_EXTREMA);
@@ -1173,7 +1343,15 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
 #undef PANO_EXTREMA
             }
             PANO_LAUNCH_CHECK(ctx, "extrema_scan");
-        }
+            return PANO_OK;
+        };
+        rc = launch_stream(0, xa.item_start[o_s]);
+        if (rc) return rc;
+        rc = launch_scan(da.tile_start[o_s], da.tile_start[o_split]);
+        if (rc) return rc;
+        sift_join_tail(ctx);
+        rc = launch_scan(da.tile_start[o_split], tiles);
+        if (rc) return rc;
         dim3 g2((unsigned)((ext_cap + 255) / 256), n);
         {
             PanoProf prof_(ctx, PK_EXTREMA);

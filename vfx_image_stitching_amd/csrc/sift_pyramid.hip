@@ -218,6 +218,65 @@ __device__ __forceinline__ void stage_interior(const float *__restrict__ plane, 
     }
 }
 
+// Interior tiles of MODE_BASE (the x2 INTER_LINEAR source window lies inside the gray frame,
+// no reflection, no clamping): the tile's gray source patch (<= 47 x 47 bytes) is loaded once
+// into LDS as floats, then every staged element is the same f32 bilinear expression as
+// Stager<MODE_BASE>::get over four LDS reads instead of four byte loads from global memory.
+constexpr int kPatch = 48;                 // patch rows / columns capacity
+constexpr int kPatchP = kPatch + 1;        // odd pitch
+template <int R, int NTHR>
+__device__ __forceinline__ void stage_base_interior(const LoadArgs &la, int f, int x0, int y0, int IWP,
+                                                    float *t, float *patch) {
+    constexpr int IW = TX + 2 * R, IH = TY + 2 * R;
+    static_assert(IH / 2 + 3 <= kPatch, "patch capacity");
+    const uint8_t *fr = la.gray + (size_t)f * la.sh * la.sw;
+    int p0, p1, q0, q1;
+    float w_unused;
+    lin_map(y0 - R, la.sh, p0, p1, w_unused);               // first source row / column
+    lin_map(x0 - R, la.sw, q0, q1, w_unused);
+    const int np = IH / 2 + 3, nq = IW / 2 + 3;             // covers the window (+ slack)
+    for (int i = threadIdx.x; i < np * kPatch; i += NTHR) {
+        const int r = i / kPatch, c = i - r * kPatch;
+        if (c < nq && p0 + r < la.sh && q0 + c < la.sw)       // slack rows past the frame: unread
+            patch[r * kPatchP + c] = (float)fr[(size_t)(p0 + r) * la.sw + q0 + c];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int NW = NTHR / 64;
+    // per-lane columns (lane, 64 + lane): patch column of c0 and the weight of c1
+    int cA, cB;
+    float wA, wB;
+    {
+        int a0, a1;
+        lin_map(x0 - R + lane, la.sw, a0, a1, wA);
+        cA = a0 - q0;
+        const int xb = 64 + lane < IW ? 64 + lane : lane;
+        lin_map(x0 - R + xb, la.sw, a0, a1, wB);
+        cB = a0 - q0;
+    }
+    for (int ty = wv; ty < IH; ty += NW) {
+        int r0, r1;
+        float wy;
+        lin_map(y0 - R + ty, la.sh, r0, r1, wy);
+        const float *P0 = patch + (r0 - p0) * kPatchP, *P1 = P0 + kPatchP;
+        {
+            const float g00 = P0[cA], g01 = P0[cA + 1], g10 = P1[cA], g11 = P1[cA + 1];
+            const float wx0 = 1.0f - wA;
+            const float h0 = g00 * wx0 + g01 * wA;
+            const float h1 = g10 * wx0 + g11 * wA;
+            t[ty * IWP + lane] = h0 * (1.0f - wy) + h1 * wy;
+        }
+        if (64 + lane < IW) {
+            const float g00 = P0[cB], g01 = P0[cB + 1], g10 = P1[cB], g11 = P1[cB + 1];
+            const float wx0 = 1.0f - wB;
+            const float h0 = g00 * wx0 + g01 * wB;
+            const float h1 = g10 * wx0 + g11 * wB;
+            t[ty * IWP + 64 + lane] = h0 * (1.0f - wy) + h1 * wy;
+        }
+    }
+}
+
 // cvtColor(BGR2GRAY) of every frame, 4 pixels per thread (sift_impl.py:27-28).
 __global__ void __launch_bounds__(256)
 gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t npx) {
@@ -377,6 +436,8 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         for (int i = tid; i < (TY + 2 * R) * IWP; i += 512) tin[i] = (float)(i & 255);
     } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TX + R <= W && y0 + TY + R <= H)
         stage_interior<R, 512>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
+    else if (MODE == MODE_BASE && x0 - R >= 2 && y0 - R >= 2 && x0 + TX + R <= W - 2 && y0 + TY + R <= H - 2)
+        stage_base_interior<R, 512>(la, f, x0, y0, IWP, tin, tin + (TY + 2 * R) * IWP);
     else
         stage_tile<MODE, 8, (TY + 2 * R + 7) / 8>(la, f, H, W, x0, y0, R, ih, iw, IWP, tin);
     __syncthreads();
@@ -752,7 +813,8 @@ int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, fl
             return band == 32 ? go(std::integral_constant<int, 32>{}) : go(std::integral_constant<int, 64>{});
         }
         constexpr int R = (NT - 1) / 2;
-        const size_t sm = (size_t)(TY + 2 * R) * ((TX + 2 * R) | 1) * sizeof(float);
+        const size_t sm = (size_t)((TY + 2 * R) * ((TX + 2 * R) | 1) + (MODE == MODE_BASE ? kPatch * kPatchP : 0)) *
+                          sizeof(float);
         {
             PanoProf prof_(ctx, PK_BLUR);
             blur_fast<MODE, NT><<<grid, 512, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
