@@ -143,43 +143,7 @@ __device__ __forceinline__ void stage_tile(const LoadArgs &la, int f, int H, int
     for (int k = 0; k < RPW; ++k) {
         const int ty = wv + NW * k;
         if (ty < ih) {
-            if (lane < iw) t[ty * IWP + lane] = v0[k];   // iw < 64: a narrow band's row
-            if (has1) t[ty * IWP + 64 + lane] = v1[k];
-        }
-    }
-}
-
-// stage_tile in two halves (software pipelining: the loads of the next band are in flight
-// during the current band's passes).  TWO = false when iw <= 64 (one column per lane).
-template <int MODE, int NW, int RPW, bool TWO>
-__device__ __forceinline__ void stage_load(const LoadArgs &la, int f, int H, int W, int x0, int y0,
-                                           int R, int ih, int iw, float (&v0)[RPW], float (&v1)[RPW]) {
-    const Stager<MODE> sg(la, f, H, W);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool has1 = TWO && 64 + lane < iw;
-    const ColMap m0 = sg.col(x0 - R + lane);
-    const ColMap m1 = sg.col(x0 - R + (has1 ? 64 + lane : lane));
-#pragma unroll
-    for (int k = 0; k < RPW; ++k) {
-        const int ty = wv + NW * k;
-        if (ty < ih) {
-            v0[k] = sg.get(y0 - R + ty, m0);
-            if (TWO) v1[k] = has1 ? sg.get(y0 - R + ty, m1) : 0.0f;
-        }
-    }
-}
-template <int NW, int RPW, bool TWO>
-__device__ __forceinline__ void stage_store(int ih, int iw, int IWP, float *t, const float (&v0)[RPW],
-                                            const float (&v1)[RPW]) {
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool has1 = TWO && 64 + lane < iw;
-#pragma unroll
-    for (int k = 0; k < RPW; ++k) {
-        const int ty = wv + NW * k;
-        if (ty < ih) {
-            if (lane < iw) t[ty * IWP + lane] = v0[k];
+            if (lane < iw) t[ty * IWP + lane] = v0[k];   // iw < 64 (narrow tile): stay in the row
             if (has1) t[ty * IWP + 64 + lane] = v1[k];
         }
     }
@@ -419,13 +383,6 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     constexpr bool CENTER = MODE != MODE_BASE;
     static_assert((TY + 2 * R) * (TX / SR) <= 512 && TX * (TY / SC) <= 512, "one item per thread");
     extern __shared__ __attribute__((aligned(16))) float tin[];   // [TY + 2R][IWP]
-#ifdef PANO_BLUR_STAGGER
-    {   // probe: offset the odd residency slots of the first dispatch round
-        const unsigned lb = linear_block_id();
-        if (lb < 1024 && ((lb >> 8) & 1))
-            for (int i = 0; i < PANO_BLUR_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
     const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
     const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TY;
     const int f = (int)(tb / (gridDim.x * gridDim.y));
@@ -484,105 +441,6 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         if constexpr (CENTER) {
             if (dog) dog[gi] = o - cen[j];
             if (in_copy) in_copy[gi] = cen[j];
-        }
-    }
-}
-
-// Band walker: a workgroup owns a SW-column strip of one frame over a segment of output rows
-// and walks down it in bands of BH = 64 row-pass rows.  Per band: stage the band's input rows
-// (SW + 2R columns) in LDS; row pass with every thread busy (thread = (row, 8-column segment))
-// into a row buffer that also holds the previous band's last 2R row-pass rows; column pass
-// (thread = (column, 8-row segment)) to HBM; carry the last 2R rows to the top of the buffer.
-// Each output gets exactly NT row-pass and NT column-pass FMAs (blur_fast recomputes the
-// row pass of a 2R-row halo per 64 x 64 tile, and leaves 2-3 of its 8 waves idle in it);
-// only the first band of a segment repeats the 2R halo rows.  Same arithmetic per output as
-// blur_fast: sequential fma in tap order in double, one f32 rounding per pass.
-constexpr int BBH = 64;   // row-pass rows per band
-
-template <int NT, int SW> struct BandGeom {
-    static constexpr int R = (NT - 1) / 2, C = 2 * R, NTHR = SW * 8;
-    static constexpr int IWP = (SW + 2 * R) | 1;   // staged input band pitch (odd)
-    static constexpr int BP = SW + 1;              // row buffer pitch (odd)
-    static constexpr int BR = C + BBH;             // row buffer rows
-    static constexpr size_t smem = (size_t)(BBH * IWP + BR * BP) * sizeof(float);
-    // output rows per segment: a whole number of bands after the first band's halo
-    static int seg_rows(int H, int k) { return BBH * k - C; }
-};
-
-template <int MODE, int NT, int SW>
-__global__ void __launch_bounds__(SW * 8, SW == 64 ? 6 : 5)
-blur_band(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
-          float *__restrict__ in_copy, int H, int W, int seg_rows, Taps taps) {
-    using G = BandGeom<NT, SW>;
-    constexpr int R = G::R, C = G::C, NTHR = G::NTHR, IWP = G::IWP, BP = G::BP;
-    constexpr int NW = NTHR / 64;
-    constexpr bool CENTER = MODE != MODE_BASE;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float *tin = smem;                  // [BBH][IWP]
-    float *buf = smem + BBH * IWP;      // [BR][BP]: row-pass rows base - C .. base + BBH - 1
-    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
-    const int sx = (int)(tb % gridDim.x), sy = (int)((tb / gridDim.x) % gridDim.y);
-    const int f = (int)(tb / (gridDim.x * gridDim.y));
-    const int x0 = sx * SW, tw = min(SW, W - x0);
-    const int s0 = sy * seg_rows, s1 = min(H, s0 + seg_rows);
-    if (s0 >= s1) return;                                   // whole workgroup
-    const int tid = threadIdx.x;
-    const int nchunk = (s1 - s0 + C + BBH - 1) / BBH;
-    // row-pass item: row rr of the band, columns 8 rseg .. 8 rseg + 7
-    const int rr = tid % BBH, rseg = tid / BBH;
-    // column-pass item: column cx, output rows 8 cs .. 8 cs + 7 of the band's output window
-    const int cx = tid % SW, cs = tid / SW;
-    const Stager<MODE> sg(la, f, H, W);
-    const ColMap cm = sg.col(x0 + min(cx, tw - 1));
-    constexpr int RPW = BBH / NW;
-    constexpr bool TWO = SW + 2 * R > 64;
-    float v0[RPW], v1[RPW];
-    stage_load<MODE, NW, RPW, TWO>(la, f, H, W, x0, s0, R, BBH, tw + 2 * R, v0, v1);
-    for (int c = 0; c < nchunk; ++c) {
-        const int base = s0 - R + BBH * c;                  // first row-pass row of this band
-        stage_store<NW, RPW, TWO>(BBH, tw + 2 * R, IWP, tin, v0, v1);
-        __syncthreads();
-        if (c + 1 < nchunk)                                 // next band's loads in flight
-            stage_load<MODE, NW, RPW, TWO>(la, f, H, W, x0, base + BBH + R, R, BBH, tw + 2 * R, v0, v1);
-        // DoG centres of this band's column-pass outputs, loaded ahead of the passes
-        float cen[8];
-        if constexpr (CENTER) {
-            if (dog || in_copy) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int y = base - R + cs * 8 + j;
-                    cen[j] = sg.get(y < s0 ? s0 : (y < s1 ? y : s1 - 1), cm);
-                }
-            }
-        }
-        if (rseg * 8 < tw) {
-            double acc[8];
-            conv_seg<NT, 8>(tin + rr * IWP + rseg * 8, 1, taps.k, acc);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) buf[(C + rr) * BP + rseg * 8 + j] = (float)acc[j];
-        }
-        __syncthreads();
-        if (cx < tw) {
-            double acc[8];
-            conv_seg<NT, 8>(buf + cs * 8 * BP + cx, BP, taps.k, acc);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int y = base - R + cs * 8 + j;        // output row (buffer row cs*8+j+R)
-                if (y < s0 || y >= s1) continue;
-                const float o = (float)acc[j];
-                const size_t gi = ((size_t)f * H + y) * W + x0 + cx;
-                if (out) out[gi] = o;
-                if constexpr (CENTER) {
-                    if (dog) dog[gi] = o - cen[j];
-                    if (in_copy) in_copy[gi] = cen[j];
-                }
-            }
-        }
-        __syncthreads();
-        // carry the last C row-pass rows to the top (the next band's staging touches only tin)
-        for (int i = tid; i < C * SW; i += NTHR) {
-            const int r = i / SW, x = i - r * SW;
-            buf[r * BP + x] = buf[(BBH + r) * BP + x];
         }
     }
 }
@@ -787,31 +645,7 @@ template <int MODE, int NT>
 int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float *in_copy,
                    int n, int H, int W, const Taps &t) {
     dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
-    static const int band = [] {
-        const char *e = getenv("PANO_BLUR_BAND");   // 0: blur_fast tiles; 32 / 64: band strip width
-        return e ? atoi(e) : 0;
-    }();
-    static const int band_k = [] {
-        const char *e = getenv("PANO_BLUR_BAND_K");  // bands per segment
-        return e ? atoi(e) : 3;
-    }();
     if constexpr (NT > 0) {
-        if (band == 32 || band == 64) {
-            auto go = [&](auto sw_tag) -> int {
-                constexpr int SW = decltype(sw_tag)::value;
-                using BG = BandGeom<NT, SW>;
-                const int seg = std::max(1, BG::seg_rows(H, std::max(1, band_k)));
-                dim3 g((W + SW - 1) / SW, (H + seg - 1) / seg, n);
-                {
-                    PanoProf prof_(ctx, PK_BLUR);
-                    blur_band<MODE, NT, SW><<<g, SW * 8, BG::smem, ctx->stream>>>(la, out, dog, in_copy, H, W,
-                                                                                 seg, t);
-                }
-                PANO_LAUNCH_CHECK(ctx, "blur_band");
-                return PANO_OK;
-            };
-            return band == 32 ? go(std::integral_constant<int, 32>{}) : go(std::integral_constant<int, 64>{});
-        }
         constexpr int R = (NT - 1) / 2;
         const size_t sm = (size_t)((TY + 2 * R) * ((TX + 2 * R) | 1) + (MODE == MODE_BASE ? kPatch * kPatchP : 0)) *
                           sizeof(float);
