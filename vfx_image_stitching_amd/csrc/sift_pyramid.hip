@@ -153,10 +153,10 @@ __device__ __forceinline__ void stage_tile(const LoadArgs &la, int f, int H, int
 // the plane, W % 4 == 0): 16-byte aligned loads over the 4-aligned superset of each row,
 // scattered into the same LDS layout as stage_tile.  A quarter of the load instructions and
 // no per-row reflection arithmetic (the interior is ~80 % of the tiles at octave 0).
-template <int R, int NTHR>
+template <int R, int NTHR, int TYT = TY>
 __device__ __forceinline__ void stage_interior(const float *__restrict__ plane, int W, int x0, int y0,
                                                int IWP, float *t) {
-    constexpr int IW = TX + 2 * R, IH = TY + 2 * R;
+    constexpr int IW = TX + 2 * R, IH = TYT + 2 * R;
     const int xa = (x0 - R) & ~3, off = (x0 - R) - xa;    // off in 0..3, wave-uniform
     const int nq = (off + IW + 3) >> 2;                   // float4 per row
     constexpr int MAXQ = (IH * ((IW + 6) / 4) + NTHR - 1) / NTHR;
@@ -186,13 +186,14 @@ __device__ __forceinline__ void stage_interior(const float *__restrict__ plane, 
 // no reflection, no clamping): the tile's gray source patch (<= 47 x 47 bytes) is loaded once
 // into LDS as floats, then every staged element is the same f32 bilinear expression as
 // Stager<MODE_BASE>::get over four LDS reads instead of four byte loads from global memory.
-constexpr int kPatch = 48;                 // patch rows / columns capacity
+constexpr int kPatch = 48;                 // patch columns capacity
 constexpr int kPatchP = kPatch + 1;        // odd pitch
-template <int R, int NTHR>
+constexpr int kPatchR = 72;                // patch rows capacity
+template <int R, int NTHR, int TYT = TY>
 __device__ __forceinline__ void stage_base_interior(const LoadArgs &la, int f, int x0, int y0, int IWP,
                                                     float *t, float *patch) {
-    constexpr int IW = TX + 2 * R, IH = TY + 2 * R;
-    static_assert(IH / 2 + 3 <= kPatch, "patch capacity");
+    constexpr int IW = TX + 2 * R, IH = TYT + 2 * R;
+    static_assert(IH / 2 + 3 <= kPatchR && IW / 2 + 3 <= kPatch, "patch capacity");
     const uint8_t *fr = la.gray + (size_t)f * la.sh * la.sw;
     int p0, p1, q0, q1;
     float w_unused;
@@ -373,30 +374,35 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
 // writes its SR outputs over them); the column pass (SC outputs per thread, all 512 threads
 // busy) writes level, DoG and level-0 copy.  Half the LDS of a two-tile design, twice the
 // waves per CU; per output the arithmetic is blur_level's (sequential fma in tap order).
-template <int MODE, int NT>
+// Tile height per tap count: the row pass has (TYT + 2R) x 4 items and the column pass
+// 64 x TYT / SC, so TYT + 2R ~ 128 keeps all 8 waves busy in both passes (a 64-row tile
+// leaves 2-3 waves idle in the row pass) and cuts the row-pass halo from 2R/64 to ~2R/100.
+constexpr int tall_rows(int NT) { return ((128 - (NT - 1)) / 8) * 8; }
+
+template <int MODE, int NT, int TYT = TY>
 __global__ void __launch_bounds__(512, 6)
 blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
           float *__restrict__ in_copy, int H, int W, Taps taps) {
     constexpr int R = (NT - 1) / 2;
     constexpr int IWP = (TX + 2 * R) | 1;
-    constexpr int SR = 16, SC = 8;
+    constexpr int SR = 16, SC = TYT / 8;
     constexpr bool CENTER = MODE != MODE_BASE;
-    static_assert((TY + 2 * R) * (TX / SR) <= 512 && TX * (TY / SC) <= 512, "one item per thread");
-    extern __shared__ __attribute__((aligned(16))) float tin[];   // [TY + 2R][IWP]
+    static_assert((TYT + 2 * R) * (TX / SR) <= 512 && TX * (TYT / SC) <= 512 && TYT % 8 == 0, "one item per thread");
+    extern __shared__ __attribute__((aligned(16))) float tin[];   // [TYT + 2R][IWP]
     const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
-    const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TY;
+    const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TYT;
     const int f = (int)(tb / (gridDim.x * gridDim.y));
-    const int tw = min(TX, W - x0), th = min(TY, H - y0);
+    const int tw = min(TX, W - x0), th = min(TYT, H - y0);
     const int tid = threadIdx.x;
     const int ih = th + 2 * R, iw = tw + 2 * R;
     if constexpr ((PANO_BLUR_ABL & 4) != 0) {
-        for (int i = tid; i < (TY + 2 * R) * IWP; i += 512) tin[i] = (float)(i & 255);
-    } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TX + R <= W && y0 + TY + R <= H)
-        stage_interior<R, 512>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
-    else if (MODE == MODE_BASE && x0 - R >= 2 && y0 - R >= 2 && x0 + TX + R <= W - 2 && y0 + TY + R <= H - 2)
-        stage_base_interior<R, 512>(la, f, x0, y0, IWP, tin, tin + (TY + 2 * R) * IWP);
+        for (int i = tid; i < (TYT + 2 * R) * IWP; i += 512) tin[i] = (float)(i & 255);
+    } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TX + R <= W && y0 + TYT + R <= H)
+        stage_interior<R, 512, TYT>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
+    else if (MODE == MODE_BASE && x0 - R >= 2 && y0 - R >= 2 && x0 + TX + R <= W - 2 && y0 + TYT + R <= H - 2)
+        stage_base_interior<R, 512, TYT>(la, f, x0, y0, IWP, tin, tin + (TYT + 2 * R) * IWP);
     else
-        stage_tile<MODE, 8, (TY + 2 * R + 7) / 8>(la, f, H, W, x0, y0, R, ih, iw, IWP, tin);
+        stage_tile<MODE, 8, (TYT + 2 * R + 7) / 8>(la, f, H, W, x0, y0, R, ih, iw, IWP, tin);
     __syncthreads();
     // column-pass item of this thread and its centres (before the row pass overwrites them)
     const int nrs = (th + SC - 1) / SC;
@@ -645,13 +651,27 @@ template <int MODE, int NT>
 int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float *in_copy,
                    int n, int H, int W, const Taps &t) {
     dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
+    static const bool tall = [] {
+        const char *e = getenv("PANO_BLUR_TALL");   // 1 (default): tall tiles; 0: 64 x 64 tiles
+        return e ? atoi(e) != 0 : true;
+    }();
     if constexpr (NT > 0) {
         constexpr int R = (NT - 1) / 2;
-        const size_t sm = (size_t)((TY + 2 * R) * ((TX + 2 * R) | 1) + (MODE == MODE_BASE ? kPatch * kPatchP : 0)) *
+        constexpr int TYT = tall_rows(NT);
+        // tall tiles only where they still leave >= 6 workgroups per CU (octave 0 of a batch):
+        // on smaller planes the lost parallelism costs more than the halo saves
+        const bool use_tall = tall && (long)grid.x * ((H + TYT - 1) / TYT) * n >= 1536;
+        const int ty = use_tall ? TYT : TY;
+        const size_t sm = (size_t)((ty + 2 * R) * ((TX + 2 * R) | 1) + (MODE == MODE_BASE ? kPatchR * kPatchP : 0)) *
                           sizeof(float);
         {
             PanoProf prof_(ctx, PK_BLUR);
-            blur_fast<MODE, NT><<<grid, 512, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+            if (use_tall) {
+                grid.y = (H + TYT - 1) / TYT;
+                blur_fast<MODE, NT, TYT><<<grid, 512, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+            } else {
+                blur_fast<MODE, NT, TY><<<grid, 512, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+            }
         }
         PANO_LAUNCH_CHECK(ctx, "blur_fast");
     } else {
