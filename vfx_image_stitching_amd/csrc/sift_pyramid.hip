@@ -153,10 +153,10 @@ __device__ __forceinline__ void stage_tile(const LoadArgs &la, int f, int H, int
 // the plane, W % 4 == 0): 16-byte aligned loads over the 4-aligned superset of each row,
 // scattered into the same LDS layout as stage_tile.  A quarter of the load instructions and
 // no per-row reflection arithmetic (the interior is ~80 % of the tiles at octave 0).
-template <int R, int NTHR, int TYT = TY>
+template <int R, int NTHR, int TYT = TY, int TXT = TX>
 __device__ __forceinline__ void stage_interior(const float *__restrict__ plane, int W, int x0, int y0,
                                                int IWP, float *t) {
-    constexpr int IW = TX + 2 * R, IH = TYT + 2 * R;
+    constexpr int IW = TXT + 2 * R, IH = TYT + 2 * R;
     const int xa = (x0 - R) & ~3, off = (x0 - R) - xa;    // off in 0..3, wave-uniform
     const int nq = (off + IW + 3) >> 2;                   // float4 per row
     constexpr int MAXQ = (IH * ((IW + 6) / 4) + NTHR - 1) / NTHR;
@@ -379,30 +379,37 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
 // leaves 2-3 waves idle in the row pass) and cuts the row-pass halo from 2R/64 to ~2R/100.
 constexpr int tall_rows(int NT) { return ((128 - (NT - 1)) / 8) * 8; }
 
-template <int MODE, int NT, int TYT = TY>
-__global__ void __launch_bounds__(512, 6)
+// Small planes (octaves 2-3 of a batch: a few hundred tiles) are latency-bound, not FMA-
+// bound: blur_fast<..., 32, 256> uses 32 x 32 tiles of 256 threads with 8 row-pass and 4
+// column-pass outputs per thread -- a quarter of the serial FMA chain per thread and 4x the
+// workgroups of the 64 x 64 form.
+template <int MODE, int NT, int TYT = TY, int TXT = TX, int NTHR = 512>
+__global__ void __launch_bounds__(NTHR, 6)
 blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
           float *__restrict__ in_copy, int H, int W, Taps taps) {
     constexpr int R = (NT - 1) / 2;
-    constexpr int IWP = (TX + 2 * R) | 1;
-    constexpr int SR = 16, SC = TYT / 8;
+    constexpr int IWP = (TXT + 2 * R) | 1;
+    constexpr int SR = TXT == 64 ? 16 : 8, SC = TYT * TXT / NTHR;
     constexpr bool CENTER = MODE != MODE_BASE;
-    static_assert((TYT + 2 * R) * (TX / SR) <= 512 && TX * (TYT / SC) <= 512 && TYT % 8 == 0, "one item per thread");
+    static_assert((TYT + 2 * R) * (TXT / SR) <= NTHR && TXT * (TYT / SC) <= NTHR && TYT % SC == 0,
+                  "one item per thread");
     extern __shared__ __attribute__((aligned(16))) float tin[];   // [TYT + 2R][IWP]
     const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
-    const int x0 = (int)(tb % gridDim.x) * TX, y0 = (int)((tb / gridDim.x) % gridDim.y) * TYT;
+    const int x0 = (int)(tb % gridDim.x) * TXT, y0 = (int)((tb / gridDim.x) % gridDim.y) * TYT;
     const int f = (int)(tb / (gridDim.x * gridDim.y));
-    const int tw = min(TX, W - x0), th = min(TYT, H - y0);
+    const int tw = min(TXT, W - x0), th = min(TYT, H - y0);
     const int tid = threadIdx.x;
     const int ih = th + 2 * R, iw = tw + 2 * R;
     if constexpr ((PANO_BLUR_ABL & 4) != 0) {
-        for (int i = tid; i < (TYT + 2 * R) * IWP; i += 512) tin[i] = (float)(i & 255);
-    } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TX + R <= W && y0 + TYT + R <= H)
-        stage_interior<R, 512, TYT>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
-    else if (MODE == MODE_BASE && x0 - R >= 2 && y0 - R >= 2 && x0 + TX + R <= W - 2 && y0 + TYT + R <= H - 2)
-        stage_base_interior<R, 512, TYT>(la, f, x0, y0, IWP, tin, tin + (TYT + 2 * R) * IWP);
+        for (int i = tid; i < (TYT + 2 * R) * IWP; i += NTHR) tin[i] = (float)(i & 255);
+    } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TXT + R <= W && y0 + TYT + R <= H)
+        stage_interior<R, NTHR, TYT, TXT>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
+    else if (TXT == TX && MODE == MODE_BASE && x0 - R >= 2 && y0 - R >= 2 && x0 + TX + R <= W - 2 &&
+             y0 + TYT + R <= H - 2)
+        stage_base_interior<R, NTHR, TYT>(la, f, x0, y0, IWP, tin, tin + (TYT + 2 * R) * IWP);
     else
-        stage_tile<MODE, 8, (TYT + 2 * R + 7) / 8>(la, f, H, W, x0, y0, R, ih, iw, IWP, tin);
+        stage_tile<MODE, NTHR / 64, (TYT + 2 * R + NTHR / 64 - 1) / (NTHR / 64)>(la, f, H, W, x0, y0, R, ih, iw,
+                                                                             IWP, tin);
     __syncthreads();
     // column-pass item of this thread and its centres (before the row pass overwrites them)
     const int nrs = (th + SC - 1) / SC;
@@ -655,8 +662,22 @@ int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, fl
         const char *e = getenv("PANO_BLUR_TALL");   // 1 (default): tall tiles; 0: 64 x 64 tiles
         return e ? atoi(e) != 0 : true;
     }();
+    static const int small_tiles = [] {
+        const char *e = getenv("PANO_BLUR_SMALL");   // planes with fewer 64x64 tiles use 32x32 tiles
+        return e ? atoi(e) : 300;                   // measured: octave 3 of parrington gains, 1-2 do not
+    }();
     if constexpr (NT > 0) {
         constexpr int R = (NT - 1) / 2;
+        if ((long)grid.x * grid.y * n < small_tiles) {
+            const size_t sm = (size_t)(32 + 2 * R) * ((32 + 2 * R) | 1) * sizeof(float);
+            dim3 g((W + 31) / 32, (H + 31) / 32, n);
+            {
+                PanoProf prof_(ctx, PK_BLUR);
+                blur_fast<MODE, NT, 32, 32, 256><<<g, 256, sm, ctx->stream>>>(la, out, dog, in_copy, H, W, t);
+            }
+            PANO_LAUNCH_CHECK(ctx, "blur_fast");
+            return PANO_OK;
+        }
         constexpr int TYT = tall_rows(NT);
         // tall tiles only where they still leave >= 6 workgroups per CU (octave 0 of a batch):
         // on smaller planes the lost parallelism costs more than the halo saves
