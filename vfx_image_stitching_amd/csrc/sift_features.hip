@@ -927,18 +927,8 @@ constexpr int kHist = 6 * 6 * 8;      // padded histogram (reference: tensor of 
 constexpr float kFix = 4194304.0f;    // 2^22: contributions <= 255 sqrt(2) fit a u32
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
-                                      // 3: sample taps from one cached location)
+                                      // 3: every sample's taps from one cached location)
 #endif
-
-__device__ __forceinline__ float rfl_f(float v) {
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-__device__ __forceinline__ double rfl_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
 
 // Frame of dense keypoint index gk (frames' keypoints back to back, counts clamped to
 // [0, cap]): chunked wave scan of the counts; false when gk is past the last keypoint.
@@ -1003,9 +993,6 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         if (lane == 0) gk = atomicAdd(wq, 1);
         gk = lo_k + __shfl(gk, 0);
         if (gk >= hi_k || !locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
-        // every per-keypoint quantity is wave-uniform: keep it in scalar registers
-        f = __builtin_amdgcn_readfirstlane(f);
-        k = __builtin_amdgcn_readfirstlane(k);
         for (int i = lane; i < kHist; i += 64) h[i] = 0ull;
         const pano_kp kp = kps[(size_t)f * cap + k];
         int oct = kp.octave & 255;
@@ -1024,14 +1011,14 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         const double hwd = (double)hw, inv_hw = 1.0 / hwd;
         int half = (int)rint(hwd * 1.4142135623730951 * 5.0 * 0.5);
         const int diag = (int)sqrt((double)(rows * rows + cols * cols));
-        half = __builtin_amdgcn_readfirstlane(half < diag ? half : diag);
+        half = half < diag ? half : diag;
         const int side = 2 * half + 1;
         // ob = remainder((ori - angle) * 8 / 360, 8): one bin is one octant (45 deg), so with
         // the gradient angle in octants ob = ori8 - angle * 8 / 360 (mod 8)
-        const float a8 = rfl_f((float)(angle * (8.0 / 360.0)));
+        const float a8 = (float)(angle * (8.0 / 360.0));
         // rbin = ys (cos / hw) + (xs sin / hw + 1.5), cbin = ys (-sin / hw) + (xs cos / hw + 1.5)
-        const double sr = rfl_d(sin_a * inv_hw), cr = rfl_d(cos_a * inv_hw);
-        const float ar = rfl_f((float)cr), ac = rfl_f((float)-sr);
+        const double sr = sin_a * inv_hw, cr = cos_a * inv_hw;
+        const float ar = (float)cr, ac = (float)-sr;
         auto sample = [&](float gx, float gy, float rbin, float cbin, float w) {
             if (!(rbin > -1.0f && rbin < 4.0f && cbin > -1.0f && cbin < 4.0f)) return;
             const float mag = __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
@@ -1065,27 +1052,23 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         };
         if (side <= kDescCols) {
             const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hw < 2.5 with slack
-            // Per patch ROW ys: the xs with |a xs + b| < lim form an interval (rrot = xs sin +
-            // ys cos: a = sin, b = ys cos; crot = xs cos - ys sin: a = cos, b = -ys sin);
-            // conservative: widened by 1e-6 (the exact bin test is per sample)
-            const double ia_r = fabs(sin_a) < 1e-12 ? 0.0 : 1.0 / sin_a;
-            const double ia_c = fabs(cos_a) < 1e-12 ? 0.0 : 1.0 / cos_a;
-            const float kq = rfl_f((float)(-0.125 * 1.4426950408889634 * inv_hw * inv_hw));
-            const int xlo_img = max(-half, 1 - px), xhi_img = min(half, cols - 2 - px);
+            // |a ys + b| < lim -> ys in an interval (rrot: a = cos, b = xs sin; crot: a = -sin,
+            // b = xs cos); conservative: widened by 1e-6, so approximate quotients are fine
+            const double ia_r = fabs(cos_a) < 1e-12 ? 0.0 : 1.0 / cos_a;
+            const double ia_c = fabs(sin_a) < 1e-12 ? 0.0 : -1.0 / sin_a;
+            const float kq = (float)(-0.125 * 1.4426950408889634 * inv_hw * inv_hw);
             int run = 0;                                   // wave-wide running total
-            for (int r4 = 0; r4 < side; r4 += 64) {
-                const int r = r4 + lane;                   // patch row r: ys = r - half
+            for (int c4 = 0; c4 < side; c4 += 64) {
+                const int c = c4 + lane;
                 int lo = 1, hi = 0;
-                if (r < side) {
-                    const int ys = r - half, rr = py + ys;
-                    // per-column bin offsets (the column tables are indexed by xs + half)
-                    const int xs = r - half;
-                    cbr[r] = (float)((double)xs * sr) + 1.5f;
-                    cbc[r] = (float)((double)xs * cr) + 1.5f;
-                    if (rr > 0 && rr < rows - 1) {
-                        lo = xlo_img;
-                        hi = xhi_img;
-                        const double bvs[2] = {ys * cos_a, -ys * sin_a};
+                if (c < side) {
+                    const int xs = c - half, cc = px + xs;
+                    cbr[c] = (float)((double)xs * sr) + 1.5f;
+                    cbc[c] = (float)((double)xs * cr) + 1.5f;
+                    if (cc > 0 && cc < cols - 1) {
+                        lo = max(-half, 1 - py);
+                        hi = min(half, rows - 2 - py);
+                        const double bvs[2] = {xs * sin_a, xs * cos_a};
                         const double ias[2] = {ia_r, ia_c};
 #pragma unroll
                         for (int qd = 0; qd < 2; ++qd) {
@@ -1102,16 +1085,16 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                         }
                     }
                 }
-                const int n_r = hi >= lo ? hi - lo + 1 : 0;
-                int incl = n_r;
+                const int n_c = hi >= lo ? hi - lo + 1 : 0;
+                int incl = n_c;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
                     const int t = __shfl_up(incl, d);
                     if (lane >= d) incl += t;
                 }
-                if (r < side) {
-                    clo[r] = lo;                           // first xs of row r
-                    cpre[r] = run + incl - n_r;
+                if (c < side) {
+                    clo[c] = lo;
+                    cpre[c] = run + incl - n_c;
                 }
                 run += __shfl(incl, 63);
             }
@@ -1120,55 +1103,68 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const int nsamp = run;
-            // Lanes in 4 groups of 16; group g walks its quarter of the row-major sample index
-            // 16 samples at a time: a group's taps are 16 consecutive floats of one row (a
-            // couple of cache lines per load instead of 64 scattered ones), and the groups sit
-            // a quarter of the patch apart (different cells: few same-address LDS atomics).
-            const int grp = lane >> 4, gl = lane & 15;
-            const int q4 = (nsamp + 3) >> 2;
-            const int dend = min((grp + 1) * q4, nsamp);
-            int d = grp * q4 + gl;
-            if (d < dend) {
-                int r = 0, r1 = side - 1;                  // largest r with cpre[r] <= d
-                while (r < r1) {
-                    const int mid = (r + r1 + 1) >> 1;
-                    if (cpre[mid] <= d) r = mid;
-                    else r1 = mid - 1;
+            const int Q = (nsamp + 63) >> 6;
+            int t = lane * Q;
+            const int tend = min(t + Q, nsamp);
+            if (t < tend) {
+                int c = 0, c1 = side - 1;                  // largest c with cpre[c] <= t
+                while (c < c1) {
+                    const int mid = (c + c1 + 1) >> 1;
+                    if (cpre[mid] <= t) c = mid;
+                    else c1 = mid - 1;
                 }
-                auto taps4 = [&](int xs, int ys, float (&g)[4]) {
+                int ys = clo[c] + (t - cpre[c]);
+                int yend = clo[c] + (cpre[c + 1] - cpre[c]);
+                // (x-1, x, x+1) of image row py + y at patch column cc
+                auto trip = [&](int cc, int y, float (&T)[3]) {
 #if PANO_DESC_ABL == 3
-                    const float *q = img + (size_t)py * cols + px + ((xs + ys) & 1);      // L1-resident
+                    const float *q = img + (size_t)py * cols + px + ((cc + y) & 1) - 1;   // L1-resident
 #else
-                    const float *q = img + (size_t)(py + ys) * cols + (px + xs);
+                    const float *q = img + (size_t)(py + y) * cols + (px + cc - half) - 1;
 #endif
-                    g[0] = q[-1];
-                    g[1] = q[1];
-                    g[2] = q[-cols];
-                    g[3] = q[cols];
+                    T[0] = q[0];
+                    T[1] = q[1];
+                    T[2] = q[2];
                 };
-                int xs = clo[r] + (d - cpre[r]), ys = r - half;
-                float G[4];
-                taps4(xs, ys, G);
-                for (;;) {
-                    // next position (16 samples on), its taps in flight while this one is binned
-                    const int dn = d + 16;
-                    int rn = r;
-                    const bool more = dn < dend;
-                    if (more)
-                        while (cpre[rn + 1] <= dn) ++rn;
-                    const int xn = clo[rn] + (dn - cpre[rn]), yn = rn - half;
-                    float Gn[4];
-                    if (more) taps4(xn, yn, Gn);
+                float br = cbr[c], bc = cbc[c], xs2 = (float)((c - half) * (c - half));
+                float Tm[3], T0[3], Tp[3];
+                trip(c, ys - 1, Tm);
+                trip(c, ys, T0);
+                trip(c, ys + 1, Tp);
+                for (int j = t; j < tend; ++j) {
+                    // the next sample's position (this column, or the next non-empty one),
+                    // its taps loaded while this sample is binned
+                    int cn = c, yn = ys + 1;
+                    const bool more = j + 1 < tend;
+                    const bool newcol = more && yn >= yend;
+                    if (newcol) {
+                        do { ++cn; } while (cpre[cn + 1] == cpre[cn]);
+                        yn = clo[cn];
+                    }
+                    float N0[3], N1[3], N2[3];
+                    if (newcol) {
+                        trip(cn, yn - 1, N0);
+                        trip(cn, yn, N1);
+                    }
+                    if (more) trip(cn, yn + 1, N2);
                     const float ysf = (float)ys;
-                    sample(G[1] - G[0], G[2] - G[3], fmaf(ysf, ar, cbr[xs + half]), fmaf(ysf, ac, cbc[xs + half]),
-                           __builtin_amdgcn_exp2f(kq * fmaf(ysf, ysf, (float)(xs * xs))));
-                    if (!more) break;
-                    d = dn;
-                    r = rn;
-                    xs = xn;
-                    ys = yn;
+                    // exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) = exp2(kq (xs^2 + ys^2)): a rotation
+                    // keeps the radius (no LDS read on the sample path)
+                    sample(T0[2] - T0[0], Tm[1] - Tp[1], fmaf(ysf, ar, br), fmaf(ysf, ac, bc),
+                           __builtin_amdgcn_exp2f(kq * fmaf(ysf, ysf, xs2)));
+                    if (newcol) {
+                        c = cn;
+                        yend = clo[c] + (cpre[c + 1] - cpre[c]);
+                        br = cbr[c];
+                        bc = cbc[c];
+                        xs2 = (float)((c - half) * (c - half));
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) G[i] = Gn[i];
+                        for (int i = 0; i < 3; ++i) { Tm[i] = N0[i]; T0[i] = N1[i]; Tp[i] = N2[i]; }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; Tp[i] = N2[i]; }
+                    }
+                    ys = yn;
                 }
             }
         } else {
