@@ -12,12 +12,12 @@ import sys
 # device kernel name -> libpano profiler class (_lib.KERNELS)
 CLASSES = [
     (r"^(gray_frames|blur_fast|blur_level|blur_tail)", "blur_level"),
-    (r"^(extrema_scan|localize)", "extrema_localize"),
+    (r"^(extrema_scan|extrema_stream|localize)", "extrema_localize"),
     (r"^orientation", "orientation"),
     (r"^(rank_keys|bucket_|emit_keypoints)", "sort_dedup"),
     (r"^descriptor", "descriptor"),
     (r"^(pack_rows|row_norms)", "row_norms"),
-    (r"^(dist_bf16|dist_mfma)", "dist_mfma"),
+    (r"^(dist_bf16|dist_mfma|dist_u8)", "dist_mfma"),
     (r"^reduce_parts", "reduce_parts"),
     (r"^(pair_shifts|pair_compact|pair_votes|pair_select)", "pair_shifts"),
     (r"^(composite|plan_device)", "composite_step"),
