@@ -142,6 +142,17 @@ def kernel_bytes(name, st, n_frames, h, w):
         return 9 * n_frames * h * w, "GB/s"
     if name in ("cyl_scatter", "cyl_gather"):
         return 6 * n_frames * h * w, "GB/s"
+    if name in ("descriptor", "orientation"):
+        # SURVEY 8(d) "S7+S9 upper bound": 12 sum(Po) bytes per frame (the three Gaussian
+        # layers keypoints live on, read once); both classes are bounded by it
+        tot = 0
+        no = ctypes.c_int32()
+        hh, ww = ctypes.c_int32(), ctypes.c_int32()
+        ctx.lib.pano_sift_level_shape(ctx.h, 0, ctypes.byref(hh), ctypes.byref(ww), ctypes.byref(no))
+        for o in range(no.value):
+            ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(hh), ctypes.byref(ww), None)
+            tot += 12 * n_frames * hh.value * ww.value
+        return tot, "GB/s"
     if name == "extrema_localize":
         tot = 0
         no = ctypes.c_int32()
