@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(512, 2)
 dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
         const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
         int n_split) {
-    __shared__ __attribute__((aligned(16))) unsigned short Bs[BT * BKP];
+    __shared__ __attribute__((aligned(16))) unsigned short Bs2[2][BT * BKP];   // double buffer
     __shared__ Part red[2][QT];
     const int p = blockIdx.z;
     const int fa = pairs.a[p], fb = pairs.b[p];
@@ -417,7 +417,7 @@ dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
             pre_norm = norms[(size_t)fb * cap + row];
         }
     };
-    auto store = [&]() {
+    auto store = [&](unsigned short *Bs) {
         unsigned short *dst = Bs + sr * BKP + 32 * sp;
         const unsigned int *u = (const unsigned int *)pre;
         unsigned int o[16];
@@ -437,13 +437,17 @@ dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
     };
     float best[2] = {INFINITY, INFINITY}, second[2] = {INFINITY, INFINITY};
     int bj[2] = {0x7fffffff, 0x7fffffff};
-    int jt = blockIdx.x;
+    // Two LDS tiles: the MFMAs of tile t read one while the next tile (its bytes prefetched
+    // into registers a tile earlier) is converted into the other, so the conversion VALU and
+    // LDS stores run under the MFMAs, and one barrier per tile suffices.  (One workgroup per
+    // CU: 180 VGPRs per lane allow two waves per SIMD.)
+    int jt = blockIdx.x, cur = 0;
     fetch(jt);
-    for (; jt < n_jt; jt += n_split) {
-        __syncthreads();                            // every wave is done with the last tile
-        store();
-        __syncthreads();
-        if (jt + n_split < n_jt) fetch(jt + n_split);   // in flight during the MFMAs
+    store(Bs2[0]);
+    if (jt + n_split < n_jt) fetch(jt + n_split);
+    for (; jt < n_jt; jt += n_split, cur ^= 1) {
+        __syncthreads();        // tile jt complete in Bs2[cur]; every wave done with Bs2[cur ^ 1]
+        const unsigned short *Bs = Bs2[cur];
         f32x16 acc[2][2];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -462,6 +466,10 @@ dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fj[a], fi[b][k], acc[a][b], 0, 0, 0);
+        }
+        if (jt + n_split < n_jt) {
+            store(Bs2[cur ^ 1]);
+            if (jt + 2 * n_split < n_jt) fetch(jt + 2 * n_split);   // in flight for a tile
         }
         const int jb = jt * BT + wj * 64 + 4 * lh;
 #pragma unroll
@@ -513,6 +521,193 @@ dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
         if (gi < NA) {
             const float na = (float)norms[(size_t)fa * cap + gi];
             parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{na + bb, jj, na + ss};
+        }
+    }
+}
+
+// ---------------------------------------------------------------- i8 MFMA path (default)
+// The descriptor bytes enter the i8 MFMA as b' = b - 128 (b ^ 0x80 read as int8), so no
+// conversion at all, at twice the bf16 MFMA rate and K = 128 exactly (no augmentation):
+//   a.b = a'.b' + 128 (sum a' + sum b') + 128^3,  sum a' = s_a - 128^2  (s = byte sum)
+//   d(i, j) = ||a_i||^2 + ||b_j||^2 - 2 a.b = R_i + C_j - 2 a'.b',
+//   R = ||a||^2 - 256 s_a,  C = ||b||^2 - 256 s_b + 2^22
+// with a'.b' accumulated exactly in i32 (|a'.b'| <= 2^21): every distance is the exact
+// integer the reference's np.dot gives, compared as integers (first index on ties).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+constexpr int BPI = PANO_DESC_DIM + 16;          // LDS row pitch in bytes (rows 36 banks apart)
+constexpr int kBig = 0x3fffffff;                 // "no distance" (padding rows, empty pairs)
+
+// R per descriptor row (rows past the frame's count: unused)
+__global__ void __launch_bounds__(256)
+row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
+           const int32_t *__restrict__ counts, int cap, int32_t *__restrict__ cst) {
+    const int f = blockIdx.y, row = blockIdx.x * 64 + (threadIdx.x >> 2), part = threadIdx.x & 3;
+    const int n = min(max(counts[f], 0), cap);
+    unsigned int sum = 0;
+    if (row < n) {
+        const uint4 *q = (const uint4 *)(desc + ((size_t)f * cap + row) * PANO_DESC_DIM + 32 * part);
+        const uint4 v0 = q[0], v1 = q[1];
+        const unsigned int w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum = __builtin_amdgcn_udot4(w[i], 0x01010101u, sum, false);
+    }
+    sum += __shfl_xor(sum, 1);
+    sum += __shfl_xor(sum, 2);
+    if (row < n && part == 0) cst[(size_t)f * cap + row] = norms[(size_t)f * cap + row] - 256 * (int)sum;
+}
+
+template <bool SECOND>
+__global__ void __launch_bounds__(512, 2)
+dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
+        const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
+        int n_split) {
+    __shared__ __attribute__((aligned(16))) unsigned char Bs2[2][BT * BPI];
+    __shared__ __attribute__((aligned(16))) int Cs2[2][BT];
+    struct IPart { int best, idx, second; };
+    __shared__ IPart red[2][QT];
+    const int p = blockIdx.z;
+    const int fa = pairs.a[p], fb = pairs.b[p];
+    int NA = counts[fa], NB = counts[fb];
+    NA = min(max(NA, 0), cap);
+    NB = min(max(NB, 0), cap);
+    const int i0 = blockIdx.y * QT;
+    const int n_jt = (NB + BT - 1) / BT;
+    if (i0 >= NA || (int)blockIdx.x >= n_jt) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wi = wv & 3, wj = wv >> 2;
+    const int lr = lane & 31, lh = lane >> 5;
+    const uint8_t *dA = desc + (size_t)fa * cap * PANO_DESC_DIM;
+    const uint8_t *dB = desc + (size_t)fb * cap * PANO_DESC_DIM;
+    // query fragments (B operand): rows i0 + wi 64 + m 32 + lr, K step k = bytes 32 k + 16 lh
+    i32x4 fi[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int row = i0 + wi * 64 + m * 32 + lr;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+            if (row < NA) v = *(const uint4 *)(dA + (size_t)row * PANO_DESC_DIM + 32 * k + 16 * lh);
+            fi[m][k] = i32x4{(int)(v.x ^ 0x80808080u), (int)(v.y ^ 0x80808080u), (int)(v.z ^ 0x80808080u),
+                             (int)(v.w ^ 0x80808080u)};
+        }
+    }
+    // candidate tile staging: thread t copies row t % 128, bytes 32 (t / 128) .. + 32, with
+    // the sign flip; the first quarter also its C
+    const int sr = tid & (BT - 1), sp = tid / BT;
+    uint4 pre[2];
+    int pre_c = kBig;
+    auto fetch = [&](int jt) {
+        const int row = jt * BT + sr;
+        pre[0] = pre[1] = make_uint4(0u, 0u, 0u, 0u);
+        pre_c = kBig;                                   // past the count: never a best
+        if (row < NB) {
+            const uint4 *src = (const uint4 *)(dB + (size_t)row * PANO_DESC_DIM + 32 * sp);
+            pre[0] = src[0];
+            pre[1] = src[1];
+            if (sp == 0) pre_c = cst[(size_t)fb * cap + row] + (1 << 22);
+        }
+    };
+    auto store = [&](int buf) {
+        uint4 *d4 = (uint4 *)(Bs2[buf] + sr * BPI + 32 * sp);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            d4[q] = make_uint4(pre[q].x ^ 0x80808080u, pre[q].y ^ 0x80808080u, pre[q].z ^ 0x80808080u,
+                               pre[q].w ^ 0x80808080u);
+        if (sp == 0) Cs2[buf][sr] = pre_c;
+    };
+    int best[2] = {kBig, kBig}, second[2] = {kBig, kBig};
+    int bj[2] = {0x7fffffff, 0x7fffffff};
+    int jt = blockIdx.x, cur = 0;
+    fetch(jt);
+    store(0);
+    if (jt + n_split < n_jt) fetch(jt + n_split);
+    for (; jt < n_jt; jt += n_split, cur ^= 1) {
+        __syncthreads();        // tile jt complete in buffer cur; every wave done with cur ^ 1
+        const unsigned char *Bs = Bs2[cur];
+        i32x16 acc[2][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            i32x4 fj[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                fj[a] = *(const i32x4 *)(Bs + (wj * 64 + a * 32 + lr) * BPI + 32 * k + 16 * lh);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fj[a], fi[b][k],
+                                                                      k == 0 ? i32x16{} : acc[a][b], 0, 0, 0);
+        }
+        if (jt + n_split < n_jt) {
+            store(cur ^ 1);
+            if (jt + 2 * n_split < n_jt) fetch(jt + 2 * n_split);
+        }
+        const int jb = jt * BT + wj * 64 + 4 * lh;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            // C of this lane's 16 candidate rows: rows (r & 3) + 8 (r >> 2) + 4 lh of block a
+            int cj[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int4 c4 = *(const int4 *)(&Cs2[cur][wj * 64 + a * 32 + 8 * g + 4 * lh]);
+                cj[4 * g] = c4.x; cj[4 * g + 1] = c4.y; cj[4 * g + 2] = c4.z; cj[4 * g + 3] = c4.w;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                int v[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = cj[r] - 2 * acc[a][b][r];
+                if (SECOND) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {   // j increasing within the lane: strict <
+                        second[b] = min(second[b], max(best[b], v[r]));
+                        const bool lt = v[r] < best[b];
+                        bj[b] = lt ? jb + a * 32 + (r & 3) + 8 * (r >> 2) : bj[b];
+                        best[b] = lt ? v[r] : best[b];
+                    }
+                } else {
+                    int m = v[0];
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) m = min(m, v[r]);
+                    if (m < best[b]) {
+                        int ri = 15;
+#pragma unroll
+                        for (int r = 14; r >= 0; --r) ri = v[r] == m ? r : ri;   // first r
+                        best[b] = m;
+                        bj[b] = jb + a * 32 + (ri & 3) + 8 * (ri >> 2);
+                    }
+                }
+            }
+        }
+    }
+    auto imerge = [](int &b, int &j, int &s, int b2, int j2, int s2) {
+        if (b2 < b || (b2 == b && j2 < j)) {
+            s = min(s2, b);
+            b = b2;
+            j = j2;
+        } else {
+            s = min(s, b2);
+        }
+    };
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int ob = __shfl_xor(best[b], 32), oj = __shfl_xor(bj[b], 32), os = __shfl_xor(second[b], 32);
+        imerge(best[b], bj[b], second[b], ob, oj, os);
+        const int il = wi * 64 + b * 32 + lr;
+        if (lh == 0) red[wj][il] = IPart{best[b], bj[b], second[b]};
+    }
+    __syncthreads();
+    if (tid < QT) {
+        IPart x = red[0][tid];
+        const IPart y = red[1][tid];
+        imerge(x.best, x.idx, x.second, y.best, y.idx, y.second);
+        const int gi = i0 + tid;
+        if (gi < NA) {
+            const int ra = cst[(size_t)fa * cap + gi];
+            const float db = x.best >= kBig ? INFINITY : (float)(ra + x.best);
+            const float ds = x.second >= kBig ? INFINITY : (float)(ra + x.second);
+            parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{db, x.idx, ds};
         }
     }
 }
@@ -637,14 +832,41 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
         int32_t *bp = best + (size_t)p0 * cap;
         float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 ? d2 + (size_t)p0 * cap : nullptr;
         dim3 grid(n_split, n_qt, np);
-        {
-            PanoProf prof_(ctx, PK_DIST_MFMA);
-            if (p2)
-                dist_u8<true><<<grid, 512, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_split);
-            else
-                dist_u8<false><<<grid, 512, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_split);
+        static const bool use_i8 = [] {
+            const char *e = getenv("PANO_MATCH_I8");     // 1: i8 MFMA; 0 (default until measured): bf16 MFMA
+            return e ? atoi(e) != 0 : false;
+        }();
+        if (use_i8) {
+            int nf = 0;
+            for (int q = 0; q < 2 * np; ++q) nf = std::max(nf, h_pairs[2 * p0 + q] + 1);
+            const size_t cst_bytes = (size_t)nf * cap * sizeof(int32_t);
+            rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes, part_bytes + cst_bytes);
+            if (rc) return rc;
+            parts = (Part *)ctx->mscratch;
+            int32_t *cst = (int32_t *)((char *)ctx->mscratch + part_bytes);
+            {
+                PanoProf prof_(ctx, PK_NORMS);
+                row_consts<<<dim3((cap + 63) / 64, nf), 256, 0, ctx->stream>>>(desc, norms, counts, cap, cst);
+            }
+            PANO_LAUNCH_CHECK(ctx, "row_consts");
+            {
+                PanoProf prof_(ctx, PK_DIST_MFMA);
+                if (p2)
+                    dist_i8<true><<<grid, 512, 0, ctx->stream>>>(desc, cst, counts, cap, pa, parts, n_split);
+                else
+                    dist_i8<false><<<grid, 512, 0, ctx->stream>>>(desc, cst, counts, cap, pa, parts, n_split);
+            }
+            PANO_LAUNCH_CHECK(ctx, "dist_i8");
+        } else {
+            {
+                PanoProf prof_(ctx, PK_DIST_MFMA);
+                if (p2)
+                    dist_u8<true><<<grid, 512, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_split);
+                else
+                    dist_u8<false><<<grid, 512, 0, ctx->stream>>>(desc, norms, counts, cap, pa, parts, n_split);
+            }
+            PANO_LAUNCH_CHECK(ctx, "dist_u8");
         }
-        PANO_LAUNCH_CHECK(ctx, "dist_u8");
         dim3 g2((cap + 255) / 256, np);
         {
             PanoProf prof_(ctx, PK_REDUCE);
