@@ -32,6 +32,17 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
+MFMA_I8_PEAK_TOPS = 5000.0      # dense i8 MFMA: the bf16 cycles at twice the K (MI355X_MICROARCH.md)
+
+
+def match_dtype(st):
+    """The distance GEMM that ran: "i8" (u8 descriptors - 128 into v_mfma_i32_32x32x32_i8,
+    the default), "bf16" or "f32"."""
+    if st.match == "f32":
+        return "f32"
+    if st.match == "u8" and os.environ.get("PANO_MATCH_I8", "1") != "0":
+        return "i8"
+    return "bf16"
 MFMA_F32_PEAK_TFLOPS = 157.3    # dense f32 MFMA
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec (the blur's arithmetic)
 
@@ -302,11 +313,13 @@ def main():
         pairs = [(i, i + 1) for i in range(len(cnt) - 1)]
         fl = sum(2.0 * cnt[a] * cnt[b] * 128 for a, b in pairs)
         ms = per_kernel["dist_mfma"]["total_ms"]
-        pk = MFMA_F32_PEAK_TFLOPS if st.match == "f32" else MFMA_BF16_PEAK_TFLOPS
+        mdt = match_dtype(st)
+        pk = {"f32": MFMA_F32_PEAK_TFLOPS, "bf16": MFMA_BF16_PEAK_TFLOPS, "i8": MFMA_I8_PEAK_TOPS}[mdt]
         tf = fl / (ms * 1e-3) / 1e12
-        roof_match = {"bound": "mfma", "kernel": "dist_mfma", "dtype": "f32" if st.match == "f32" else "bf16", "descriptors": st.match,
-                      "achieved": round(tf, 2), "peak": pk, "unit": "TFLOP/s",
-                      "frac": round(tf / pk, 5), "flop_per_step": fl,
+        roof_match = {"bound": "mfma", "kernel": "dist_mfma", "dtype": mdt, "descriptors": st.match,
+                      "achieved": round(tf, 2), "peak": pk, "unit": "TOPS" if mdt == "i8" else "TFLOP/s",
+                      "frac": round(tf / pk, 5), "frac_of_bf16_peak": round(tf / MFMA_BF16_PEAK_TFLOPS, 5),
+                      "flop_per_step": fl,
                       "mean_keypoints": round(float(cnt.mean()), 1),
                       "kernel_ms_per_step": round(ms, 4)}
 
@@ -326,7 +339,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": ("u8 frames; f32 pyramid (fp64-accumulated blur); match " +
-                  ("f32 MFMA" if st.match == "f32" else "bf16 MFMA, exact for integer descriptors")
+                  {"f32": "f32 MFMA", "bf16": "bf16 MFMA, exact for integer descriptors",
+                   "i8": "i8 MFMA on u8 descriptors - 128, exact integer distances"}[match_dtype(st)]
                   if args.method == "sift" else "u8 frames; f64 Harris response; f32 descriptors"),
         "data": "reference parrington JPEGs (packed under data/), decoded, resident in HBM"
         if args.workload != "synthetic" else "synthetic 1080p sequence (SURVEY 8d config 5)",
