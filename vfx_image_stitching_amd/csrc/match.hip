@@ -538,6 +538,13 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 constexpr int BPI = PANO_DESC_DIM + 16;          // LDS row pitch in bytes (rows 36 banks apart)
 constexpr int kBig = 0x3fffffff;                 // "no distance" (padding rows, empty pairs)
 
+// c + a * b in one VALU op (|a|, |b| < 2^23 here: a'.b' is within +-2^21)
+__device__ __forceinline__ int mad_i24(int a, int b, int c) {
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(b), "v"(c));
+    return r;
+}
+
 // R per descriptor row (rows past the frame's count: unused)
 __global__ void __launch_bounds__(256)
 row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
@@ -660,7 +667,7 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
             for (int b = 0; b < 2; ++b) {
                 int v[16];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = cj[r] - 2 * acc[a][b][r];
+                for (int r = 0; r < 16; ++r) v[r] = mad_i24(acc[a][b][r], -2, cj[r]);
                 if (SECOND) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {   // j increasing within the lane: strict <
