@@ -517,129 +517,179 @@ struct OriParams {
     double scale_factor, radius_factor, peak_ratio;
 };
 
+// Dense candidate index gk (frames back to back, counts strided kCntStride and clamped to
+// [0, cap]) -> (frame, index); false past the last candidate.
+__device__ __forceinline__ bool locate_strided(const int32_t *__restrict__ counts, int n_frames, int cap,
+                                               int gk, int &f, int &k) {
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    for (int f0 = 0; f0 < n_frames; f0 += 64) {
+        int c = f0 + lane < n_frames ? counts[(f0 + lane) * kCntStride] : 0;
+        c = c < 0 ? 0 : (c < cap ? c : cap);
+        int incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int tot = __shfl(incl, 63);
+        if (gk < base + tot) {
+            const int j = __popcll(__ballot(base + incl <= gk));
+            f = f0 + j;
+            k = gk - base - (__shfl(incl, j) - __shfl(c, j));
+            return true;
+        }
+        base += tot;
+    }
+    return false;
+}
+
+// One WAVE per candidate, persistent: the grid is the resident workgroups (a grid sized by the
+// candidate capacity dispatched ~37k mostly-empty workgroups at parrington, 410k at 1080p),
+// each XCD takes a contiguous eighth of the candidates and its waves pull them from the XCD's
+// own counter (as descriptor_wave).  Per candidate: the (side+2)^2 neighbourhood staged in
+// LDS, each lane its run of column-major samples into 2^40 fixed-point u64 LDS atomics,
+// smoothing and peak interpolation in f64 (the reference's), one aggregated append.
 __global__ void __launch_bounds__(256)
 orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
-            const int32_t *__restrict__ cand_cnt, int cand_cap, RawKp *__restrict__ raw,
-            int32_t *__restrict__ raw_cnt, int raw_cap, int32_t *__restrict__ zero, int nzero) {
+            const int32_t *__restrict__ cand_cnt, int cand_cap, int n_frames, int32_t *__restrict__ work,
+            RawKp *__restrict__ raw, int32_t *__restrict__ raw_cnt, int raw_cap, int32_t *__restrict__ zero,
+            int nzero) {
     // the sort's bucket counters are zeroed here (their first use is the next launch)
-    for (int i = linear_block_id() * 256 + threadIdx.x; i < nzero; i += gridDim.x * gridDim.y * 256)
-        zero[i] = 0;
+    for (int i = (int)blockIdx.x * 256 + threadIdx.x; i < nzero; i += gridDim.x * 256) zero[i] = 0;
     __shared__ unsigned long long hist[4][PANO_ORI_BINS];
     __shared__ double hd[4][PANO_ORI_BINS];
     __shared__ double sm[4][PANO_ORI_BINS];
     __shared__ float patch[4][kOriPatch * kOriPatch];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const unsigned tb = xcd_swizzle_chunked<16>(linear_block_id(), gridDim.x * gridDim.y);
-    const int f = (int)(tb / gridDim.x), bx = (int)(tb % gridDim.x);
-    const int ci = bx * 4 + wv;
-    int cnt = cand_cnt[f * kCntStride];
-    cnt = cnt < cand_cap ? cnt : cand_cap;
-    if (bx * 4 >= cnt) return;   // uniform: no wave of this block is active
-    const bool active = ci < cnt;
-    if (lane < PANO_ORI_BINS) hist[wv][lane] = 0ull;
-    __syncthreads();
-    Cand k{};
-    if (active) {
-        k = cands[(size_t)f * cand_cap + ci];
-        const int o = k.octave;
-        const int H = pa.H[o], W = pa.W[o];
-        const float *img = pa.gauss[o][k.layer] + (size_t)f * H * W;
-        const float scale = (float)(op.scale_factor * (double)k.size) / (float)(1 << (o + 1));
-        const int radius = (int)rintf((float)op.radius_factor * scale);
-        const float wfac = -0.5f / (scale * scale);
-        const int cy = (int)rintf(k.y / (float)(1 << o));
-        const int cx = (int)rintf(k.x / (float)(1 << o));
-        const int side = 2 * radius + 1;
-        const int S = side * side;
-        // stage the (side+2)^2 neighbourhood (clamped; out-of-image samples are skipped
-        // below) so each sample's four gradient taps are LDS reads
-        const int P = side + 2;
-        const bool staged = P <= kOriPatch;
-        float *pt = patch[wv];
-        if (staged) {
-            const int by = cy - radius - 1, bx = cx - radius - 1;
-            for (int e = lane; e < P * P; e += 64) {
-                const int r = e / P, c = e - (e / P) * P;
-                const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
-                pt[r * kOriPatch + c] = img[(size_t)yy * W + xx];
-            }
-        }
+    int total = 0;
+    for (int f0 = 0; f0 < n_frames; f0 += 64) {
+        int c = f0 + lane < n_frames ? cand_cnt[(f0 + lane) * kCntStride] : 0;
+        c = c < 0 ? 0 : (c < cand_cap ? c : cand_cap);
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+        total += c;
+    }
+    const int xcd = blockIdx.x & 7;                                   // gridDim.x % 8 == 0
+    const int lo_k = (int)((long long)total * xcd / 8), hi_k = (int)((long long)total * (xcd + 1) / 8);
+    int32_t *wq = work + xcd * kCntStride;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        // lane l walks its own run of Q consecutive column-major samples (neighbouring lanes
-        // are Q samples apart: different bins, fewer same-address LDS atomics)
-        const int Q = (S + 63) / 64;
-        const int j0 = lane * Q;
-        int xi = j0 / side, yi = j0 - (j0 / side) * side;
-        const int jend = min(j0 + Q, S);
-        for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
-            const int dx = xi - radius, dy = yi - radius;
-            const int yy = cy + dy, xx = cx + dx;
-            if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
-            float gx, gy;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (;;) {
+        int gk = 0;
+        if (lane == 0) gk = atomicAdd(wq, 1);
+        gk = lo_k + __shfl(gk, 0);
+        int f = 0, ci = 0;
+        if (gk >= hi_k || !locate_strided(cand_cnt, n_frames, cand_cap, gk, f, ci)) break;
+        f = __builtin_amdgcn_readfirstlane(f);
+        ci = __builtin_amdgcn_readfirstlane(ci);
+        if (lane < PANO_ORI_BINS) hist[wv][lane] = 0ull;
+        const Cand k = cands[(size_t)f * cand_cap + ci];
+        {
+            const int o = k.octave;
+            const int H = pa.H[o], W = pa.W[o];
+            const float *img = pa.gauss[o][k.layer] + (size_t)f * H * W;
+            const float scale = (float)(op.scale_factor * (double)k.size) / (float)(1 << (o + 1));
+            const int radius = (int)rintf((float)op.radius_factor * scale);
+            const float wfac = -0.5f / (scale * scale);
+            const int cy = (int)rintf(k.y / (float)(1 << o));
+            const int cx = (int)rintf(k.x / (float)(1 << o));
+            const int side = 2 * radius + 1;
+            const int S = side * side;
+            // stage the (side+2)^2 neighbourhood (clamped; out-of-image samples are skipped
+            // below) so each sample's four gradient taps are LDS reads
+            const int P = side + 2;
+            const bool staged = P <= kOriPatch;
+            float *pt = patch[wv];
             if (staged) {
-                const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
-                gx = q[1] - q[-1];
-                gy = q[-kOriPatch] - q[kOriPatch];
-            } else {
-                gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
-                gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+                const int by = cy - radius - 1, bx = cx - radius - 1;
+                for (int e = lane; e < P * P; e += 64) {
+                    const int r = e / P, c = e - (e / P) * P;
+                    const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
+                    pt[r * kOriPatch + c] = img[(size_t)yy * W + xx];
+                }
             }
-            const float mag = sqrtf(gx * gx + gy * gy);
-            const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
-            const float w = expf(wfac * (float)(dx * dx + dy * dy));
-            const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
-            const double val = (double)(w * mag);
-            atomicAdd(&hist[wv][bin], rint_fix(val * kHistScale));
+            wave_sync();
+            // lane l walks its own run of Q consecutive column-major samples (neighbouring
+            // lanes are Q samples apart: different bins, fewer same-address LDS atomics)
+            const int Q = (S + 63) / 64;
+            const int j0 = lane * Q;
+            int xi = j0 / side, yi = j0 - (j0 / side) * side;
+            const int jend = min(j0 + Q, S);
+            for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
+                const int dx = xi - radius, dy = yi - radius;
+                const int yy = cy + dy, xx = cx + dx;
+                if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
+                float gx, gy;
+                if (staged) {
+                    const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
+                    gx = q[1] - q[-1];
+                    gy = q[-kOriPatch] - q[kOriPatch];
+                } else {
+                    gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
+                    gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+                }
+                const float mag = sqrtf(gx * gx + gy * gy);
+                const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+                const float w = expf(wfac * (float)(dx * dx + dy * dy));
+                const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
+                const double val = (double)(w * mag);
+                atomicAdd(&hist[wv][bin], rint_fix(val * kHistScale));
+            }
         }
-    }
-    __syncthreads();
-    if (lane < PANO_ORI_BINS) hd[wv][lane] = (double)(long long)hist[wv][lane] * kHistInv;
-    __syncthreads();
-    if (lane < PANO_ORI_BINS) {
-        const int b = lane, nb = PANO_ORI_BINS;
-        const double *h = hd[wv];
-        sm[wv][b] = ((6 * h[b] + 4 * (h[(b + nb - 1) % nb] + h[(b + 1) % nb])) +
-                     h[(b + nb - 2) % nb]) + h[(b + 2) % nb];
-        sm[wv][b] = sm[wv][b] / 16.0;
-    }
-    __syncthreads();
-    // peaks -> keypoints; one (wave-aggregated) append per candidate
-    const int nb = PANO_ORI_BINS;
-    const int p = lane;
-    bool emit = false;
-    double angle = 0.0;
-    if (active && lane < nb) {
-        const double *s = sm[wv];
-        double mx = s[0];
-        for (int b = 1; b < nb; ++b) mx = fmax(mx, s[b]);
-        const double l = s[(p + nb - 1) % nb], r = s[(p + 1) % nb];
-        if (s[p] > l && s[p] > r && s[p] >= op.peak_ratio * mx) {
-            const double interp =
-                np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * s[p]) + r), (double)nb);
-            angle = 360.0 - interp * 360.0 / nb;
-            if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
-            emit = true;
+        wave_sync();
+        if (lane < PANO_ORI_BINS) hd[wv][lane] = (double)(long long)hist[wv][lane] * kHistInv;
+        wave_sync();
+        if (lane < PANO_ORI_BINS) {
+            const int b = lane, nb = PANO_ORI_BINS;
+            const double *h = hd[wv];
+            sm[wv][b] = ((6 * h[b] + 4 * (h[(b + nb - 1) % nb] + h[(b + 1) % nb])) +
+                         h[(b + nb - 2) % nb]) + h[(b + 2) % nb];
+            sm[wv][b] = sm[wv][b] / 16.0;
         }
+        wave_sync();
+        // peaks -> keypoints; one (wave-aggregated) append per candidate
+        const int nb = PANO_ORI_BINS;
+        const int p = lane;
+        bool emit = false;
+        double angle = 0.0;
+        if (lane < nb) {
+            const double *sv = sm[wv];
+            double mx = sv[0];
+            for (int b = 1; b < nb; ++b) mx = fmax(mx, sv[b]);
+            const double l = sv[(p + nb - 1) % nb], r = sv[(p + 1) % nb];
+            if (sv[p] > l && sv[p] > r && sv[p] >= op.peak_ratio * mx) {
+                const double interp =
+                    np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * sv[p]) + r), (double)nb);
+                angle = 360.0 - interp * 360.0 / nb;
+                if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
+                emit = true;
+            }
+        }
+        const unsigned long long m = __ballot(emit);
+        if (m) {
+            int base = 0;
+            if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&raw_cnt[f * kCntStride], __popcll(m));
+            base = __shfl(base, __ffsll((long long)m) - 1);
+            if (emit) {
+                RawKp q;
+                q.x = k.x;
+                q.y = k.y;
+                q.size = k.size;
+                q.angle = (float)angle;
+                q.response = k.response;
+                q.octave = k.octave_field;
+                q.frame = f;
+                q.order = ((uint64_t)k.order << 6) | (uint64_t)p;
+                const int slot = base + __popcll(m & ((1ull << lane) - 1));
+                if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = q;
+            }
+        }
+        wave_sync();                       // hist / hd / sm / patch reused by the next candidate
     }
-    const unsigned long long m = __ballot(emit);
-    if (!m) return;
-    int base = 0;
-    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&raw_cnt[f * kCntStride], __popcll(m));
-    base = __shfl(base, __ffsll((long long)m) - 1);
-    if (!emit) return;
-    RawKp q;
-    q.x = k.x;
-    q.y = k.y;
-    q.size = k.size;
-    q.angle = (float)angle;
-    q.response = k.response;
-    q.octave = k.octave_field;
-    q.frame = f;
-    q.order = ((uint64_t)k.order << 6) | (uint64_t)p;
-    const int slot = base + __popcll(m & ((1ull << lane) - 1));
-    if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = q;
 }
 
 // ------------------------------------------------------------------ S8
@@ -1242,8 +1292,9 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint32_t));
     if (rc) return rc;
     uint32_t *raw_ext = (uint32_t *)ctx->frame_off;
-    // [err] [cand f] [raw f] [ext f] [descriptor work queue per XCD x 8], one line apiece
-    const size_t cnt_ints = (3 * (size_t)n + 1 + 8) * kCntStride;
+    // [err] [cand f] [raw f] [ext f] [descriptor, orientation work queues per XCD x 8 each],
+    // one line apiece
+    const size_t cnt_ints = (3 * (size_t)n + 1 + 16) * kCntStride;
     rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, cnt_ints * sizeof(int32_t));
     if (rc) return rc;
     int32_t *err = ctx->counters;
@@ -1251,6 +1302,7 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     int32_t *raw_cnt = cand_cnt + (size_t)n * kCntStride;
     int32_t *ext_cnt = raw_cnt + (size_t)n * kCntStride;
     int32_t *desc_work = ext_cnt + (size_t)n * kCntStride;
+    int32_t *ori_work = desc_work + 8 * kCntStride;
     rc = launch_fill(ctx, ctx->counters, 0, cnt_ints * sizeof(int32_t));
     if (rc) return rc;
 
@@ -1382,11 +1434,22 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     int32_t *bslot = (int32_t *)(ctx->sorted + 2 * per);
     int32_t *bstart = (int32_t *)(ctx->sorted + 3 * per);
     {
-        dim3 grid((unsigned)((cand_cap + 3) / 4), n);
+        static int ori_resident = 0;
+        if (!ori_resident) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, orientation, 256, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+                per_cu <= 0 || cus <= 0)
+                per_cu = 4, cus = 256;
+            ori_resident = per_cu * cus;
+        }
+        const size_t slots = ((size_t)n * cand_cap + 3) / 4;
+        const unsigned blocks = (unsigned)std::max<size_t>(8, std::min<size_t>((slots + 7) & ~size_t(7),
+                                                                              (size_t)ori_resident & ~size_t(7)));
         {
             PanoProf prof_(ctx, PK_ORIENT);
-            orientation<<<grid, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap,
-                                                       ctx->raw, raw_cnt, (int)raw_cap, bstart, nb * n);
+            orientation<<<blocks, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap, n, ori_work,
+                                                         ctx->raw, raw_cnt, (int)raw_cap, bstart, nb * n);
         }
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
