@@ -438,21 +438,30 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     }
     __syncthreads();
     if (!colw) return;
+    // all SC outputs first (the sliding window interleaves their FMA chains), then predicated
+    // stores: an early exit in the store loop let the compiler compute one output at a time,
+    // a dependent chain of NT FMAs each
     double acc[SC];
     conv_seg<NT, SC>(tin + crs * SC * IWP + cxp, IWP, taps.k, acc);
+    float o[SC];
 #pragma unroll
     for (int j = 0; j < SC; ++j) {
-        const int ty = crs * SC + j;
-        if (ty >= th) break;
-        const float o = (float)acc[j];
-        const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + cxp;
+        o[j] = (float)acc[j];
+        asm volatile("" ::"v"(o[j]));                           // no sinking into the stores' branches
+    }
+    const int nvalid = th - crs * SC;                           // rows of this item inside the plane
+    const size_t g0 = ((size_t)f * H + y0 + crs * SC) * W + x0 + cxp;
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+        const size_t gi = g0 + (size_t)j * W;
+        if (j >= nvalid) continue;
         if constexpr ((PANO_BLUR_ABL & 2) != 0) {
-            if (o == -1.2345f) out[gi] = o + cen[j];          // never true: keeps the work live
+            if (o[j] == -1.2345f) out[gi] = o[j] + cen[j];    // never true: keeps the work live
             continue;
         }
-        if (out) out[gi] = o;
+        if (out) out[gi] = o[j];
         if constexpr (CENTER) {
-            if (dog) dog[gi] = o - cen[j];
+            if (dog) dog[gi] = o[j] - cen[j];
             if (in_copy) in_copy[gi] = cen[j];
         }
     }
