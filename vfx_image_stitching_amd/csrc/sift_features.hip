@@ -511,6 +511,10 @@ localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
 
 
 // ------------------------------------------------------------------ S7
+#ifndef PANO_ORI_COPIES
+#define PANO_ORI_COPIES 1      // histogram copies per wave (measured: 4 and 8 no faster)
+#endif
+constexpr int kOriCopies = PANO_ORI_COPIES;
 constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
 
 struct OriParams {
@@ -553,11 +557,11 @@ __device__ __forceinline__ bool locate_strided(const int32_t *__restrict__ count
 __global__ void __launch_bounds__(256)
 orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             const int32_t *__restrict__ cand_cnt, int cand_cap, int n_frames, int32_t *__restrict__ work,
-            RawKp *__restrict__ raw, int32_t *__restrict__ raw_cnt, int raw_cap, int32_t *__restrict__ zero,
-            int nzero) {
-    // the sort's bucket counters are zeroed here (their first use is the next launch)
-    for (int i = (int)blockIdx.x * 256 + threadIdx.x; i < nzero; i += gridDim.x * 256) zero[i] = 0;
-    __shared__ unsigned long long hist[4][PANO_ORI_BINS];
+            RawKp *__restrict__ raw, int32_t *__restrict__ raw_cnt, int raw_cap) {
+    // kOriCopies interleaved copies of each wave's histogram (copy = lane % kOriCopies): lanes
+    // on similar gradient directions hit the same bin; spreading them over copies cuts the
+    // same-address LDS atomic serialisation, and integer sums merge exactly
+    __shared__ unsigned long long hist[4][kOriCopies][PANO_ORI_BINS];
     __shared__ double hd[4][PANO_ORI_BINS];
     __shared__ double sm[4][PANO_ORI_BINS];
     __shared__ float patch[4][kOriPatch * kOriPatch];
@@ -586,7 +590,7 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         if (gk >= hi_k || !locate_strided(cand_cnt, n_frames, cand_cap, gk, f, ci)) break;
         f = __builtin_amdgcn_readfirstlane(f);
         ci = __builtin_amdgcn_readfirstlane(ci);
-        if (lane < PANO_ORI_BINS) hist[wv][lane] = 0ull;
+        for (int i = lane; i < kOriCopies * PANO_ORI_BINS; i += 64) (&hist[wv][0][0])[i] = 0ull;
         const Cand k = cands[(size_t)f * cand_cap + ci];
         {
             const int o = k.octave;
@@ -637,11 +641,16 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
                 const float w = expf(wfac * (float)(dx * dx + dy * dy));
                 const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
                 const double val = (double)(w * mag);
-                atomicAdd(&hist[wv][bin], rint_fix(val * kHistScale));
+                atomicAdd(&hist[wv][lane % kOriCopies][bin], rint_fix(val * kHistScale));
             }
         }
         wave_sync();
-        if (lane < PANO_ORI_BINS) hd[wv][lane] = (double)(long long)hist[wv][lane] * kHistInv;
+        if (lane < PANO_ORI_BINS) {
+            unsigned long long t = 0;
+#pragma unroll
+            for (int c = 0; c < kOriCopies; ++c) t += hist[wv][c][lane];
+            hd[wv][lane] = (double)(long long)t * kHistInv;
+        }
         wave_sync();
         if (lane < PANO_ORI_BINS) {
             const int b = lane, nb = PANO_ORI_BINS;
@@ -727,48 +736,60 @@ __device__ __forceinline__ unsigned long long xy_key(const RawKp &r) {
     return ((unsigned long long)sortable(r.x) << 32) | sortable(r.y);
 }
 
-__global__ void __launch_bounds__(256)
-bucket_count(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
-             int32_t *__restrict__ bstart, int32_t *__restrict__ bslot) {
-    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
-    const int cnt = raw_cnt[f * kCntStride];
-    if (cnt > raw_cap || i >= cnt) return;
-    const int b = x_bucket(raw[(size_t)f * raw_cap + i].x, nb);
-    bslot[(size_t)f * raw_cap + i] = atomicAdd(&bstart[(size_t)f * nb + b], 1);
-}
+// bucket_build, one workgroup per frame: floor(x) histogram in LDS (the atomic's return
+// value is the keypoint's slot in its bucket), exclusive scan to bucket starts, and the
+// bucket member lists -- the three passes of the counting sort with block barriers between
+// them instead of kernel boundaries.
+constexpr int kSortThreads = 1024;
+constexpr int kSortMaxBuckets = 4096 + 1;     // base width + 1 (frames <= 2047 px, scan key)
 
-__global__ void __launch_bounds__(1024)
-bucket_scan(int32_t *__restrict__ bstart, int nb) {   // counts -> exclusive starts, in place
-    __shared__ int sh[1024];
-    int32_t *c = bstart + (size_t)blockIdx.x * nb;
-    const int tid = threadIdx.x;
-    int carry = 0;
-    for (int base = 0; base < nb; base += 1024) {
-        const int v = base + tid < nb ? c[base + tid] : 0;
-        sh[tid] = v;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            const int t = tid >= off ? sh[tid - off] : 0;
-            __syncthreads();
-            sh[tid] += t;
-            __syncthreads();
-        }
-        if (base + tid < nb) c[base + tid] = carry + sh[tid] - v;
-        carry += sh[1023];
-        __syncthreads();
+__global__ void __launch_bounds__(kSortThreads)
+bucket_build(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
+             int32_t *__restrict__ bstart, int32_t *__restrict__ bslot, uint32_t *__restrict__ mem) {
+    __shared__ int32_t bc[kSortMaxBuckets];
+    __shared__ int32_t wsum[kSortThreads / 64];
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int cnt = raw_cnt[f * kCntStride];
+    if (cnt > raw_cap || nb > kSortMaxBuckets) return;   // emit_keypoints reports the overflow
+    const RawKp *rec = raw + (size_t)f * raw_cap;
+    int32_t *slot = bslot + (size_t)f * raw_cap;
+    for (int b = tid; b < nb; b += kSortThreads) bc[b] = 0;
+    __syncthreads();
+    for (int i = tid; i < cnt; i += kSortThreads) slot[i] = atomicAdd(&bc[x_bucket(rec[i].x, nb)], 1);
+    __syncthreads();
+    // exclusive scan of bc: each thread a contiguous run, wave scans of the run totals
+    const int per = (nb + kSortThreads - 1) / kSortThreads, b0 = tid * per;
+    int run = 0;
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) run += bc[b0 + k];
+    int incl = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
     }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int base = incl - run;
+    for (int w = 0; w < wv; ++w) base += wsum[w];
+    for (int k = 0; k < per; ++k) {
+        const int b = b0 + k;
+        if (b >= nb) break;
+        const int c = bc[b];
+        bc[b] = base;
+        bstart[(size_t)f * nb + b] = base;
+        base += c;
+    }
+    __syncthreads();
+    uint32_t *mb = mem + (size_t)f * raw_cap;
+    for (int i = tid; i < cnt; i += kSortThreads) mb[bc[x_bucket(rec[i].x, nb)] + slot[i]] = (uint32_t)i;
 }
 
-__global__ void __launch_bounds__(256)
-bucket_scatter(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
-               const int32_t *__restrict__ bstart, const int32_t *__restrict__ bslot,
-               uint32_t *__restrict__ mem) {
-    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
-    const int cnt = raw_cnt[f * kCntStride];
-    if (cnt > raw_cap || i >= cnt) return;
-    const int b = x_bucket(raw[(size_t)f * raw_cap + i].x, nb);
-    mem[(size_t)f * raw_cap + bstart[(size_t)f * nb + b] + bslot[(size_t)f * raw_cap + i]] = (uint32_t)i;
-}
+// Rank of each keypoint = bucket start + members that sort before it.  The same loop flags a
+// duplicate (remove_duplicate_keypoints :319-327 keeps the first of each run of equal (pt,
+// size, angle); those four are the comparator's leading keys, so such runs are contiguous
+// and a keypoint is dropped iff an equal one sorts before it): sorted[rank] = index | dup << 31.
+constexpr uint32_t kDupBit = 0x80000000u;
 
 __global__ void __launch_bounds__(256)
 bucket_rank(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
@@ -785,25 +806,33 @@ bucket_rank(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, 
     const int s = bstart[(size_t)f * nb + b];
     const int e = b + 1 < nb ? bstart[(size_t)f * nb + b + 1] : cnt;
     int r = s;
+    bool dup = false;
     for (int m = s; m < e; ++m) {
         const uint32_t j = mb[m];
         if (j == (uint32_t)i) continue;
         const RawKp &rj = rec[j];
         const unsigned long long kj = xy_key(rj);
-        r += kj < ki || (kj == ki && rec_before(rj, ri));
+        const bool before = kj < ki || (kj == ki && rec_before(rj, ri));
+        r += before;
+        dup |= before && rj.x == ri.x && rj.y == ri.y && rj.size == ri.size && rj.angle == ri.angle;
     }
-    if (r < cnt) sorted[(size_t)f * raw_cap + r] = (uint32_t)i;
+    if (r < cnt) sorted[(size_t)f * raw_cap + r] = (uint32_t)i | (dup ? kDupBit : 0u);
     else atomicExch(&sorted[(size_t)f * raw_cap], 0xFFFFFFFFu);   // order broken: flag
 }
 
-__global__ void __launch_bounds__(1024)
+// De-duplicated keypoints in sorted order, converted (convert_keypoints_to_input_image_size
+// :330-346), one workgroup per frame: a block scan of the keep flags over contiguous rank
+// runs, then every thread writes its run's kept keypoints (index loads batched so the
+// record loads of a run are in flight together).
+__global__ void __launch_bounds__(kSortThreads)
 emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
                const uint32_t *__restrict__ sorted, pano_kp *__restrict__ out, int cap,
                int32_t *__restrict__ counts, int32_t *__restrict__ err,
                const int32_t *__restrict__ ext_cnt, int ext_cap,
                const int32_t *__restrict__ cand_cnt, int cand_cap) {
-    __shared__ int32_t scan[1024];
-    const int f = blockIdx.x, tid = threadIdx.x;
+    __shared__ int32_t wsum[kSortThreads / 64];
+    __shared__ int32_t total;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const RawKp *rec = raw + (size_t)f * raw_cap;
     const uint32_t *idx = sorted + (size_t)f * raw_cap;
     const int cnt = raw_cnt[f * kCntStride];
@@ -811,61 +840,59 @@ emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cn
         if (tid == 0) { err[0] = PANO_E_OVERFLOW; counts[f] = -1; }
         return;
     }
-    // every slot must hold a live index (rank_keys is a permutation of 0..cnt-1)
-    int bad = 0;
-    for (int i = tid; i < cnt; i += 1024) bad |= idx[i] >= (uint32_t)cnt;
+    const int per = (cnt + kSortThreads - 1) / kSortThreads;
+    const int beg = tid * per, end = min(beg + per, cnt);
+    // every slot must hold a live index (the ranks are a permutation of 0..cnt-1)
+    int bad = 0, mine = 0;
+    for (int i = beg; i < end; ++i) {
+        const uint32_t v = idx[i];
+        bad |= (v & ~kDupBit) >= (uint32_t)cnt;
+        mine += (v & kDupBit) == 0;
+    }
     if (__syncthreads_or(bad)) {
         if (tid == 0) { err[0] = PANO_E_OVERFLOW; err[1] = 0x5017; counts[f] = -1; }
         return;
     }
-    // de-duplicate consecutive equal (pt, size, angle), then block-wide exclusive scan
-    const int per = (cnt + 1023) / 1024;
-    const int beg = tid * per;
-    int mine = 0;
-    for (int t = 0; t < per; ++t) {
-        const int i = beg + t;
-        if (i >= cnt) break;
-        bool keep = true;
-        if (i > 0) {
-            const RawKp &a = rec[idx[i - 1]], &b = rec[idx[i]];
-            keep = !(a.x == b.x && a.y == b.y && a.size == b.size && a.angle == b.angle);
-        }
-        mine += keep;
+    int incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
     }
-    scan[tid] = mine;
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int v = tid >= off ? scan[tid - off] : 0;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
-    }
-    int pos = scan[tid] - mine;
-    for (int t = 0; t < per; ++t) {
-        const int i = beg + t;
-        if (i >= cnt) break;
-        const RawKp &b = rec[idx[i]];
-        bool keep = true;
-        if (i > 0) {
-            const RawKp &a = rec[idx[i - 1]];
-            keep = !(a.x == b.x && a.y == b.y && a.size == b.size && a.angle == b.angle);
+    int pos = incl - mine;
+    for (int w = 0; w < wv; ++w) pos += wsum[w];
+    if (tid == kSortThreads - 1) total = pos + mine;
+    constexpr int B = 8;
+    for (int i0 = beg; i0 < end; i0 += B) {
+        uint32_t v[B];
+        RawKp r[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) v[k] = i0 + k < end ? idx[i0 + k] : kDupBit;
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+            if (!(v[k] & kDupBit)) r[k] = rec[v[k]];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            if (v[k] & kDupBit) continue;
+            if (pos < cap) {
+                pano_kp q;
+                q.x = r[k].x * 0.5f;
+                q.y = r[k].y * 0.5f;
+                q.size = r[k].size * 0.5f;
+                q.angle = r[k].angle;
+                q.response = r[k].response;
+                q.octave = (r[k].octave & ~255) | ((r[k].octave - 1) & 255);
+                out[(size_t)f * cap + pos] = q;
+            }
+            ++pos;
         }
-        if (!keep) continue;
-        if (pos < cap) {
-            pano_kp q;
-            q.x = b.x * 0.5f;
-            q.y = b.y * 0.5f;
-            q.size = b.size * 0.5f;
-            q.angle = b.angle;
-            q.response = b.response;
-            q.octave = (b.octave & ~255) | ((b.octave - 1) & 255);
-            out[(size_t)f * cap + pos] = q;
-        }
-        ++pos;
     }
-    if (tid == 1023) {
-        counts[f] = scan[1023];                  // the true count, even above cap
-        if (scan[1023] > cap) err[0] = PANO_E_OVERFLOW;   // keypoints past cap were dropped
+    __syncthreads();
+    if (tid == 0) {
+        counts[f] = total;                       // the true count, even above cap
+        if (total > cap) err[0] = PANO_E_OVERFLOW;   // keypoints past cap were dropped
     }
 }
 
@@ -950,15 +977,19 @@ __device__ __forceinline__ float atan2_oct(float y, float x) {
 // Descriptors, one WAVE per keypoint, persistent: waves stride over the keypoints of the
 // whole batch (no workgroups for empty capacity slots).  Per keypoint the wave derives, per
 // patch column, the row interval inside the rotated square and the image (conservative; the
-// exact bin test is per sample), scans the interval lengths into a dense sample index, and
-// each lane walks its own run of that index down patch columns (the gradient taps come from
-// a sliding window of row triples: one 12-byte load per sample, the next one in flight while
-// the current sample is binned; neighbouring lanes are Q samples apart: different cells /
-// orientations, few same-address LDS atomics).  Each sample is spread trilinearly into the
-// wave's 6 x 6 x 8 histogram (padding bins included: no bounds branches) as 2^22 fixed-point
-// u64 LDS atomics -- integer sums, deterministic and order independent (LDS f32 atomics
-// measured 5x slower on gfx950).  The normalisation is the reference's, np.linalg.norm in
-// OpenBLAS's sdot order across the lanes.
+// exact bin test is per sample), merges them over STRIPS of kDescSW adjacent columns (union
+// interval), scans the strip lengths into a dense (strip, row) index, and each lane walks its
+// own run of that index down strips.  The gradient taps come from a sliding window of three
+// image rows x (kDescSW + 2) columns: ONE wide load per step serves the strip's kDescSW
+// samples (the kernel is bound by tap-load instructions -- each lane touches its own cache
+// line -- so 4 samples per load instead of 1 cut it 0.35 -> 0.28 ms at parrington), the next
+// step's load in flight while the current samples are binned; neighbouring lanes are Q steps
+// apart: different cells / orientations, few same-address LDS atomics.  Each sample is
+// spread trilinearly into the wave's 6 x 6 x 8 histogram (padding bins included: no bounds
+// branches) as 2^22 fixed-point u64 LDS atomics, into one of kDescCopies interleaved copies
+// (copy = lane % kDescCopies, summed at the end) -- integer sums, deterministic and order
+// independent (LDS f32 atomics measured 5x slower on gfx950).  The normalisation is the
+// reference's, np.linalg.norm in OpenBLAS's sdot order across the lanes.
 //
 // Arithmetic (generate_descriptors :361-526): every per-sample quantity is f32.  Everything
 // the reference computes in float64 (rotation, bins, weights) enters only through continuous
@@ -975,6 +1006,15 @@ constexpr int kDescCols = 128;        // patch sides up to this use the dense in
                                       // parameters: side <= 73)
 constexpr int kHist = 6 * 6 * 8;      // padded histogram (reference: tensor of (ww+2, ww+2, nb))
 constexpr float kFix = 4194304.0f;    // 2^22: contributions <= 255 sqrt(2) fit a u32
+#ifndef PANO_DESC_SW
+#define PANO_DESC_SW 4                // patch columns per strip: one (SW + 2)-float load per step
+#endif
+constexpr int kDescSW = PANO_DESC_SW;
+#ifndef PANO_DESC_COPIES
+#define PANO_DESC_COPIES 2            // histogram copies per wave (copy = lane % copies)
+#endif
+constexpr int kDescCopies = PANO_DESC_COPIES;
+static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "strip width divides 64");
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
                                       // 3: every sample's taps from one cached location)
@@ -1007,16 +1047,20 @@ __device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ coun
     return false;
 }
 
+#ifndef PANO_DESC_OCC
+#define PANO_DESC_OCC 4               // waves per SIMD the register budget is sized for
+#endif
 template <bool OUT_U8>
-__global__ void __launch_bounds__(64 * kDescWaves, 5)
+__global__ void __launch_bounds__(64 * kDescWaves, PANO_DESC_OCC)
 descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int32_t *__restrict__ counts, int n_frames, int cap, int32_t *__restrict__ work,
                 float *__restrict__ desc, uint8_t *__restrict__ desc_u8, int32_t *__restrict__ norms) {
-    __shared__ unsigned long long hist[kDescWaves][kHist];
+    __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHist];
     __shared__ int col_lo[kDescWaves][kDescCols], col_pre[kDescWaves][kDescCols + 1];
     __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    unsigned long long *h = hist[wv];
+    unsigned long long *h0 = hist[wv];
+    unsigned long long *h = h0 + (lane & (kDescCopies - 1)) * kHist;   // this lane's copy
     int *clo = col_lo[wv], *cpre = col_pre[wv];
     float *cbr = col_br[wv], *cbc = col_bc[wv];
     // XCD-aware split (workgroup b runs on XCD b % 8): each XCD takes one contiguous eighth of
@@ -1043,7 +1087,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         if (lane == 0) gk = atomicAdd(wq, 1);
         gk = lo_k + __shfl(gk, 0);
         if (gk >= hi_k || !locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
-        for (int i = lane; i < kHist; i += 64) h[i] = 0ull;
+        for (int i = lane; i < kDescCopies * kHist; i += 64) h0[i] = 0ull;
         const pano_kp kp = kps[(size_t)f * cap + k];
         int oct = kp.octave & 255;
         if (oct >= 128) oct |= -128;
@@ -1107,15 +1151,19 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const double ia_r = fabs(cos_a) < 1e-12 ? 0.0 : 1.0 / cos_a;
             const double ia_c = fabs(sin_a) < 1e-12 ? 0.0 : -1.0 / sin_a;
             const float kq = (float)(-0.125 * 1.4426950408889634 * inv_hw * inv_hw);
+            constexpr int kEmpty = 1 << 20;
             int run = 0;                                   // wave-wide running total
             for (int c4 = 0; c4 < side; c4 += 64) {
                 const int c = c4 + lane;
-                int lo = 1, hi = 0;
+                int lo = kEmpty, hi = -kEmpty;
+                // a column outside the patch or the image gets a bin base no sample passes
+                // (rbin >= 4): its strip-mates' rows are walked, its own samples rejected
+                float brc = 1e30f, bcc = 1e30f;
                 if (c < side) {
                     const int xs = c - half, cc = px + xs;
-                    cbr[c] = (float)((double)xs * sr) + 1.5f;
-                    cbc[c] = (float)((double)xs * cr) + 1.5f;
                     if (cc > 0 && cc < cols - 1) {
+                        brc = (float)((double)xs * sr) + 1.5f;
+                        bcc = (float)((double)xs * cr) + 1.5f;
                         lo = max(-half, 1 - py);
                         hi = min(half, rows - 2 - py);
                         const double bvs[2] = {xs * sin_a, xs * cos_a};
@@ -1133,86 +1181,112 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                             lo = max(lo, (int)ceil(l));
                             hi = min(hi, (int)floor(u));
                         }
+                        if (hi < lo) { lo = kEmpty; hi = -kEmpty; }
                     }
                 }
-                const int n_c = hi >= lo ? hi - lo + 1 : 0;
-                int incl = n_c;
+                cbr[c] = brc;
+                cbc[c] = bcc;
+                // strip = kDescSW adjacent columns: the union of their row intervals (the
+                // exact bin test per sample rejects the extra rows)
+#pragma unroll
+                for (int d = 1; d < kDescSW; d <<= 1) {
+                    lo = min(lo, __shfl_xor(lo, d));
+                    hi = max(hi, __shfl_xor(hi, d));
+                }
+                const bool lead = (lane & (kDescSW - 1)) == 0;
+                const int n_s = lead && hi >= lo ? hi - lo + 1 : 0;
+                int incl = n_s;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
                     const int t = __shfl_up(incl, d);
                     if (lane >= d) incl += t;
                 }
-                if (c < side) {
-                    clo[c] = lo;
-                    cpre[c] = run + incl - n_c;
+                if (lead && c < side) {
+                    clo[c / kDescSW] = lo;
+                    cpre[c / kDescSW] = run + incl - n_s;
                 }
                 run += __shfl(incl, 63);
             }
-            if (lane == 0) cpre[side] = run;
+            const int nstrip = (side + kDescSW - 1) / kDescSW;
+            if (lane == 0) cpre[nstrip] = run;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int nsamp = run;
+            const int nsamp = run;                         // (strip, row) steps
             const int Q = (nsamp + 63) >> 6;
             int t = lane * Q;
             const int tend = min(t + Q, nsamp);
             if (t < tend) {
-                int c = 0, c1 = side - 1;                  // largest c with cpre[c] <= t
-                while (c < c1) {
-                    const int mid = (c + c1 + 1) >> 1;
-                    if (cpre[mid] <= t) c = mid;
-                    else c1 = mid - 1;
+                int sx = 0, s1 = nstrip - 1;               // largest strip with cpre[sx] <= t
+                while (sx < s1) {
+                    const int mid = (sx + s1 + 1) >> 1;
+                    if (cpre[mid] <= t) sx = mid;
+                    else s1 = mid - 1;
                 }
-                int ys = clo[c] + (t - cpre[c]);
-                int yend = clo[c] + (cpre[c + 1] - cpre[c]);
-                // (x-1, x, x+1) of image row py + y at patch column cc
-                auto trip = [&](int cc, int y, float (&T)[3]) {
+                int ys = clo[sx] + (t - cpre[sx]);
+                int yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                // columns x-1 .. x+kDescSW of image row py + y at strip sx: ONE wide load per
+                // step serves the strip's kDescSW samples.  Rows stay in [0, rows - 1]; the
+                // columns of a strip with an invalid column can reach kDescSW floats before or
+                // after the row (the neighbouring row or level plane of the same pyramid
+                // buffer: allocated), and those samples are rejected before their taps are used
+                constexpr int WN = kDescSW + 2;
+                auto win = [&](int sxx, int y, float (&T)[WN]) {
 #if PANO_DESC_ABL == 3
-                    const float *q = img + (size_t)py * cols + px + ((cc + y) & 1) - 1;   // L1-resident
+                    const float *q = img + (size_t)py * cols + px + ((sxx + y) & 1) - 1;   // L1-resident
 #else
-                    const float *q = img + (size_t)(py + y) * cols + (px + cc - half) - 1;
+                    const float *q = img + (size_t)(py + y) * cols + (px + sxx * kDescSW - half) - 1;
 #endif
-                    T[0] = q[0];
-                    T[1] = q[1];
-                    T[2] = q[2];
+#pragma unroll
+                    for (int i = 0; i < WN; ++i) T[i] = q[i];
                 };
-                float br = cbr[c], bc = cbc[c], xs2 = (float)((c - half) * (c - half));
-                float Tm[3], T0[3], Tp[3];
-                trip(c, ys - 1, Tm);
-                trip(c, ys, T0);
-                trip(c, ys + 1, Tp);
+                float br[kDescSW], bc[kDescSW], xs2[kDescSW];
+                auto strip_consts = [&](int sxx) {
+#pragma unroll
+                    for (int i = 0; i < kDescSW; ++i) {
+                        const int c = sxx * kDescSW + i;
+                        br[i] = cbr[c];
+                        bc[i] = cbc[c];
+                        xs2[i] = (float)((c - half) * (c - half));
+                    }
+                };
+                strip_consts(sx);
+                float Tm[WN], T0[WN], Tp[WN];
+                win(sx, ys - 1, Tm);
+                win(sx, ys, T0);
+                win(sx, ys + 1, Tp);
                 for (int j = t; j < tend; ++j) {
-                    // the next sample's position (this column, or the next non-empty one),
-                    // its taps loaded while this sample is binned
-                    int cn = c, yn = ys + 1;
+                    // the next step's position (this strip, or the next non-empty one), its
+                    // taps loaded while this step's samples are binned
+                    int sn = sx, yn = ys + 1;
                     const bool more = j + 1 < tend;
-                    const bool newcol = more && yn >= yend;
-                    if (newcol) {
-                        do { ++cn; } while (cpre[cn + 1] == cpre[cn]);
-                        yn = clo[cn];
+                    const bool newstrip = more && yn >= yend;
+                    if (newstrip) {
+                        do { ++sn; } while (cpre[sn + 1] == cpre[sn]);
+                        yn = clo[sn];
                     }
-                    float N0[3], N1[3], N2[3];
-                    if (newcol) {
-                        trip(cn, yn - 1, N0);
-                        trip(cn, yn, N1);
+                    float N0[WN], N1[WN], N2[WN];
+                    if (newstrip) {
+                        win(sn, yn - 1, N0);
+                        win(sn, yn, N1);
                     }
-                    if (more) trip(cn, yn + 1, N2);
-                    const float ysf = (float)ys;
+                    if (more) win(sn, yn + 1, N2);
+                    const float ysf = (float)ys, ys2 = ysf * ysf;
                     // exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) = exp2(kq (xs^2 + ys^2)): a rotation
                     // keeps the radius (no LDS read on the sample path)
-                    sample(T0[2] - T0[0], Tm[1] - Tp[1], fmaf(ysf, ar, br), fmaf(ysf, ac, bc),
-                           __builtin_amdgcn_exp2f(kq * fmaf(ysf, ysf, xs2)));
-                    if (newcol) {
-                        c = cn;
-                        yend = clo[c] + (cpre[c + 1] - cpre[c]);
-                        br = cbr[c];
-                        bc = cbc[c];
-                        xs2 = (float)((c - half) * (c - half));
 #pragma unroll
-                        for (int i = 0; i < 3; ++i) { Tm[i] = N0[i]; T0[i] = N1[i]; Tp[i] = N2[i]; }
+                    for (int i = 0; i < kDescSW; ++i)
+                        sample(T0[i + 2] - T0[i], Tm[i + 1] - Tp[i + 1], fmaf(ysf, ar, br[i]),
+                               fmaf(ysf, ac, bc[i]), __builtin_amdgcn_exp2f(kq * (ys2 + xs2[i])));
+                    if (newstrip) {
+                        sx = sn;
+                        yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                        strip_consts(sx);
+#pragma unroll
+                        for (int i = 0; i < WN; ++i) { Tm[i] = N0[i]; T0[i] = N1[i]; Tp[i] = N2[i]; }
                     } else {
 #pragma unroll
-                        for (int i = 0; i < 3; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; Tp[i] = N2[i]; }
+                        for (int i = 0; i < WN; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; Tp[i] = N2[i]; }
                     }
                     ys = yn;
                 }
@@ -1238,7 +1312,10 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // crop the padding: element i = (r, c, o) of the 4 x 4 x 8 block
         auto interior = [&](int i) {
-            const unsigned long long v = h[((i >> 5) + 1) * 48 + (((i >> 3) & 3) + 1) * 8 + (i & 7)];
+            const int e = ((i >> 5) + 1) * 48 + (((i >> 3) & 3) + 1) * 8 + (i & 7);
+            unsigned long long v = 0;
+#pragma unroll
+            for (int c = 0; c < kDescCopies; ++c) v += h0[c * kHist + e];
             return (float)((double)v * (1.0 / 4194304.0));
         };
         float lo = interior(lane), hi = interior(64 + lane);
@@ -1449,27 +1526,18 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         {
             PanoProf prof_(ctx, PK_ORIENT);
             orientation<<<blocks, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap, n, ori_work,
-                                                         ctx->raw, raw_cnt, (int)raw_cap, bstart, nb * n);
+                                                         ctx->raw, raw_cnt, (int)raw_cap);
         }
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
     {
         dim3 grid((unsigned)((raw_cap + 255) / 256), n);
+        if (nb > kSortMaxBuckets) return pano_fail(ctx, PANO_E_UNSUPPORTED, "frame too wide for the keypoint sort");
         {
             PanoProf prof_(ctx, PK_SORT);
-            bucket_count<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, bslot);
+            bucket_build<<<n, kSortThreads, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, bslot, mem);
         }
-        PANO_LAUNCH_CHECK(ctx, "bucket_count");
-        {
-            PanoProf prof_(ctx, PK_SORT);
-            bucket_scan<<<n, 1024, 0, ctx->stream>>>(bstart, nb);
-        }
-        PANO_LAUNCH_CHECK(ctx, "bucket_scan");
-        {
-            PanoProf prof_(ctx, PK_SORT);
-            bucket_scatter<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, bslot, mem);
-        }
-        PANO_LAUNCH_CHECK(ctx, "bucket_scatter");
+        PANO_LAUNCH_CHECK(ctx, "bucket_build");
         {
             PanoProf prof_(ctx, PK_SORT);
             bucket_rank<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, mem,
@@ -1478,7 +1546,7 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         PANO_LAUNCH_CHECK(ctx, "bucket_rank");
         {
             PanoProf prof_(ctx, PK_SORT);
-            emit_keypoints<<<n, 1024, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted,
+            emit_keypoints<<<n, kSortThreads, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted,
                                                         kps, cap, counts, err, ext_cnt, (int)ext_cap,
                                                         cand_cnt, (int)cand_cap);
         }

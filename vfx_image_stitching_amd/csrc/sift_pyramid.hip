@@ -266,6 +266,9 @@ gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t 
 // Register-blocked sliding window: SEG consecutive outputs of one row (or column) from
 // SEG + NT - 1 staged inputs; output j receives taps t = 0..NT-1 in order (the oracle's
 // sequential sum), all index arithmetic compile-time after unrolling.
+#ifndef PANO_TAIL_SYNC
+#define PANO_TAIL_SYNC 0    // 1: full __syncthreads in blur_tail (A/B of lds_barrier)
+#endif
 #ifndef PANO_BLUR_ABL
 #define PANO_BLUR_ABL 0     // timing ablations of blur_fast only: bit 1 no FMAs, 2 no stores, 4 no loads
 #endif
@@ -499,6 +502,20 @@ __device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_N
     return (int)floor(d * inv);
 }
 
+// Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global stores (__syncthreads' release fence drains every outstanding HBM write of the wave,
+// a few microseconds per barrier; the tail writes each level's planes while it cascades and
+// nothing in the kernel reads them back).
+__device__ __forceinline__ void lds_barrier() {
+#if PANO_TAIL_SYNC
+    __syncthreads();
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#endif
+}
+
 // One tail level, compile-time tap count (NT = 0: runtime count n).  in / outb are [64][kTP]
 // LDS planes; g / d the frame's Gaussian and DoG planes in HBM.  The small octaves are all
 // border: instead of reflecting every tap (a runtime modulo per tap and output), the level
@@ -545,7 +562,7 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
         const int y = i / PW, c = i - (i / PW) * PW;
         pad[y * kPP + c] = in[y * kTP + reflect101(c - R, W)];
     }
-    __syncthreads();
+    lds_barrier();
     // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
     const int nseg = (W + SG - 1) / SG;
     for (int it = tid; it < H * nseg; it += kTailThreads) {
@@ -556,14 +573,14 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
         for (int j = 0; j < SG; ++j)
             if (x0 + j < W) rowt[(y + R) * kTP + x0 + j] = (float)acc[j];
     }
-    __syncthreads();
+    lds_barrier();
     // reflected rows of the row-pass output
     for (int i = tid; i < 2 * R * W; i += kTailThreads) {
         const int q = i / W, x = i - (i / W) * W;
         const int ry = q < R ? q - R : H + (q - R);
         rowt[(ry + R) * kTP + x] = rowt[(reflect101(ry, H) + R) * kTP + x];
     }
-    __syncthreads();
+    lds_barrier();
     // column pass: item = (column x, segment of SG rows); lanes on consecutive columns
     const int nrs = (H + SG - 1) / SG;
     for (int it = tid; it < W * nrs; it += kTailThreads) {
@@ -613,7 +630,7 @@ blur_tail(TailArgs ta) {
             }
             cur = dst;
             keep = -1;
-            __syncthreads();
+            lds_barrier();
         }
         for (int l = 1; l < ta.n_lvl; ++l) {
             const int n = ta.ntap[l];
@@ -630,7 +647,7 @@ blur_tail(TailArgs ta) {
                 case 27: tail_level<27>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
                 default: tail_level<0>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
             }
-            __syncthreads();
+            lds_barrier();
             cur = out;
             if (l == ta.n_lvl - 3) keep = cur;
         }
