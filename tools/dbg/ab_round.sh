@@ -12,8 +12,9 @@ fi
 BENCH_ARGS="--steps 10 --warmup 2" bash tools/dbg/ab_bench.sh || exit $?
 if [ "${AB_SYN:-0}" = 1 ]; then
   for v in base ${VARIANTS}; do
-    if [ $v = base ]; then L=""; else L=tools/ab/libpano_$v.so; fi
-    PANO_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --workload synthetic --steps 4 --warmup 1 > gpurun_out/abs_$v.txt 2>&1 || exit $?
+    L=""; E=""
+    case $v in base) ;; env:*) E=${v#env:} ;; *) L=tools/ab/libpano_$v.so ;; esac
+    env $E PANO_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --workload synthetic --steps 4 --warmup 1 > gpurun_out/abs_$v.txt 2>&1 || exit $?
     python3 -c "
 import json;d=json.loads(open('gpurun_out/abs_$v.txt').read().strip().split('\n')[-1]);print('syn $v', d['ms_per_step'], json.dumps(d['kernels_ms_per_step']))"
   done
