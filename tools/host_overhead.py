@@ -36,4 +36,4 @@ torch.cuda.synchronize()
 t4 = time.perf_counter()
 print(f"run(): {(t1 - t0) / N * 1e6:.1f} us/stitch; launch+wait only: {(t2 - t1) / N * 1e6:.1f} us; "
       f"launch only (async, {N} queued): {(t3 - t2) / N * 1e6:.1f} us CPU per launch, "
-      f"drain {(t4 - t3) * 1e3:.1f} ms")
+      f"drain {(t4 - t3) * 1e3:.1f} ms; back-to-back GPU time {(t4 - t2) / N * 1e6:.1f} us/graph")

@@ -707,7 +707,11 @@ int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, fl
         constexpr int TYT = tall_rows(NT);
         // tall tiles only where they still leave >= 6 workgroups per CU (octave 0 of a batch):
         // on smaller planes the lost parallelism costs more than the halo saves
-        const bool use_tall = tall && (long)grid.x * ((H + TYT - 1) / TYT) * n >= 1536;
+        static const long tall_min = [] {
+            const char *e = getenv("PANO_BLUR_TALL_MIN");   // fewest tall-tile workgroups
+            return e ? atol(e) : 1536L;
+        }();
+        const bool use_tall = tall && (long)grid.x * ((H + TYT - 1) / TYT) * n >= tall_min;
         const int ty = use_tall ? TYT : TY;
         const size_t sm = (size_t)((ty + 2 * R) * ((TX + 2 * R) | 1) + (MODE == MODE_BASE ? kPatchR * kPatchP : 0)) *
                           sizeof(float);
