@@ -511,6 +511,9 @@ localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
 
 
 // ------------------------------------------------------------------ S7
+#ifndef PANO_ORI_ABL
+#define PANO_ORI_ABL 0         // timing ablations of orientation only (bit 1: no atan2f, 2: no expf)
+#endif
 #ifndef PANO_ORI_COPIES
 #define PANO_ORI_COPIES 1      // histogram copies per wave (measured: 4 and 8 no faster)
 #endif
@@ -637,8 +640,16 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
                     gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
                 }
                 const float mag = sqrtf(gx * gx + gy * gy);
+#if PANO_ORI_ABL & 1                                  // timing ablation: no atan2f
+                const float ang = fabsf(gy + gx) * 3.0f;
+#else
                 const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+#endif
+#if PANO_ORI_ABL & 2                                  // timing ablation: no expf
+                const float w = wfac * (float)(dx * dx + dy * dy) + 1.0f;
+#else
                 const float w = expf(wfac * (float)(dx * dx + dy * dy));
+#endif
                 const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
                 const double val = (double)(w * mag);
                 atomicAdd(&hist[wv][lane % kOriCopies][bin], rint_fix(val * kHistScale));
@@ -977,17 +988,21 @@ __device__ __forceinline__ float atan2_oct(float y, float x) {
 // Descriptors, one WAVE per keypoint, persistent: waves stride over the keypoints of the
 // whole batch (no workgroups for empty capacity slots).  Per keypoint the wave derives, per
 // patch column, the row interval inside the rotated square and the image (conservative; the
-// exact bin test is per sample), merges them over STRIPS of kDescSW adjacent columns (union
-// interval), scans the strip lengths into a dense (strip, row) index, and each lane walks its
-// own run of that index down strips.  The gradient taps come from a sliding window of three
-// image rows x (kDescSW + 2) columns: ONE wide load per step serves the strip's kDescSW
-// samples (the kernel is bound by tap-load instructions -- each lane touches its own cache
-// line -- so 4 samples per load instead of 1 cut it 0.35 -> 0.28 ms at parrington), the next
-// step's load in flight while the current samples are binned; neighbouring lanes are Q steps
-// apart: different cells / orientations, few same-address LDS atomics.  Each sample is
+// exact bin test is per sample), merges them over SUPER-STRIPS of kDescGrp x kDescSW
+// adjacent columns (union interval), scans their lengths into a dense (super-strip, row)
+// index, and each group of kDescGrp adjacent lanes walks its own run of that index, lane
+// `sub` of the group taking strip `sub` (kDescSW columns) of each super-strip row.  The
+// gradient taps come from a sliding window of three image rows x (kDescSW + 2) columns: ONE
+// wide load per step serves the strip's kDescSW samples, the next step's load in flight while
+// the current samples are binned, and a group's loads of one step fall in ~one cache line.
+// The kernel is bound by its tap loads missing L1 (every step of a lane is a new image row;
+// a timing ablation with L1-resident taps runs 3x faster): 4 samples per load instead of 1
+// cut it 0.35 -> 0.25 ms at parrington.  Groups are Q steps apart: different cells /
+// orientations, few same-address LDS atomics.  Each sample is
 // spread trilinearly into the wave's 6 x 6 x 8 histogram (padding bins included: no bounds
 // branches) as 2^22 fixed-point u64 LDS atomics, into one of kDescCopies interleaved copies
-// (copy = lane % kDescCopies, summed at the end) -- integer sums, deterministic and order
+// (copy = lane % kDescCopies >= kDescGrp, so a group's lanes never share an address; summed at
+// the end) -- integer sums, deterministic and order
 // independent (LDS f32 atomics measured 5x slower on gfx950).  The normalisation is the
 // reference's, np.linalg.norm in OpenBLAS's sdot order across the lanes.
 //
@@ -1013,7 +1028,15 @@ constexpr int kDescSW = PANO_DESC_SW;
 #ifndef PANO_DESC_COPIES
 #define PANO_DESC_COPIES 2            // histogram copies per wave (copy = lane % copies)
 #endif
-constexpr int kDescCopies = PANO_DESC_COPIES;
+#ifndef PANO_DESC_GRP
+#define PANO_DESC_GRP 2               // lanes walking one row of kDescGrp adjacent strips together
+#endif
+constexpr int kDescGrp = PANO_DESC_GRP;
+constexpr int kDescSS = kDescSW * kDescGrp;   // columns of a group's super-strip
+// a group's lanes bin into different histogram copies: no same-address atomics among them
+constexpr int kDescCopies = PANO_DESC_COPIES > kDescGrp ? PANO_DESC_COPIES : kDescGrp;
+static_assert(kDescSS <= 16 && (kDescGrp & (kDescGrp - 1)) == 0, "super-strip divides 64");
+
 static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "strip width divides 64");
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
@@ -1186,14 +1209,14 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 }
                 cbr[c] = brc;
                 cbc[c] = bcc;
-                // strip = kDescSW adjacent columns: the union of their row intervals (the
-                // exact bin test per sample rejects the extra rows)
+                // super-strip = kDescSS adjacent columns: the union of their row intervals
+                // (the exact bin test per sample rejects the extra rows)
 #pragma unroll
-                for (int d = 1; d < kDescSW; d <<= 1) {
+                for (int d = 1; d < kDescSS; d <<= 1) {
                     lo = min(lo, __shfl_xor(lo, d));
                     hi = max(hi, __shfl_xor(hi, d));
                 }
-                const bool lead = (lane & (kDescSW - 1)) == 0;
+                const bool lead = (lane & (kDescSS - 1)) == 0;
                 const int n_s = lead && hi >= lo ? hi - lo + 1 : 0;
                 int incl = n_s;
 #pragma unroll
@@ -1202,19 +1225,24 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                     if (lane >= d) incl += t;
                 }
                 if (lead && c < side) {
-                    clo[c / kDescSW] = lo;
-                    cpre[c / kDescSW] = run + incl - n_s;
+                    clo[c / kDescSS] = lo;
+                    cpre[c / kDescSS] = run + incl - n_s;
                 }
                 run += __shfl(incl, 63);
             }
-            const int nstrip = (side + kDescSW - 1) / kDescSW;
+            const int nstrip = (side + kDescSS - 1) / kDescSS;
             if (lane == 0) cpre[nstrip] = run;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int nsamp = run;                         // (strip, row) steps
-            const int Q = (nsamp + 63) >> 6;
-            int t = lane * Q;
+            // lane group g (kDescGrp adjacent lanes) walks its run of (super-strip, row) steps;
+            // lane `sub` of the group takes strip `sub` of each super-strip, so one load
+            // instruction covers a group's kDescSS-column row span in ~1 cache line
+            const int nsamp = run;                         // (super-strip, row) steps
+            constexpr int NG = 64 / kDescGrp;
+            const int Q = (nsamp + NG - 1) / NG;
+            const int sub = lane & (kDescGrp - 1);
+            int t = (lane / kDescGrp) * Q;
             const int tend = min(t + Q, nsamp);
             if (t < tend) {
                 int sx = 0, s1 = nstrip - 1;               // largest strip with cpre[sx] <= t
@@ -1235,7 +1263,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
 #if PANO_DESC_ABL == 3
                     const float *q = img + (size_t)py * cols + px + ((sxx + y) & 1) - 1;   // L1-resident
 #else
-                    const float *q = img + (size_t)(py + y) * cols + (px + sxx * kDescSW - half) - 1;
+                    const float *q = img + (size_t)(py + y) * cols + (px + sxx * kDescSS + sub * kDescSW - half) - 1;
 #endif
 #pragma unroll
                     for (int i = 0; i < WN; ++i) T[i] = q[i];
@@ -1244,7 +1272,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 auto strip_consts = [&](int sxx) {
 #pragma unroll
                     for (int i = 0; i < kDescSW; ++i) {
-                        const int c = sxx * kDescSW + i;
+                        const int c = sxx * kDescSS + sub * kDescSW + i;
                         br[i] = cbr[c];
                         bc[i] = cbc[c];
                         xs2[i] = (float)((c - half) * (c - half));

@@ -481,10 +481,16 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
 // Two barriers per level.  Odd LDS pitch (65): lanes on consecutive rows / columns are
 // bank-conflict free.  Per output it is blur_level's arithmetic (sequential fma in tap
 // order, one f32 rounding per pass), hence bit-identical.
-constexpr int kTailDim = 64;
+#ifndef PANO_TAIL_DIM
+#define PANO_TAIL_DIM 64                      // octaves whose planes fit this square join the tail
+#endif
+#ifndef PANO_TAIL_THREADS
+#define PANO_TAIL_THREADS 512
+#endif
+constexpr int kTailDim = PANO_TAIL_DIM;
 constexpr int kTailOct = 8;
 constexpr int kTP = kTailDim + 1;             // LDS pitch
-constexpr int kTailThreads = 512;
+constexpr int kTailThreads = PANO_TAIL_THREADS;
 
 struct TailArgs {
     const float *prev;                          // G[o_tail-1][n_lvl-3], frame stride ph*pw
