@@ -5,7 +5,7 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
 A step = one whole stitch of one rank's sequence, inputs resident in HBM:
-cylindrical projection -> SIFT features of every frame -> NN match (fp32 MFMA) -> RANSAC
+cylindrical projection -> SIFT features of every frame -> NN match (exact i8 MFMA) -> RANSAC
 -> [N>1: all_gather of per-pair records] -> drift correction + composite plan -> composite
 (band) -> crop bounding box [N>1: 4-int all_reduce].  Rank r stitches the parrington loop
 starting at frame 17 r (18 frames, 17 pairs): per-GPU work is fixed ("weak" scaling) and the
@@ -14,8 +14,11 @@ job is one panorama of N laps, N*17 + 1 distinct frames.
 value  = distinct input Mpx of the job / max-over-ranks seconds per step.
 roofline: the dominant kernel, timed live with HIP events on the library's stream over the
 timed region (libpano pano_prof_*), against its algorithmic bytes (DESIGN.md "Roofline").
-cpu_baseline: the oracle (numpy restatement, bit-exact vs the reference) on rank 0 at N=1
-over a bounded sample (first 4 frames = 3 pairs of the same workload), 1 thread.
+cpu_baseline: the oracle (numpy restatement, bit-exact vs the reference) on rank 0 at N=1,
+per-frame SIFT on a pool of single-threaded workers (one per host core it may use, <= 16),
+the rest on one core; `cores` says how many.
+pcie_inclusive: the same stitch with the frames uploaded from and the crop downloaded to
+pinned host memory every step (never `value`).
 """
 from __future__ import annotations
 
@@ -364,24 +367,46 @@ def main():
 
 def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx):
     """Host-to-host stitch rate: per step, the uint8 frames go pinned host -> HBM (into the
-    resident input buffer), the stitch runs, and the cropped panorama comes back to pinned
-    host memory; steps bracketed by synchronize like the timed region."""
+    resident input buffer), the stitch runs, and the crop's canvas rows come back to pinned
+    host memory in one contiguous copy (the panorama is a view of them, as the device result
+    is a view of the canvas); steps bracketed by synchronize like the timed region.  The H2D
+    and D2H legs are also timed alone (HIP events) so a slow PCIe path shows as such."""
     import torch
     host_in = torch.from_numpy(np.ascontiguousarray(frames)).pin_memory()
     res = st.run(dev, focals, margin=margin, graph=graph)
     host_out = torch.empty(res.canvas.numel(), dtype=torch.uint8).pin_memory()
+
+    def rows_of(res):
+        """The canvas rows holding the crop, as one contiguous device range (flat uint8)."""
+        pano = res.panorama
+        base = res.canvas.reshape(-1)
+        row = res.canvas.stride(0)
+        first = (pano.storage_offset() - res.canvas.storage_offset()) // row
+        return base[first * row:(first + pano.shape[0]) * row], pano
+
+    flat, pano = rows_of(res)
+    cur = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(cur)
+    dev.copy_(host_in, non_blocking=True)
+    ev[1].record(cur)
+    host_out[:flat.numel()].copy_(flat, non_blocking=True)
+    ev[2].record(cur)
     torch.cuda.synchronize()
+    h2d_ms, d2h_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
     t0 = time.perf_counter()
     for _ in range(steps):
         dev.copy_(host_in, non_blocking=True)
-        pano = st.run(dev, focals, margin=margin, graph=graph).panorama
-        host_out[:pano.numel()].view(pano.shape).copy_(pano, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
+        flat, pano = rows_of(st.run(dev, focals, margin=margin, graph=graph))
+        host_out[:flat.numel()].copy_(flat, non_blocking=True)
+        cur.synchronize()
     el = (time.perf_counter() - t0) / steps
     return {"value": round(mpx / el, 3), "unit": "Mpx/s", "ms_per_step": round(el * 1e3, 4),
-            "includes": "pinned H2D of the uint8 frames + stitch + pinned D2H of the cropped "
-                        "panorama, per step (SURVEY 8(d) wall, JPEG I/O excluded)",
-            "bytes_h2d": int(host_in.numel()), "bytes_d2h": int(pano.numel())}
+            "includes": "pinned H2D of the uint8 frames + stitch + pinned D2H of the crop's canvas "
+                        "rows, per step (SURVEY 8(d) wall, JPEG I/O excluded)",
+            "h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
+            "bytes_h2d": int(host_in.numel()), "bytes_d2h": int(flat.numel()),
+            "panorama_bytes": int(pano.numel())}
 
 
 def check_parity(st, dev, focals, margin, workload, method, graph):

@@ -551,6 +551,41 @@ __device__ __forceinline__ bool locate_strided(const int32_t *__restrict__ count
     return false;
 }
 
+// Persistent waves claim their next work item one item ahead (kClaimAhead), so the queue
+// atomic's latency overlaps the current item, or when they finish one.  Measured: ahead is
+// slower at parrington (a wave holding a claimed item behind a long one delays the drain).
+#ifndef PANO_CLAIM_AHEAD
+#define PANO_CLAIM_AHEAD 0
+#endif
+constexpr bool kClaimAhead = PANO_CLAIM_AHEAD != 0;
+
+// The dense work index of a persistent wave -> (frame, index).  For <= 64 frames the clamped
+// counts and their inclusive prefix live in registers (lane = frame), loaded once per wave, so
+// each dequeue is one ballot and two lane reads instead of a scan over HBM-resident counts.
+struct FrameIndex {
+    int c = 0, incl = 0;
+    bool regs = false;
+    __device__ void init(const int32_t *__restrict__ counts, int stride, int n_frames, int cap) {
+        const int lane = threadIdx.x & 63;
+        regs = n_frames <= 64;
+        if (!regs) return;
+        c = lane < n_frames ? counts[lane * stride] : 0;
+        c = c < 0 ? 0 : (c < cap ? c : cap);
+        incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+    }
+    // gk < total (the caller's bound): frames wholly before gk, then the offset inside
+    __device__ __forceinline__ void locate(int gk, int &f, int &k) const {
+        const int j = __popcll(__ballot(incl <= gk));
+        f = j;
+        k = gk - (__shfl(incl, j) - __shfl(c, j));
+    }
+};
+
 // One WAVE per candidate, persistent: the grid is the resident workgroups (a grid sized by the
 // candidate capacity dispatched ~37k mostly-empty workgroups at parrington, 410k at 1080p),
 // each XCD takes a contiguous eighth of the candidates and its waves pull them from the XCD's
@@ -585,12 +620,18 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    FrameIndex fi;
+    fi.init(cand_cnt, kCntStride, n_frames, cand_cap);
+    int claim = 0;
+    if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
-        int gk = 0;
-        if (lane == 0) gk = atomicAdd(wq, 1);
-        gk = lo_k + __shfl(gk, 0);
+        if (!kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
+        const int gk = lo_k + __shfl(claim, 0);
+        if (gk >= hi_k) break;
+        if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
         int f = 0, ci = 0;
-        if (gk >= hi_k || !locate_strided(cand_cnt, n_frames, cand_cap, gk, f, ci)) break;
+        if (fi.regs) fi.locate(gk, f, ci);
+        else if (!locate_strided(cand_cnt, n_frames, cand_cap, gk, f, ci)) break;
         f = __builtin_amdgcn_readfirstlane(f);
         ci = __builtin_amdgcn_readfirstlane(ci);
         for (int i = lane; i < kOriCopies * PANO_ORI_BINS; i += 64) (&hist[wv][0][0])[i] = 0ull;
@@ -1105,11 +1146,17 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     unsigned long long abl_sink = 0;
     (void)nx;
     int f = 0, k = 0;
+    FrameIndex fi;
+    fi.init(counts, 1, n_frames, cap);
+    int claim = 0;
+    if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
-        int gk = 0;
-        if (lane == 0) gk = atomicAdd(wq, 1);
-        gk = lo_k + __shfl(gk, 0);
-        if (gk >= hi_k || !locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
+        if (!kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
+        const int gk = lo_k + __shfl(claim, 0);
+        if (gk >= hi_k) break;
+        if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
+        if (fi.regs) fi.locate(gk, f, k);
+        else if (!locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
         for (int i = lane; i < kDescCopies * kHist; i += 64) h0[i] = 0ull;
         const pano_kp kp = kps[(size_t)f * cap + k];
         int oct = kp.octave & 255;
