@@ -564,6 +564,9 @@ row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
     if (row < n && part == 0) cst[(size_t)f * cap + row] = norms[(size_t)f * cap + row] - 256 * (int)sum;
 }
 
+#ifndef PANO_I8_QLDS
+#define PANO_I8_QLDS 1                   // query tile in LDS (0: in registers)
+#endif
 #ifndef PANO_I8_WAVES
 #define PANO_I8_WAVES 4                  // 4 waves per SIMD (two workgroups per CU): measured 2.87 -> 2.57 ms at 1080p
 #endif
@@ -574,6 +577,12 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
         int n_split) {
     __shared__ __attribute__((aligned(16))) unsigned char Bs2[2][BT * BPI];
     __shared__ __attribute__((aligned(16))) int Cs2[2][BT];
+#if PANO_I8_QLDS
+    // the query tile (B operand of every MFMA) in LDS, sign-flipped once: read per tile
+    // instead of held in 32 VGPRs (register pressure spilled the staging state to scratch
+    // inside the tile loop)
+    __shared__ __attribute__((aligned(16))) unsigned char Qs[QT * BPI];
+#endif
     struct IPart { int best, idx, second; };
     __shared__ IPart red[2][QT];
     const int p = blockIdx.z;
@@ -590,6 +599,18 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
     const uint8_t *dA = desc + (size_t)fa * cap * PANO_DESC_DIM;
     const uint8_t *dB = desc + (size_t)fb * cap * PANO_DESC_DIM;
     // query fragments (B operand): rows i0 + wi 64 + m 32 + lr, K step k = bytes 32 k + 16 lh
+#if PANO_I8_QLDS
+    for (int e = tid; e < QT * (PANO_DESC_DIM / 16); e += 512) {   // 16-byte pieces
+        const int r = e >> 3, q = e & 7, row = i0 + r;
+        uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+        if (row < NA) v = *(const uint4 *)(dA + (size_t)row * PANO_DESC_DIM + 16 * q);
+        *(uint4 *)(Qs + r * BPI + 16 * q) = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u,
+                                                       v.z ^ 0x80808080u, v.w ^ 0x80808080u);
+    }
+    auto qfrag = [&](int m, int k) {
+        return *(const i32x4 *)(Qs + (wi * 64 + m * 32 + lr) * BPI + 32 * k + 16 * lh);
+    };
+#else
     i32x4 fi[2][4];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -602,6 +623,8 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
                              (int)(v.w ^ 0x80808080u)};
         }
     }
+    auto qfrag = [&](int m, int k) { return fi[m][k]; };
+#endif
     // candidate tile staging: thread t copies row t % 128, bytes 32 (t / 128) .. + 32, with
     // the sign flip; the first quarter also its C
     const int sr = tid & (BT - 1), sp = tid / BT;
@@ -638,15 +661,17 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
         i32x16 acc[2][2];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            i32x4 fj[2];
+            i32x4 fj[2], fq[2];
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < 2; ++a) {
                 fj[a] = *(const i32x4 *)(Bs + (wj * 64 + a * 32 + lr) * BPI + 32 * k + 16 * lh);
+                fq[a] = qfrag(a, k);
+            }
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fj[a], fi[b][k],
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fj[a], fq[b],
                                                                       k == 0 ? i32x16{} : acc[a][b], 0, 0, 0);
         }
         if (jt + n_split < n_jt) {
