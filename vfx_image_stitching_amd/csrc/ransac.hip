@@ -90,7 +90,8 @@ pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
              const int32_t *__restrict__ counts, int cap, PairArg pairs,
              const int32_t *__restrict__ best, const float *__restrict__ d1,
              const float *__restrict__ d2, float desc_thresh, double ratio2,
-             double2 *__restrict__ moves, int32_t *__restrict__ midx, int32_t *__restrict__ kcount) {
+             double2 *__restrict__ moves, int32_t *__restrict__ midx, int32_t *__restrict__ kcount,
+             int32_t *__restrict__ votes) {
     __shared__ int ish[2 * RB];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int fa = pairs.a[p], fb = pairs.b[p];
@@ -122,6 +123,7 @@ pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
             }
             mv[K + pos] = make_double2(xa - xb, ya - yb);
             mi[K + pos] = i;
+            if (votes) votes[(size_t)p * cap + K + pos] = 0;      // pair_votes accumulates
         }
         K += tot;
     }
@@ -129,7 +131,13 @@ pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
 }
 
 constexpr int VB = 256;   // hypotheses per pair_votes workgroup
+constexpr int VJS = 8;    // splits of the match range per hypothesis chunk (grid.z)
 
+// Votes of hypotheses m0 .. m0 + VB - 1 against the matches of split blockIdx.z: the K x K
+// test has one dependent f64 chain per (m, j), so a workgroup per (hypothesis chunk, pair)
+// left ~1.4 waves per SIMD and exposed the chain and LDS latency (1080p: 0.63 ms per step).
+// Splitting the match range VJS ways gives VJS x the waves; four matches per iteration are
+// four independent chains.  Partial counts are integer atomics into zeroed votes: exact.
 __global__ void __launch_bounds__(VB)
 pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount, int cap,
            double thr, int32_t *__restrict__ votes) {
@@ -138,22 +146,35 @@ pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount
     const int K = kcount[p];
     const int m0 = blockIdx.x * VB;
     if (m0 >= K) return;                              // whole workgroup
+    const int jlo = (int)((long long)K * blockIdx.z / VJS), jhi = (int)((long long)K * (blockIdx.z + 1) / VJS);
+    if (jlo >= jhi) return;
     const double2 *mv = moves + (size_t)p * cap;
     const int m = m0 + tid;
     const double2 me = m < K ? mv[m] : make_double2(0.0, 0.0);
     int v = 0;
-    for (int j0 = 0; j0 < K; j0 += VB) {
+    for (int j0 = jlo; j0 < jhi; j0 += VB) {
         __syncthreads();
-        if (j0 + tid < K) tile[tid] = mv[j0 + tid];
+        if (j0 + tid < jhi) tile[tid] = mv[j0 + tid];
         __syncthreads();
-        const int nj = K - j0 < VB ? K - j0 : VB;
-        for (int j = 0; j < nj; ++j) {
+        const int nj = jhi - j0 < VB ? jhi - j0 : VB;
+        int j = 0;
+        for (; j + 4 <= nj; j += 4) {
+            int c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double ddx = tile[j + u].x - me.x;
+                const double ddy = tile[j + u].y - me.y;
+                c[u] = (ddx * ddx + ddy * ddy) < thr;
+            }
+            v += (c[0] + c[1]) + (c[2] + c[3]);
+        }
+        for (; j < nj; ++j) {
             const double ddx = tile[j].x - me.x;
             const double ddy = tile[j].y - me.y;
             v += (ddx * ddx + ddy * ddy) < thr;
         }
     }
-    if (m < K) votes[(size_t)p * cap + m] = v;
+    if (m < K && v) atomicAdd(&votes[(size_t)p * cap + m], v);
 }
 
 __global__ void __launch_bounds__(RB)
@@ -275,13 +296,13 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
             pair_compact<<<np, RB, 0, ctx->stream>>>(
                 kps, xy_i32, counts, cap, pa, best + o, d1 + o, d2 ? d2 + o : nullptr,
-                (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, moves + o, midx + o, kcount + p0);
+                (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, moves + o, midx + o, kcount + p0, votes + o);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_compact");
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
-            pair_votes<<<dim3((cap + VB - 1) / VB, np), VB, 0, ctx->stream>>>(moves + o, kcount + p0, cap,
-                                                                             thr, votes + o);
+            pair_votes<<<dim3((cap + VB - 1) / VB, np, VJS), VB, 0, ctx->stream>>>(moves + o, kcount + p0, cap,
+                                                                                  thr, votes + o);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_votes");
         {
@@ -311,7 +332,7 @@ int launch_match_compact(pano_ctx *ctx, const pano_kp *kps, const int32_t *count
         pair_compact<<<np, RB, 0, ctx->stream>>>(kps, nullptr, counts, cap, pa, best, d1, d2,
                                                 desc_thresh > 0 ? (float)desc_thresh : INFINITY,
                                                 ratio > 0 ? ratio * ratio : 0.0,
-                                                (double2 *)moves, midx, kcount);
+                                                (double2 *)moves, midx, kcount, nullptr);
     }
     PANO_LAUNCH_CHECK(ctx, "pair_compact");
     return PANO_OK;

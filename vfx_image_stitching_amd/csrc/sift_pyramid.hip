@@ -564,10 +564,10 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
     };
     // reflected columns
     const int PW = W + 2 * R;
-    for (int i = tid; i < H * PW; i += kTailThreads) {
-        const int y = i / PW, c = i - (i / PW) * PW;
-        pad[y * kPP + c] = in[y * kTP + reflect101(c - R, W)];
-    }
+    constexpr int NWV = kTailThreads / 64;
+    const int lane = tid & 63, wv = tid >> 6;           // rows by wave, columns by lane
+    for (int y = wv; y < H; y += NWV)
+        for (int c = lane; c < PW; c += 64) pad[y * kPP + c] = in[y * kTP + reflect101(c - R, W)];
     lds_barrier();
     // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
     const int nseg = (W + SG - 1) / SG;
@@ -581,10 +581,10 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
     }
     lds_barrier();
     // reflected rows of the row-pass output
-    for (int i = tid; i < 2 * R * W; i += kTailThreads) {
-        const int q = i / W, x = i - (i / W) * W;
+    for (int q = wv; q < 2 * R; q += NWV) {
         const int ry = q < R ? q - R : H + (q - R);
-        rowt[(ry + R) * kTP + x] = rowt[(reflect101(ry, H) + R) * kTP + x];
+        const int sy = reflect101(ry, H);
+        for (int x = lane; x < W; x += 64) rowt[(ry + R) * kTP + x] = rowt[(sy + R) * kTP + x];
     }
     lds_barrier();
     // column pass: item = (column x, segment of SG rows); lanes on consecutive columns
@@ -607,6 +607,7 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
 
 __global__ void __launch_bounds__(kTailThreads)
 blur_tail(TailArgs ta) {
+    __shared__ double taps_s[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // every level's taps, loaded once
     __shared__ float lv[3][kTailDim * kTP];      // current / next level, octave seed
     __shared__ float pad[kTailDim * kPP];         // level with reflected columns
     __shared__ float rowt[kRowtRows * kTP];       // row-pass output with reflected rows
@@ -614,6 +615,9 @@ blur_tail(TailArgs ta) {
     // fills every CU: raise its waves' issue priority so the chain is not starved
     __builtin_amdgcn_s_setprio(3);
     const int f = blockIdx.x, tid = threadIdx.x;
+    // taps to LDS once: each level's loop then starts on LDS reads, not on a global load
+    for (int i = tid; i < ta.n_lvl * PANO_MAX_TAPS; i += kTailThreads) taps_s[i] = ta.taps[i];
+    lds_barrier();
     int cur = 0, keep = -1;
     for (int oi = 0; oi < ta.n_oct; ++oi) {
         const int H = ta.H[oi], W = ta.W[oi];
@@ -644,7 +648,7 @@ blur_tail(TailArgs ta) {
             while (out == cur || out == keep) ++out;
             float *g = (ta.full || l < ta.n_lvl - 1) ? ta.G[oi][l] + (size_t)f * H * W : nullptr;
             float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
-            const double *tg = ta.taps + l * PANO_MAX_TAPS;
+            const double *tg = taps_s + l * PANO_MAX_TAPS;
             switch (n) {   // the reference's kernel sizes; others take the runtime-count path
                 case 11: tail_level<11>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
                 case 13: tail_level<13>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
