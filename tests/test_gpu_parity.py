@@ -9,6 +9,8 @@ Bars (DESIGN.md "Parity"):
 from __future__ import annotations
 
 import ctypes
+import os
+import sys
 
 import numpy as np
 import pytest
@@ -678,3 +680,17 @@ def test_synthetic_1080p_vs_oracle_golden(gpu, gold_json, gold_npz):
         assert abs(int(r[p]["n_matches"]) - want["n_matches"]) <= max(2, want["n_matches"] // 1000)
         assert abs(r[p]["dx"] - want["move"][0]) <= 1e-3 and abs(r[p]["dy"] - want["move"][1]) <= 1e-3, \
             (p, r[p], want)
+
+
+@pytest.mark.parametrize("tt", ["32", "64"])
+def test_fused_pair_blur_bit_exact(gpu, tt):
+    """The fused two-level blur (blur_pair: levels (1, 2) and (4, 5) of the small octaves in one
+    launch, the first level computed on the second's halo region with BORDER_REFLECT_101
+    restored at the image edges) gives every Gaussian and DoG level bit-identical to the
+    oracle.  It is off by default (measured no faster), so it runs in a child process with
+    PANO_BLUR_PAIR=3 (the switch is read once per process)."""
+    import subprocess
+    env = dict(os.environ, PANO_BLUR_PAIR="3", PANO_BLUR_PAIR_TT=tt)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "pair_blur_check.py")],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

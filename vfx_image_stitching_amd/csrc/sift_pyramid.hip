@@ -470,6 +470,130 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     }
 }
 
+// ------------------------------------------------------------------ fused level pairs
+// Two cascaded levels in ONE launch for the latency-bound octaves (a few hundred to a few
+// thousand workgroups per level, ~5-20 us of launch and wave-quantisation latency each):
+// a TT x TT output tile stages G[l-1] with the halo of both levels (R1 + R2), computes G[l]
+// on the tile plus the next level's halo (R2), replaces the part of that region outside the
+// image by its BORDER_REFLECT_101 image (what the next level reads there, exactly), writes
+// G[l] / DoG[l-1] of the tile, then computes G[l+1] on the tile from the region in LDS and
+// writes G[l+1] / DoG[l].  Every output is blur_fast's arithmetic (sequential fma in tap
+// order, one f32 rounding per pass), hence bit-identical; the price is level l's FMAs on the
+// (TT + 2 R2)^2 region, the saving one launch and one HBM round trip of G[l] per pair.
+constexpr int kPairSeg = 8;     // outputs per thread item in every pass
+
+template <int NT1, int NT2, int TT>
+struct PairShape {
+    static constexpr int R1 = (NT1 - 1) / 2, R2 = (NT2 - 1) / 2, RS = R1 + R2;
+    static constexpr int IH = TT + 2 * RS, IWP = (TT + 2 * RS) | 1;     // staged G[l-1]
+    static constexpr int RP = (TT + 2 * R2 + kPairSeg) | 1;            // row-pass pitch
+    static constexpr int SP = TT + 1;                                 // side tile pitch
+    static constexpr int floats = IH * IWP + kPairSeg + (IH + kPairSeg) * RP + TT * SP;
+};
+
+template <int MODE, int NT1, int NT2, int TT, int NTHR>
+__global__ void __launch_bounds__(NTHR)
+blur_pair(LoadArgs la, float *__restrict__ out1, float *__restrict__ dog1, float *__restrict__ in_copy,
+          float *__restrict__ out2, float *__restrict__ dog2, int H, int W, Taps t1, Taps t2) {
+    using S = PairShape<NT1, NT2, TT>;
+    constexpr int R2 = S::R2, RS = S::RS, IWP = S::IWP, RP = S::RP, SP = S::SP;
+    constexpr int SG = kPairSeg, NW = NTHR / 64;
+    extern __shared__ __attribute__((aligned(16))) float smp[];
+    float *tin = smp;                                   // [IH][IWP] G[l-1], then the G[l] region
+    float *rb = smp + S::IH * IWP + SG;                 // [IH + SG][RP] row-pass outputs
+    float *side = rb + (S::IH + SG) * RP;               // [TT][SP] G[l-1], then G[l], of the tile
+    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
+    const int x0 = (int)(tb % gridDim.x) * TT, y0 = (int)((tb / gridDim.x) % gridDim.y) * TT;
+    const int f = (int)(tb / (gridDim.x * gridDim.y));
+    const int tw = min(TT, W - x0), th = min(TT, H - y0);
+    const int tid = threadIdx.x;
+    const int ih = th + 2 * RS, iw = tw + 2 * RS;
+    stage_tile<MODE, NW, (S::IH + NW - 1) / NW>(la, f, H, W, x0, y0, RS, ih, iw, IWP, tin);
+    __syncthreads();
+    for (int i = tid; i < th * tw; i += NTHR) {
+        const int y = i / tw, x = i - y * tw;
+        side[y * SP + x] = tin[(y + RS) * IWP + x + RS];
+    }
+    // ---- level l, row pass: every staged row, region columns c = 0 .. ow1 - 1
+    const int ow1 = tw + 2 * R2, oh1 = th + 2 * R2;
+    {
+        const int nseg = (ow1 + SG - 1) / SG;
+        for (int it = tid; it < ih * nseg; it += NTHR) {
+            const int row = it % ih, sg = it / ih;
+            double acc[SG];
+            conv_seg<NT1, SG>(tin + row * IWP + sg * SG, 1, t1.k, acc);
+#pragma unroll
+            for (int j = 0; j < SG; ++j) rb[row * RP + sg * SG + j] = (float)acc[j];
+        }
+    }
+    __syncthreads();
+    // ---- level l, column pass: region rows r = 0 .. oh1 - 1, into tin (pitch IWP)
+    {
+        const int nrs = (oh1 + SG - 1) / SG;
+        for (int it = tid; it < ow1 * nrs; it += NTHR) {
+            const int c = it % ow1, rs = it / ow1;
+            double acc[SG];
+            conv_seg<NT1, SG>(rb + rs * SG * RP + c, RP, t1.k, acc);
+#pragma unroll
+            for (int j = 0; j < SG; ++j)
+                if (rs * SG + j < oh1) tin[(rs * SG + j) * IWP + c] = (float)acc[j];
+        }
+    }
+    __syncthreads();
+    // ---- region positions outside the image take their reflected image value (reads only
+    // inside-image positions, writes only outside ones: one pass)
+    const int ry0 = y0 - R2, rx0 = x0 - R2;
+    if (ry0 < 0 || rx0 < 0 || y0 + th + R2 > H || x0 + tw + R2 > W) {
+        for (int i = tid; i < oh1 * ow1; i += NTHR) {
+            const int r = i / ow1, c = i - r * ow1;
+            const int y = ry0 + r, x = rx0 + c;
+            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) continue;
+            tin[r * IWP + c] = tin[(reflect101(y, H) - ry0) * IWP + reflect101(x, W) - rx0];
+        }
+        __syncthreads();
+    }
+    // ---- level l out: G[l], DoG[l-1] (and level 0 of the octave for MODE_DOWN)
+    for (int i = tid; i < th * tw; i += NTHR) {
+        const int y = i / tw, x = i - y * tw;
+        const float g = tin[(y + R2) * IWP + x + R2], c = side[y * SP + x];
+        const size_t gi = ((size_t)f * H + y0 + y) * W + x0 + x;
+        if (out1) out1[gi] = g;
+        dog1[gi] = g - c;
+        if (MODE == MODE_DOWN && in_copy) in_copy[gi] = c;
+        side[y * SP + x] = g;
+    }
+    // ---- level l + 1, row pass: region rows, tile columns
+    {
+        const int nseg = (tw + SG - 1) / SG;
+        for (int it = tid; it < oh1 * nseg; it += NTHR) {
+            const int row = it % oh1, sg = it / oh1;
+            double acc[SG];
+            conv_seg<NT2, SG>(tin + row * IWP + sg * SG, 1, t2.k, acc);
+#pragma unroll
+            for (int j = 0; j < SG; ++j) rb[row * RP + sg * SG + j] = (float)acc[j];
+        }
+    }
+    __syncthreads();
+    // ---- level l + 1, column pass and out: G[l+1], DoG[l]
+    {
+        const int nrs = (th + SG - 1) / SG;
+        for (int it = tid; it < tw * nrs; it += NTHR) {
+            const int x = it % tw, rs = it / tw;
+            double acc[SG];
+            conv_seg<NT2, SG>(rb + rs * SG * RP + x, RP, t2.k, acc);
+#pragma unroll
+            for (int j = 0; j < SG; ++j) {
+                const int y = rs * SG + j;
+                if (y >= th) break;
+                const float g = (float)acc[j];
+                const size_t gi = ((size_t)f * H + y0 + y) * W + x0 + x;
+                if (out2) out2[gi] = g;
+                dog2[gi] = g - side[y * SP + x];
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ small-octave tail
 // Octaves whose levels fit one 64 x 64 tile are latency-bound as separate launches (one
 // tiny workgroup per frame, ~7 us each, 5 per octave).  blur_tail runs them all in ONE
@@ -762,6 +886,56 @@ int launch_blur(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, float
     }
 }
 
+// Fused pair (levels l, l + 1) of one octave; PANO_E_UNSUPPORTED for tap pairs without an
+// instantiation (the caller then launches the levels one by one).
+template <int MODE, int NT1, int NT2, int TT, int NTHR>
+int launch_pair_tt(pano_ctx *ctx, const LoadArgs &la, float *out1, float *dog1, float *in_copy, float *out2,
+                   float *dog2, int n, int H, int W, const Taps &t1, const Taps &t2) {
+    const size_t sm = (size_t)PairShape<NT1, NT2, TT>::floats * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_pair<MODE, NT1, NT2, TT, NTHR>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        attr = true;
+    }
+    dim3 grid((W + TT - 1) / TT, (H + TT - 1) / TT, n);
+    {
+        PanoProf prof_(ctx, PK_BLUR);
+        blur_pair<MODE, NT1, NT2, TT, NTHR><<<grid, NTHR, sm, ctx->stream>>>(la, out1, dog1, in_copy, out2, dog2,
+                                                                           H, W, t1, t2);
+    }
+    PANO_LAUNCH_CHECK(ctx, "blur_pair");
+    return PANO_OK;
+}
+
+// 32 x 32 tiles of 256 threads (default), or 64 x 64 of 512 (PANO_BLUR_PAIR_TT=64: less
+// halo recompute, fewer workgroups)
+template <int MODE, int NT1, int NT2>
+int launch_pair_nt(pano_ctx *ctx, const LoadArgs &la, float *out1, float *dog1, float *in_copy, float *out2,
+                   float *dog2, int n, int H, int W, const Taps &t1, const Taps &t2) {
+    static const int tt = [] {
+        const char *e = getenv("PANO_BLUR_PAIR_TT");
+        return e && atoi(e) == 64 ? 64 : 32;
+    }();
+    if (tt == 64 && H >= 64 && W >= 64)
+        return launch_pair_tt<MODE, NT1, NT2, 64, 512>(ctx, la, out1, dog1, in_copy, out2, dog2, n, H, W, t1, t2);
+    return launch_pair_tt<MODE, NT1, NT2, 32, 256>(ctx, la, out1, dog1, in_copy, out2, dog2, n, H, W, t1, t2);
+}
+
+template <int MODE>
+int launch_pair(pano_ctx *ctx, const LoadArgs &la, float *out1, float *dog1, float *in_copy, float *out2,
+                float *dog2, int n, int H, int W, const Taps &t1, const Taps &t2) {
+    if (t1.n == 11 && t2.n == 13)
+        return launch_pair_nt<MODE, 11, 13>(ctx, la, out1, dog1, in_copy, out2, dog2, n, H, W, t1, t2);
+    if constexpr (MODE == MODE_LEVEL) {
+        if (t1.n == 21 && t2.n == 27)
+            return launch_pair_nt<MODE, 21, 27>(ctx, la, out1, dog1, in_copy, out2, dog2, n, H, W, t1, t2);
+        if (t1.n == 17 && t2.n == 21)
+            return launch_pair_nt<MODE, 17, 21>(ctx, la, out1, dog1, in_copy, out2, dog2, n, H, W, t1, t2);
+    }
+    return PANO_E_UNSUPPORTED;
+}
+
 }  // namespace
 
 // Scalars of S1/S2 exactly as the reference computes them (Python/numpy doubles; glibc
@@ -942,13 +1116,56 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
         ctx->o_tail = o_side;
         return PANO_OK;
     };
+    // fused level pairs (blur_pair, PANO_BLUR_PAIR) on the latency-bound octaves: (1, 2) and
+    // (4, 5) of every octave o >= 1 whose plane has fewer than PANO_BLUR_PAIR_TILES 64 x 64
+    // tiles per batch; level 3 alone keeps the next octave's (and the tail's) start after it
+    static const long pair_tiles = [] {
+        const char *e = getenv("PANO_BLUR_PAIR_TILES");
+        return e ? atol(e) : 4000L;
+    }();
+    static const int pair_mask = [] {
+        // bit 0: levels (1, 2); bit 1: (4, 5).  Measured on MI355X: (1, 2) within
+        // noise of the level-by-level launches at parrington and 1080p, (4, 5) slower (level
+        // 4's 21 taps over the 27-tap halo region: 3.3x its FMAs), so off by default
+        const char *e = getenv("PANO_BLUR_PAIR");
+        return e ? atoi(e) : 0;
+    }();
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
         ctx->stream = o >= o_side ? ctx->side : main_stream;     // side-stream octaves
+        const bool pairs_here = o >= 1 && nl == 6 && H >= 32 && W >= 32 &&
+                                (long)((W + 63) / 64) * ((H + 63) / 64) * n < pair_tiles;
         for (int l = 1; l < nl; ++l) {
             float *out = G + ctx->gauss_off[o][l];
             float *dg = D + ctx->dog_off[o][l - 1];
             LoadArgs la{};
+            const bool pair = pairs_here && ((l == 1 && (pair_mask & 1)) || (l == 4 && (pair_mask & 2)));
+            if (pair) {
+                float *out2 = G + ctx->gauss_off[o][l + 1];
+                float *dg2 = D + ctx->dog_off[o][l];
+                const bool keep1 = full || l + 1 < nl - 1 || l < nl - 2;   // G[l] read downstream
+                const bool keep2 = full || l + 1 < nl - 1;
+                if (l == 1) {
+                    la.src = G + ctx->gauss_off[o - 1][nl - 3];
+                    la.sh = ctx->oct_h[o - 1];
+                    la.sw = ctx->oct_w[o - 1];
+                    la.ifx = 1.0 / ((double)W / la.sw);
+                    la.ify = 1.0 / ((double)H / la.sh);
+                    rc = launch_pair<MODE_DOWN>(ctx, la, keep1 ? out : nullptr, dg,
+                                                full ? G + ctx->gauss_off[o][0] : nullptr, keep2 ? out2 : nullptr,
+                                                dg2, n, H, W, tl[l], tl[l + 1]);
+                } else {
+                    la.src = G + ctx->gauss_off[o][l - 1];
+                    rc = launch_pair<MODE_LEVEL>(ctx, la, (full || l < nl - 2) ? out : nullptr, dg, nullptr,
+                                                 keep2 ? out2 : nullptr, dg2, n, H, W, tl[l], tl[l + 1]);
+                }
+                if (rc == PANO_OK) {
+                    ++l;                                   // level l + 1 done too
+                    continue;
+                }
+                if (rc != PANO_E_UNSUPPORTED) { ctx->stream = main_stream; return rc; }
+                la = LoadArgs{};                           // no fused form: level by level
+            }
             if (l == 1 && o > 0) {
                 // next-octave base = INTER_NEAREST (w//2, h//2) of level nl-3 of octave o-1,
                 // materialised as G[o][0] by the same launch
