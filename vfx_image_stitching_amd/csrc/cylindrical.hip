@@ -71,11 +71,18 @@ cyl_gather(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
 // exact: every candidate of a conservative box around f tan((k +- 1/2)/f) is tested with
 // the forward map.  Also zeroes the column's non-zero flag (cyl_inverse raises it).
 __global__ void __launch_bounds__(256)
-cyl_columns(int w, FocalArg focal, int2 *__restrict__ cols, uint8_t *__restrict__ colnz) {
+cyl_columns(int w, FocalArg focal, int2 *__restrict__ cols, uint8_t *__restrict__ colnz,
+            double2 *__restrict__ colden) {
     const int xp = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
     if (xp >= w) return;
     const double fl = focal.f[f];
     const int cx = w / 2, k = xp - cx;
+    {
+        // per SOURCE column x = xp: sqrt(xd^2 + f^2) and its ratio to f, the row map's
+        // column constants (cyl_inverse reads them instead of recomputing per pixel)
+        const double den = sqrt((double)k * (double)k + fl * fl);
+        colden[(size_t)f * w + xp] = make_double2(den, den / fl);
+    }
     // inverse images of k -+ 1/2 (arguments kept inside the atan range; clamped to the frame)
     const double lim = 1.5707963267948966 - 1e-12;
     const double ta = fmax(fmin((k - 0.5) / fl, lim), -lim), tb = fmax(fmin((k + 0.5) / fl, lim), -lim);
@@ -99,19 +106,18 @@ cyl_columns(int w, FocalArg focal, int2 *__restrict__ cols, uint8_t *__restrict_
 
 __global__ void __launch_bounds__(256)
 cyl_inverse(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 *__restrict__ cols,
-            uint8_t *__restrict__ colnz, int h, int w, FocalArg focal) {
+            const double2 *__restrict__ colden, uint8_t *__restrict__ colnz, int h, int w, FocalArg focal) {
     const int xp = blockIdx.x * 64 + (threadIdx.x & 63);
     const int yp = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int f = blockIdx.z;
     if (xp >= w || yp >= h) return;
     const double fl = focal.f[f];
-    const int cx = w / 2, cy = h / 2, k = yp - cy;
+    const int cy = h / 2, k = yp - cy;
     const int2 cr = cols[(size_t)f * w + xp];
     long best = -1;                                   // largest row-major source index
     for (int x = cr.x; x <= cr.y; ++x) {
-        const int xd = x - cx;
-        const double den = sqrt((double)xd * (double)xd + fl * fl);
-        const double s = den / fl;
+        const double2 ds = colden[(size_t)f * w + x];     // the same two roundings, once per column
+        const double den = ds.x, s = ds.y;
         // rows whose forward y' can be k: a box around [(k - 1/2) s, (k + 1/2) s], scanned
         // from the top (the first hit is this column's largest row)
         const int r1 = (int)ceil((k + 0.5) * s) + 1, r0 = (int)floor((k - 0.5) * s) - 1;
@@ -149,9 +155,10 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
     const size_t plane = (size_t)h * w;
     static const bool scatter_form = getenv("PANO_CYL_SCATTER") != nullptr;
     if (!scatter_form) {
-        int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, (size_t)n * w * sizeof(int2));
+        int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, (size_t)n * w * (sizeof(int2) + sizeof(double2)));
         if (rc) return rc;
-        int2 *cols = (int2 *)ctx->bscratch;
+        double2 *colden = (double2 *)ctx->bscratch;                      // 16-byte aligned first
+        int2 *cols = (int2 *)(colden + (size_t)n * w);
         for (int f0 = 0; f0 < n; f0 += kFocalChunk) {
             const int nf = n - f0 < kFocalChunk ? n - f0 : kFocalChunk;
             FocalArg fa;
@@ -159,13 +166,13 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
             {
                 PanoProf prof_(ctx, PK_CYL_SCATTER);
                 cyl_columns<<<dim3((w + 255) / 256, nf), 256, 0, ctx->stream>>>(
-                    w, fa, cols + (size_t)f0 * w, colnz ? colnz + (size_t)f0 * w : nullptr);
+                    w, fa, cols + (size_t)f0 * w, colnz ? colnz + (size_t)f0 * w : nullptr, colden + (size_t)f0 * w);
             }
             PANO_LAUNCH_CHECK(ctx, "cyl_columns");
             {
                 PanoProf prof_(ctx, PK_CYL_GATHER);
                 cyl_inverse<<<dim3((w + 63) / 64, (h + 3) / 4, nf), 256, 0, ctx->stream>>>(
-                    src + f0 * plane * 3, dst + f0 * plane * 3, cols + (size_t)f0 * w,
+                    src + f0 * plane * 3, dst + f0 * plane * 3, cols + (size_t)f0 * w, colden + (size_t)f0 * w,
                     colnz ? colnz + (size_t)f0 * w : nullptr, h, w, fa);
             }
             PANO_LAUNCH_CHECK(ctx, "cyl_inverse");
