@@ -694,3 +694,29 @@ def test_fused_pair_blur_bit_exact(gpu, tt):
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "pair_blur_check.py")],
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_frame_above_2047_px_vs_oracle_golden(gpu, gold_json, gold_npz):
+    """A 2304 x 2176 frame (both sides above the old 12-bit scan-key limit; base image 4608 x
+    4352) against the oracle's golden (tests/golden/make_golden_large.py): cylindrical digest,
+    every keypoint (the _compare_features bars) and every 8th descriptor row."""
+    from vfx_image_stitching_amd import _lib, data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    meta = gold_json("sift_large_frame.json")
+    z = gold_npz("sift_large_frame.npz")
+    H, W = meta["shape"]
+    frames, focals, _ = data.synthetic_sequence(n_frames=144, h=H, w=W, start=0, count=1)
+    st = Stitcher("sift", cap=1 << 17)
+    cyl, _ = st.cylindrical(st.upload(frames), focals)
+    assert digest(cyl.cpu().numpy()[0]) == meta["cyl_digest"]
+    kps, desc, counts = st.features(cyl)
+    n = int(counts.cpu().numpy()[0])
+    assert n == meta["count"], (n, meta["count"])
+    rec = kps[0, :n].cpu().numpy().view(_lib.KP_NP).reshape(-1)
+    d = desc[0, :n].cpu().numpy()
+    g = {k: z[k] for k in ("x", "y", "size", "angle", "response", "octave")}
+    for k in ("x", "y", "response", "octave"):
+        np.testing.assert_array_equal(rec[k], g[k].astype(rec[k].dtype), err_msg=k)
+    np.testing.assert_allclose(rec["size"], g["size"], rtol=3e-7, atol=0)
+    sel = np.arange(0, n, meta["sub"])
+    _compare_features(rec[sel], d[sel], {k: v[sel] for k, v in g.items()}, z["desc_sub"])

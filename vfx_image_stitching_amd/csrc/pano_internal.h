@@ -40,7 +40,8 @@ struct Cand {
     int32_t octave_field;
     int16_t octave, layer;        // octave index and localised layer
     int32_t frame;
-    uint32_t order;               // scan order key (octave*8 + layer0) << 24 | y << 12 | x
+    int32_t pad;
+    uint64_t order;               // scan order key (octave*8 + layer0) << 32 | y << 16 | x
 };
 
 // Device-side view of one pyramid level of a frame batch.

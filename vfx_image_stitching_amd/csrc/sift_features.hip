@@ -175,13 +175,15 @@ struct DogArgs {
     int n_oct;
 };
 
-__device__ __forceinline__ uint32_t scan_key(int o, int layer0, int y, int x) {
-    return ((uint32_t)(o * 8 + layer0) << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+// The reference's scan order (octave, layer, row, column) as one integer: 16 bits per
+// coordinate, so frames up to 4096 px per side (base 8192, the sort's bucket limit).
+__device__ __forceinline__ uint64_t scan_key(int o, int layer0, int y, int x) {
+    return ((uint64_t)(o * 8 + layer0) << 32) | ((uint64_t)y << 16) | (uint64_t)x;
 }
 
 template <int NL>
 __global__ void __launch_bounds__(256)
-extrema_scan(DogArgs a, int border, double thresh, uint32_t *__restrict__ raw,
+extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
              int32_t *__restrict__ raw_cnt, int raw_cap, int tile_base) {
     constexpr int ni = NL - 2;
     __shared__ float s[NL][ETY + 2][ELW];
@@ -316,11 +318,11 @@ __device__ __forceinline__ float min3f(float a, float b, float c) { return fminf
 
 template <int NL, int SR>
 __global__ void __launch_bounds__(256)
-extrema_stream(XArgs a, int border, double thresh, uint32_t *__restrict__ raw,
+extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
                int32_t *__restrict__ raw_cnt, int raw_cap, int item_base, int item_end) {
     constexpr int ni = NL - 2;
     constexpr int BUF = 64;
-    __shared__ uint32_t kbuf[4][BUF];
+    __shared__ uint64_t kbuf[4][BUF];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int f = blockIdx.y;
@@ -422,9 +424,9 @@ __device__ __forceinline__ float dog_at(const DogArgs &a, int o, int lvl, int f,
 }
 
 // One extremum through the quadratic fit and the contrast / edge tests.
-__device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint32_t key, int f, Cand &k) {
-    const int o = (int)(key >> 24) / 8, layer0 = (int)(key >> 24) % 8;
-    const int y = (int)((key >> 12) & 4095), x = (int)(key & 4095);
+__device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key, int f, Cand &k) {
+    const int o = (int)(key >> 32) / 8, layer0 = (int)(key >> 32) % 8;
+    const int y = (int)((key >> 16) & 65535), x = (int)(key & 65535);
     const int ni = lp.ni, border = lp.border;
     const int H = a.H[o], W = a.W[o];
     // ---- quadratic fit (sift_impl.py:169-211), keeping the max_iter quirk
@@ -489,7 +491,7 @@ __device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint32_t key
 }
 
 __global__ void __launch_bounds__(256)
-localize(DogArgs a, LocParams lp, const uint32_t *__restrict__ raw,
+localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
          const int32_t *__restrict__ raw_cnt, int raw_cap, Cand *__restrict__ cands,
          int32_t *__restrict__ cand_cnt, int cand_cap) {
     const int f = blockIdx.y;
@@ -793,7 +795,7 @@ __device__ __forceinline__ unsigned long long xy_key(const RawKp &r) {
 // bucket member lists -- the three passes of the counting sort with block barriers between
 // them instead of kernel boundaries.
 constexpr int kSortThreads = 1024;
-constexpr int kSortMaxBuckets = 4096 + 1;     // base width + 1 (frames <= 2047 px, scan key)
+constexpr int kSortMaxBuckets = 8192 + 1;     // base width + 1 (frames <= 4096 px)
 
 __global__ void __launch_bounds__(kSortThreads)
 bucket_build(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
@@ -1441,9 +1443,9 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     if (rc) return rc;
     rc = pano_grow(ctx, (void **)&ctx->raw, &ctx->raw_cap, raw_cap * n * sizeof(RawKp));
     if (rc) return rc;
-    rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint32_t));
+    rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint64_t));
     if (rc) return rc;
-    uint32_t *raw_ext = (uint32_t *)ctx->frame_off;
+    uint64_t *raw_ext = (uint64_t *)ctx->frame_off;
     // [err] [cand f] [raw f] [ext f] [descriptor, orientation work queues per XCD x 8 each],
     // one line apiece
     const size_t cnt_ints = (3 * (size_t)n + 1 + 16) * kCntStride;
@@ -1481,8 +1483,8 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         if (iw > 0 && ih > 0) tiles += da.tiles_x[o] * ((ih + ETY - 1) / ETY);
     }
     da.tile_start[no] = tiles;
-    if (ctx->h * 2 > 4095 || ctx->w * 2 > 4095)
-        return pano_fail(ctx, PANO_E_UNSUPPORTED, "frames above 2047 px need a wider scan key");
+    if (ctx->h > 4096 || ctx->w > 4096)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "frames above 4096 px per side (the keypoint sort's buckets)");
     // Extrema: the streaming kernel for the large octaves (a wave walks 32 rows of a strip),
     // the LDS-tiled scan for the small ones (few rows: more, shorter workgroups win); the
     // octaves of a pending blur tail are scanned after the join.
