@@ -1122,7 +1122,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int32_t *__restrict__ counts, int n_frames, int cap, int32_t *__restrict__ work,
                 float *__restrict__ desc, uint8_t *__restrict__ desc_u8, int32_t *__restrict__ norms) {
     __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHist];
-    __shared__ int col_lo[kDescWaves][kDescCols], col_pre[kDescWaves][kDescCols + 1];
+    __shared__ int col_lo[kDescWaves][kDescCols / kDescSS], col_pre[kDescWaves][kDescCols / kDescSS + 1];   // per super-strip
     __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     unsigned long long *h0 = hist[wv];
