@@ -706,27 +706,30 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             hd[wv][lane] = (double)(long long)t * kHistInv;
         }
         wave_sync();
-        if (lane < PANO_ORI_BINS) {
-            const int b = lane, nb = PANO_ORI_BINS;
+        const int nb = PANO_ORI_BINS;
+        double svl = -1.0;                 // this lane's smoothed bin (histogram values are >= 0)
+        if (lane < nb) {
+            const int b = lane;
             const double *h = hd[wv];
-            sm[wv][b] = ((6 * h[b] + 4 * (h[(b + nb - 1) % nb] + h[(b + 1) % nb])) +
-                         h[(b + nb - 2) % nb]) + h[(b + 2) % nb];
-            sm[wv][b] = sm[wv][b] / 16.0;
+            svl = ((6 * h[b] + 4 * (h[(b + nb - 1) % nb] + h[(b + 1) % nb])) + h[(b + nb - 2) % nb]) +
+                  h[(b + 2) % nb];
+            svl = svl / 16.0;
+            sm[wv][b] = svl;
         }
+        double mx = svl;                   // the maximum: exact in any order
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) mx = fmax(mx, __shfl_xor(mx, d));
         wave_sync();
         // peaks -> keypoints; one (wave-aggregated) append per candidate
-        const int nb = PANO_ORI_BINS;
         const int p = lane;
         bool emit = false;
         double angle = 0.0;
         if (lane < nb) {
             const double *sv = sm[wv];
-            double mx = sv[0];
-            for (int b = 1; b < nb; ++b) mx = fmax(mx, sv[b]);
             const double l = sv[(p + nb - 1) % nb], r = sv[(p + 1) % nb];
-            if (sv[p] > l && sv[p] > r && sv[p] >= op.peak_ratio * mx) {
+            if (svl > l && svl > r && svl >= op.peak_ratio * mx) {
                 const double interp =
-                    np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * sv[p]) + r), (double)nb);
+                    np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * svl) + r), (double)nb);
                 angle = 360.0 - interp * 360.0 / nb;
                 if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
                 emit = true;
