@@ -520,6 +520,7 @@ localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
 #define PANO_ORI_COPIES 1      // histogram copies per wave (measured: 4 and 8 no faster)
 #endif
 constexpr int kOriCopies = PANO_ORI_COPIES;
+constexpr float kInv360 = 1.0f / 360.0f;   // RN(1 / 360)
 constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
 
 struct OriParams {
@@ -693,7 +694,12 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
 #else
                 const float w = expf(wfac * (float)(dx * dx + dy * dy));
 #endif
-                const int bin = ((int)rintf((ang * 36.0f) / 360.0f)) % PANO_ORI_BINS;
+                // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same
+                // bin as the IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
+                const float a36 = ang * 36.0f;
+                const float q0 = a36 * kInv360;
+                int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
+                bin = bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
                 const double val = (double)(w * mag);
                 atomicAdd(&hist[wv][lane % kOriCopies][bin], rint_fix(val * kHistScale));
             }
