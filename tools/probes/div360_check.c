@@ -1,7 +1,8 @@
 /* Exhaustive check (every f32 a in [0, 12960]) that the reciprocal-and-correction division
    used for the orientation bin, q = a*y; r = fma(-q, 360, a); q + r*y with y = RN(1/360),
    gives the same bin rint(a / 360) as the IEEE division (mismatches only for subnormal
-   quotients, all bin 0).  gcc -O2 -ffp-contract=off div360_check.c -lm; ~40 s. */
+   quotients, all bin 0).  gcc -O2 -ffp-contract=off div360_check.c -lm; ~40 s.
+   With 360 -> 255 and the range [0, 256] (localize's DoG / 255): 0 mismatches. */
 #include <stdio.h>
 #include <math.h>
 #include <string.h>

@@ -424,6 +424,15 @@ __device__ __forceinline__ float dog_at(const DogArgs &a, int o, int lvl, int f,
 }
 
 // One extremum through the quadratic fit and the contrast / edge tests.
+// v / 255 by the reciprocal and one exact-residual correction: equal to the IEEE quotient for
+// every f32 |v| <= 256, subnormals included (exhaustive: tools/probes/div360_check.c with
+// the divisor 255); DoG values are within +-255
+__device__ __forceinline__ float div255(float v) {
+    constexpr float y = 1.0f / 255.0f;
+    const float q = v * y;
+    return fmaf(fmaf(-q, 255.0f, v), y, q);
+}
+
 __device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key, int f, Cand &k) {
     const int o = (int)(key >> 32) / 8, layer0 = (int)(key >> 32) % 8;
     const int y = (int)((key >> 16) & 65535), x = (int)(key & 65535);
@@ -437,7 +446,7 @@ __device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key
         for (int dz = 0; dz < 3; ++dz)
             for (int dy = 0; dy < 3; ++dy)
                 for (int dx = 0; dx < 3; ++dx)
-                    c[dz][dy][dx] = dog_at(a, o, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx) / 255.0f;
+                    c[dz][dy][dx] = div255(dog_at(a, o, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx));
         const float cv = c[1][1][1];
         g[0] = 0.5f * (c[1][1][2] - c[1][1][0]);
         g[1] = 0.5f * (c[1][2][1] - c[1][0][1]);
