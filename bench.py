@@ -110,6 +110,10 @@ def parse():
     ap.add_argument("--cap", type=int, default=0, help="keypoint capacity per frame (0 = auto)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch eagerly instead of replaying captured hipGraphs")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: a fixed sequence per rank (default); strong: ONE fixed sequence "
+                         "(the set's 18 frames, or the synthetic 144-frame / 143-pair batch) "
+                         "whose pairs are sharded over the ranks")
     return ap.parse_args()
 
 
@@ -123,18 +127,43 @@ def synthetic_shards(world):
     return D.shard_ranges(min(143, SYNTH_PAIRS_PER_RANK * world), world)
 
 
-def workload(name, rank, world):
+SYNTH_FRAMES = 144             # config 5: the 144-frame synthetic batch, 143 stitched pairs
+
+
+def strong_shards(name, world):
+    """Strong scaling: the pairs of ONE fixed sequence over the ranks (contiguous, balanced;
+    grail / parrington 17 pairs over 8 ranks = 3,2,...,2; synthetic 143 over 8 = 18 x 7 + 17)."""
+    from vfx_image_stitching_amd import distributed as D
+    n_pairs = SYNTH_FRAMES - 1 if name == "synthetic" else 17
+    return D.shard_ranges(n_pairs, world)
+
+
+def workload(name, rank, world, scaling="weak"):
+    """-> (this rank's frames, focals, crop margin, (h, w), distinct frames of the job,
+    per-rank pair counts).  Rank r holds the frames of its pairs plus the boundary frame."""
     from vfx_image_stitching_amd import data
+    if scaling == "strong":
+        shards = strong_shards(name, world)
+        s, c = shards[rank]
+        counts = [cc for _, cc in shards]
+        if name == "synthetic":
+            frames, focals, _ = data.synthetic_sequence(n_frames=SYNTH_FRAMES, h=1080, w=1920,
+                                                        start=s, count=c + 1)
+            return frames, focals, 15, (1080, 1920), SYNTH_FRAMES, counts
+        names, frames, focals, margin = data.load_set(name)
+        return frames[s:s + c + 1], focals[s:s + c + 1], margin, frames.shape[1:3], len(frames), counts
     if name == "synthetic":
         shards = synthetic_shards(world)
         s, c = shards[rank]
         # each rank generates only its own frames (the generator is window-independent)
-        frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920, start=s, count=c + 1)
-        return frames, focals, 15, (1080, 1920), sum(cc for _, cc in shards) + 1
+        frames, focals, _ = data.synthetic_sequence(n_frames=SYNTH_FRAMES, h=1080, w=1920, start=s,
+                                                    count=c + 1)
+        counts = [cc for _, cc in shards]
+        return frames, focals, 15, (1080, 1920), sum(counts) + 1, counts
     names, frames, focals, margin = data.load_set(name)
     n = len(frames)
     fr, fo = data.cyclic_sequence(frames, focals, start=(n - 1) * rank, count=n)
-    return fr, fo, margin, frames.shape[1:3], world * (n - 1) + 1
+    return fr, fo, margin, frames.shape[1:3], world * (n - 1) + 1, [n - 1] * world
 
 
 def kernel_bytes(name, st, n_frames, h, w):
@@ -196,13 +225,11 @@ def main():
     from vfx_image_stitching_amd import distributed as D
     from vfx_image_stitching_amd.pipeline import Stitcher
 
-    frames, focals, margin, (h, w), distinct = workload(args.workload, rank, world)
+    frames, focals, margin, (h, w), distinct, counts = workload(args.workload, rank, world, args.scaling)
     n_local = len(frames)
     cap = args.cap or (4096 if args.workload != "synthetic" else 65536)
     st = Stitcher(args.method, cap=cap, match=args.match)
     dev = st.upload(frames)                                   # resident in HBM
-    counts = [c for _, c in synthetic_shards(world)] if args.workload == "synthetic" \
-        else [n_local - 1] * world
     pair_start = sum(counts[:rank])
 
     def step(graph=False):
@@ -328,11 +355,12 @@ def main():
 
     # correctness of what was timed: the single-GPU panorama against the reference's digest
     parity = None
-    if world == 1 and args.workload != "synthetic":
+    if world == 1 and args.workload != "synthetic" and len(frames) == 18:
         parity = check_parity(st, dev, focals, margin, args.workload, args.method, args.graph)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "synthetic":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "synthetic" \
+            and len(frames) == 18:
         cpu = cpu_baseline(frames, focals, args.cpu_frames, args.method, h, w)
 
     line = {
@@ -340,7 +368,7 @@ def main():
         else f"Mpixels/s stitched ({args.workload}, {args.method})",
         "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None,
+        "scaling": args.scaling, "vs_baseline": None,
         "dtype": ("u8 frames; f32 pyramid (fp64-accumulated blur); match " +
                   {"f32": "f32 MFMA", "bf16": "bf16 MFMA, exact for integer descriptors",
                    "i8": "i8 MFMA on u8 descriptors - 128, exact integer distances"}[match_dtype(st)]
@@ -348,7 +376,8 @@ def main():
         "data": "reference parrington JPEGs (packed under data/), decoded, resident in HBM"
         if args.workload != "synthetic" else "synthetic 1080p sequence (SURVEY 8d config 5)",
         "config": {"workload": f"{args.workload} {args.method} end-to-end: {distinct} frames "
-                               f"{h}x{w}, {distinct - 1} pairs, {world} rank(s) x {n_local} frames",
+                               f"{h}x{w}, {distinct - 1} pairs, {world} rank(s), this rank {n_local} "
+                               f"frames ({args.scaling} scaling)",
                    "frames": distinct, "frame_hw": [h, w], "parallelism": f"pairs sharded x{world}",
                    "method": args.method, "match_gemm": st.match,
                    "launch": "hipGraph replay" if args.graph else "eager"},
@@ -450,6 +479,19 @@ def _oracle_features(args):
         return osift.detect_and_describe(cyl) if method == "sift" else oharris.detect_and_describe(cyl)
 
 
+def _warm_worker():
+    """Pool initializer: every worker imports numpy / the oracle and loads its C blur before
+    the timed region (first imports would otherwise land inside it)."""
+    from oracle import cv2_compat, harris, sift, stitch  # noqa: F401
+    from threadpoolctl import threadpool_limits  # noqa: F401
+    cv2_compat._cv_blur_lib()
+
+
+def _ready(_):
+    time.sleep(0.2)                    # one short task per worker: all are up before t0
+    return os.getpid()
+
+
 def cpu_cores():
     """Host cores this process may use, capped at the box's CPU share (16)."""
     try:
@@ -469,8 +511,10 @@ def cpu_baseline(frames, focals, n, method, h, w):
     n = len(frames) if n <= 0 else min(n, len(frames))
     cores = cpu_cores()
     ctx = mp.get_context("spawn")                              # no fork of a HIP process
-    with ctx.Pool(min(cores, n)) as pool:
-        pool.map(_oracle_features, [(frames[0], focals[0], method)])          # warm the workers
+    k = min(cores, n)
+    with ctx.Pool(k, initializer=_warm_worker) as pool:
+        pool.map(_ready, range(k), chunksize=1)                              # every worker warm
+        pool.map(_oracle_features, [(frames[0], focals[0], method)])        # numpy kernels warm
         t0 = time.perf_counter()
         feats = pool.map(_oracle_features, [(frames[i], focals[i], method) for i in range(n)])
         ostitch.stitch(list(frames[:n]), list(focals[:n]), method=method, margin=15, features=feats)

@@ -139,6 +139,45 @@ int pano_sift_pyramid(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
 int pano_sift_level_shape(pano_ctx *ctx, int octave, int *h_out, int *w_out, int *n_octaves);
 int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int dog, float *d_out);
 
+/* Stage functions on caller data (sift_visualizeUI.py:104-115 calls them one by one):
+ *
+ * pano_sift_base         generate_base_image(image, sigma, assumed_blur)  sift_impl.py:45-56
+ *                        d_gray [n][h][w] f32 gray -> d_base [n][2h][2w] f32 (x2 INTER_LINEAR,
+ *                        then GaussianBlur sigma_diff).  Exact for integer-valued gray.
+ * pano_sift_pyramid_base generate_gaussian_images(base, num_octaves, kernels) + generate_DoG_images
+ *                        sift_impl.py:82-111 on ANY f32 base d_base [n][H0][W0]: the base is
+ *                        level 0 of octave 0; every Gaussian and DoG level stays resident
+ *                        (pano_sift_copy_level reads them back).  The kernels are those of
+ *                        params (sigma, num_intervals).
+ * pano_sift_reserve_levels + pano_sift_set_level
+ *                        lay out a resident pyramid for n frames with octave 0 of H0 x W0 and
+ *                        upload caller levels into it (Gaussian: dog = 0, DoG: dog = 1), e.g.
+ *                        pyramids the caller built or edited; pano_sift_dog recomputes every
+ *                        DoG level from the resident Gaussian levels (generate_DoG_images).
+ * pano_sift_extrema      find_scale_space_extrema(gaussian_images, dog_images, ...)
+ *                        sift_impl.py:117-140 on the resident pyramid: the oriented keypoints
+ *                        BEFORE remove_duplicate_keypoints, in the reference's scan order
+ *                        (octave, layer, y, x; orientations in peak order), base coordinates.
+ *                        d_raw [n][cap], d_counts [n] (> cap: entries dropped; -1: an internal
+ *                        scratch capacity overflowed, PANO_E_OVERFLOW from pano_sync).
+ * pano_sift_describe     generate_descriptors(keypoints, gaussian_images)  sift_impl.py:361-526
+ *                        for caller keypoints (input-image coordinates, converted octave
+ *                        field) d_kps [n][cap] / d_counts [n] on the resident pyramid, which
+ *                        must hold every Gaussian level (pano_sift_pyramid, _pyramid_base or
+ *                        _reserve_levels): d_desc [n][cap][128] f32.  A keypoint whose octave
+ *                        or layer lies outside the pyramid gets a zero descriptor. */
+int pano_sift_base(pano_ctx *ctx, const float *d_gray, int n, int h, int w,
+                   const pano_sift_params *params, float *d_base);
+int pano_sift_pyramid_base(pano_ctx *ctx, const float *d_base, int n, int H0, int W0, int n_octaves,
+                           const pano_sift_params *params);
+int pano_sift_reserve_levels(pano_ctx *ctx, int n, int H0, int W0, int n_octaves, int n_levels);
+int pano_sift_set_level(pano_ctx *ctx, int frame, int octave, int level, int dog, const float *d_in);
+int pano_sift_dog(pano_ctx *ctx);
+int pano_sift_extrema(pano_ctx *ctx, const pano_sift_params *params, pano_kp *d_raw, int cap,
+                      int32_t *d_counts);
+int pano_sift_describe(pano_ctx *ctx, const pano_sift_params *params, const pano_kp *d_kps,
+                       const int32_t *d_counts, int cap, float *d_desc);
+
 /* ---------------------------------------------------------------- H1..H3
  * compute_keypoints_and_descriptors_harris(img_bgr, max_points)  image_stitching_harris.py:187-214
  * d_xy [n][max_points][2] int32 (x, y), d_desc [n][max_points][128] f32, d_counts [n]. */

@@ -20,15 +20,17 @@ imread / imwrite            image_stitching_sift.py:282,386
 Numeric definitions (these ARE the oracle's definitions):
 
 * BGR2GRAY on uint8 is OpenCV's fixed point ``(1868 B + 9617 G + 4899 R + 8192) >> 14``.
-* GaussianBlur taps follow getGaussianKernel: ``t_i = exp(-x_i^2 / (2 s^2))`` in double,
-  stored in the kernel dtype (f32 kernel for f32 images, f64 for f64), normalised by
-  multiplying with ``1 / sum`` (sum in double) and stored again in the kernel dtype.
-  ``ksize = rint(8 s + 1) | 1`` when ksize is (0, 0) (float images).
-  Separable: row pass, then column pass; BORDER_REFLECT_101 with periodic repetition
-  for images narrower than the kernel.  Each output of a pass is accumulated in double
-  in tap order ``i = 0 .. n-1`` and rounded once to the image dtype.  For f32 images
-  every product ``tap_f32 * pixel_f32`` is exact in double, so only the summation order
-  is fixed by this definition (and it is what the HIP kernels do).
+* GaussianBlur on float32 images (the SIFT path) is OpenCV 4.x's arithmetic, pinned by the
+  author's published SIFT panoramas (grail pixel-identical): taps from
+  getGaussianKernelBitExact cast to f32; ``ksize = rint(8 s + 1) | 1``; a row pass
+  ``s = x0*k0; s = fma(x_i, k_i, s)`` in f32 over the taps in order, into an f32 buffer;
+  a column pass in the symmetric form ``s = S0*kc; s = fma(S_+i + S_-i, k_i, s)`` in f32,
+  i = 1..r outward from the centre (oracle/cv_blur.c).  BORDER_REFLECT_101 with periodic
+  repetition for images narrower than the kernel.  Other arithmetic variants stay
+  selectable for the sweep (``BLUR_VARIANT``).
+* GaussianBlur on float64 images (the Harris path): taps ``t_i = exp(-x_i^2 / (2 s^2))``
+  normalised by their double sum, separable, each output accumulated in double in tap
+  order (pinned pixel-identically by the published Harris panoramas).
 * INTER_LINEAR (x2): ``sx = (dx + 0.5) * inv - 0.5``, clamped at both edges, f32 weights;
   exact for integer-valued inputs.
 * INTER_NEAREST: ``sx = min(floor(dx * (1 / (dst_w / src_w))), src_w - 1)``.
@@ -157,6 +159,105 @@ def getGaussianKernel(ksize: int, sigma: float, ktype=np.float64) -> np.ndarray:
     return taps
 
 
+def getGaussianKernelBitExact(ksize: int, sigma: float) -> np.ndarray:
+    """OpenCV 4.x getGaussianKernel (via getGaussianKernelBitExact, imgproc/src/smooth.dispatch.cpp).
+
+    softdouble arithmetic is IEEE double without contraction, which Python floats are; the
+    one difference is OpenCV's own softdouble ``exp`` against libm's (both within an ulp of
+    double, far below the f32 rounding of the taps).  Per tap: ``exp(x*x * (-0.125 / s^2))``
+    with the integer ``x = 1 - n, 3 - n, ...`` (twice the offset), the sum as
+    ``2 * sum(side taps) + 1``, and every tap multiplied by ``1 / sum``; the centre tap is
+    ``1 / sum`` itself.  Returned as float64 (the caller casts to the kernel dtype).
+    """
+    if sigma <= 0:
+        sigma = ((ksize - 1) * 0.5 - 1) * 0.3 + 0.8
+    scale2x = -0.125 / (sigma * sigma)
+    n2 = (ksize - 1) // 2
+    vals = []
+    s = 0.0
+    x = 1 - ksize
+    for _ in range(n2):
+        t = math.exp(float(x * x) * scale2x)
+        vals.append(t)
+        s += t
+        x += 2
+    s *= 2.0
+    s += 1.0
+    if ksize % 2 == 0:
+        s += 1.0
+    mul1 = 1.0 / s
+    out = np.empty(ksize, np.float64)
+    if ksize % 2 == 1:
+        out[n2] = mul1
+    for i in range(n2):
+        t = vals[i] * mul1
+        out[i] = t
+        out[ksize - 1 - i] = t
+    return out
+
+
+# f32 GaussianBlur arithmetic variants (oracle/cv_blur.c).  "taps:row:col" with
+#   taps  legacy   -- getGaussianKernel above (f32 taps summed in double; OpenCV 3.x)
+#         bitexact -- getGaussianKernelBitExact (OpenCV 4.x)
+#   row   f64 | fma | mul   (f64 accumulate; f32 sequential fused; f32 sequential unfused)
+#   col   f64 | symfma | symmul | fma   (f32 symmetric pair form fused / unfused; f32 sequential)
+# The default, bitexact:fma:symfma (OpenCV 4.x taps; RowVec_32f and SymmColumnVec_32f under
+# FMA3), reproduces the author's published SIFT grail panorama pixel for pixel and the
+# parrington one at its published shape (tools/blur_variants.py, DESIGN.md 4); legacy:f64:f64
+# is the round-1/2 definition.
+_ROW_MODES = {"f64": 0, "fma": 1, "mul": 2}
+_COL_MODES = {"f64": 0, "symfma": 1, "symmul": 2, "fma": 3}
+DEFAULT_BLUR = "bitexact:fma:symfma"
+BLUR_VARIANT = os.environ.get("CV2_COMPAT_BLUR", DEFAULT_BLUR)
+_CVB = None
+
+
+def set_blur_variant(spec: str) -> None:
+    global BLUR_VARIANT
+    taps, row, col = spec.split(":")
+    if taps not in ("legacy", "bitexact") or row not in _ROW_MODES or col not in _COL_MODES:
+        raise ValueError(f"blur variant {spec!r}")
+    BLUR_VARIANT = spec
+
+
+def _cv_blur_lib():
+    global _CVB
+    if _CVB is None:
+        import ctypes
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcv_blur.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(path)
+        fp = ctypes.POINTER(ctypes.c_float)
+        lib.cvb_gaussian_f32.argtypes = [fp, fp, fp, ctypes.c_int, ctypes.c_int, fp, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int]
+        lib.cvb_gaussian_f32.restype = ctypes.c_int
+        _CVB = lib
+    return _CVB
+
+
+def gaussian_f32_variant(img: np.ndarray, ksize: int, sigma: float, spec: str) -> np.ndarray:
+    """Square-kernel f32 GaussianBlur under an arithmetic variant (see BLUR_VARIANT)."""
+    import ctypes
+    taps, row, col = spec.split(":")
+    if taps == "legacy":
+        k = getGaussianKernel(ksize, sigma, np.float32)
+    else:
+        k = getGaussianKernelBitExact(ksize, sigma).astype(np.float32)
+    k = np.ascontiguousarray(k, np.float32)
+    src = np.ascontiguousarray(img, np.float32)
+    h, w = src.shape
+    dst = np.empty_like(src)
+    tmp = np.empty_like(src)
+    fp = ctypes.POINTER(ctypes.c_float)
+    rc = _cv_blur_lib().cvb_gaussian_f32(src.ctypes.data_as(fp), dst.ctypes.data_as(fp),
+                                         tmp.ctypes.data_as(fp), h, w, k.ctypes.data_as(fp),
+                                         ksize, _ROW_MODES[row], _COL_MODES[col])
+    if rc != 0:
+        raise ValueError("cvb_gaussian_f32 refused its arguments")
+    return dst
+
+
 def reflect101(idx: np.ndarray, n: int) -> np.ndarray:
     """BORDER_REFLECT_101 index map, periodic for offsets beyond one reflection."""
     if n == 1:
@@ -191,6 +292,10 @@ def GaussianBlur(img, ksize, sigmaX, dst=None, sigmaY=0, borderType=BORDER_REFLE
     if kh <= 0:
         kh = gaussian_ksize(sigmaY)
     kt = img.dtype.type
+    if kt is np.float32 and BLUR_VARIANT != "legacy:f64:f64":
+        if kw != kh or sigmaX != sigmaY or img.ndim != 2:
+            raise NotImplementedError("f32 GaussianBlur restated for square kernels (all call sites)")
+        return gaussian_f32_variant(img, kw, sigmaX, BLUR_VARIANT)
     kx = getGaussianKernel(kw, sigmaX, kt)
     ky = getGaussianKernel(kh, sigmaY, kt)
     if img.ndim != 2:

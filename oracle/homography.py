@@ -9,7 +9,7 @@ RANSAC sampler), so the product path (csrc/homography.hip) fixes a deterministic
 algorithm and this module restates exactly that algorithm in numpy:
 
 ``knn2``            exact brute-force two nearest neighbours, squared L2 (FLANN approximates)
-``good_matches``    d1 < ratio^2 * d2 on the squared distances (ratio on the distances)
+``good_matches``    float32 sqrt(d1) < ratio * sqrt(d2) (the matcher's L2 distances, Python floats)
 ``sample``          splitmix64(seed ^ pair << 48 ^ hyp << 16 ^ draw) mod K, distinct indices
 ``good_sample``     cv2 HomographyEstimatorCallback::checkSubset: no collinear triple, equal
                     triangle orientations in source and destination
@@ -60,13 +60,15 @@ def knn2(desc_a: np.ndarray, desc_b: np.ndarray):
 
 def good_matches(best, d1, d2, ratio=0.7, desc_thresh=0.0):
     """Indices i of the good matches in query order (the visualiser's ``good`` list)."""
-    d1 = np.asarray(d1, np.float32).astype(np.float64)
-    d2 = np.asarray(d2, np.float32).astype(np.float64)
+    d1 = np.asarray(d1, np.float32)
+    d2 = np.asarray(d2, np.float32)
     ok = np.asarray(best) >= 0
     if desc_thresh > 0:
         ok &= d1 < np.float32(desc_thresh)
     if ratio > 0:
-        ok &= d1 < (ratio * ratio) * d2
+        # sift_visualizeUI.py:252-257: m.distance < 0.7 * n.distance, the matcher's float32
+        # L2 distances (sqrt of the squared distance) compared as Python floats
+        ok &= np.sqrt(d1).astype(np.float64) < ratio * np.sqrt(d2).astype(np.float64)
     return np.nonzero(ok)[0]
 
 

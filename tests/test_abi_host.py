@@ -64,7 +64,9 @@ def test_gaussian_taps_match_cv2_restatement(sigma):
     out = (ctypes.c_double * 64)()
     n = ctypes.c_int32()
     assert lib.pano_sift_taps(sigma, out, ctypes.byref(n)) == 0
-    k = cv2_compat.getGaussianKernel(cv2_compat.gaussian_ksize(sigma), sigma, np.float32)
+    # OpenCV 4.x getGaussianKernel(CV_32F): the bit-exact kernel cast to f32 (the published
+    # SIFT panoramas pin this form)
+    k = cv2_compat.getGaussianKernelBitExact(cv2_compat.gaussian_ksize(sigma), sigma).astype(np.float32)
     assert n.value == len(k)
     np.testing.assert_array_equal(np.array(out[:n.value]), k.astype(np.float64))
 

@@ -532,6 +532,24 @@ def test_run_rank_world1_is_the_single_gpu_stitch(gpu, parrington, graph):
     st.release_graphs()
 
 
+def test_run_rank_world1_falls_back_to_the_host_plan(gpu):
+    """World 1 with columns covered by three frames (|dx| < w / 2): the device plan refuses
+    and run_rank composites with the host plan, as Stitcher.run does -- same bytes."""
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd import distributed as D
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    frames, focals, _ = data.synthetic_sequence(n_frames=6, h=256, w=320, step=100, focal=400.0)
+    st = Stitcher("sift")
+    dev = st.upload(frames)
+    full = st.run(dev, focals, margin=5, device_plan=False)
+    canvas = full.canvas.cpu().numpy()
+    out = D.run_rank(st, dev, list(focals), 0, [len(frames) - 1], margin=5)
+    assert np.array_equal(out["records"].view(np.uint8), full.records.view(np.uint8))
+    assert out["canvas_hw"] == canvas.shape[:2] and out["x_offset"] == 0
+    assert np.array_equal(out["band"].cpu().numpy(), canvas)
+    assert out["bbox"] == full.bbox
+
+
 # ------------------------------------------------------------------ hipGraph replay
 @pytest.mark.parametrize("method,setname", [("sift", "parrington"), ("harris", "grail")])
 def test_graph_replay_matches_eager(gpu, method, setname, gold_json):
@@ -588,9 +606,8 @@ def test_lowe_ratio_filter_vs_exact_knn2(gpu, gold_npz, ratio):
     """pano_match (kNN-2: d1, d2) + pano_pair_shifts with ratio > 0 on the reference's own
     prtn00 / prtn01 keypoints and descriptors, against the oracle's exact brute-force kNN-2:
     match i is kept iff d1 < desc_thresh and m.distance < ratio * n.distance
-    (sift_visualizeUI.py:252-257 on exact -- not FLANN -- neighbours; the kernel compares the
-    squared distances, d1 < ratio^2 d2, which is the same decision for these exact integer
-    distances), and the translation vote runs on the survivors."""
+    (sift_visualizeUI.py:252-257 on exact -- not FLANN -- neighbours, float32 L2 distances
+    compared as Python floats), and the translation vote runs on the survivors."""
     import torch
     from vfx_image_stitching_amd import _lib
     g = gold_npz("sift_pair.npz")
@@ -624,8 +641,8 @@ def test_lowe_ratio_filter_vs_exact_knn2(gpu, gold_npz, ratio):
     full = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2 * A @ B.T
     order = np.argsort(full, axis=1, kind="stable")
     m1, m2 = full[np.arange(len(A)), order[:, 0]], full[np.arange(len(A)), order[:, 1]]
-    keep = (m1 < 25000) & (np.sqrt(m1) < ratio * np.sqrt(m2))
-    assert np.array_equal(keep, (m1 < 25000) & (m1 < ratio * ratio * m2))
+    keep = (m1 < 25000) & (np.sqrt(m1.astype(np.float32)).astype(np.float64) <
+                           ratio * np.sqrt(m2.astype(np.float32)).astype(np.float64))
     matches = [((float(kp[0, i]["x"]), float(kp[0, i]["y"])),
                 (float(kp[1, order[i, 0]]["x"]), float(kp[1, order[i, 0]]["y"])))
                for i in np.nonzero(keep)[0]]

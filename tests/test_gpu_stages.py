@@ -1,0 +1,186 @@
+"""The sift_impl stage functions, called one by one as the reference's GUI calls them
+(/root/reference/sift_visualizeUI.py:104-115), on the GPU through the C-ABI.
+
+Goldens: tests/golden/sift_pair.npz, the reference's own staged run on prtn00 / prtn01 /
+prtn02 (tests/golden/make_golden.py sift_pair): every pyramid level's digest, the raw
+oriented keypoints of find_scale_space_extrema ({stem}_raw_*), the final keypoints and the
+uint8 descriptors.  Bars as tests/test_gpu_parity.py: pyramid bit-exact, positions /
+responses / octaves exact, size <= 1 ulp, angle bin flips <= 0.1 %, descriptors <= 1 LSB.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import digest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def frames00(parrington):
+    from oracle import stitch as ostitch
+    names, frames, focals, _ = parrington
+    out = {}
+    for stem in ("prtn00", "prtn01"):
+        i = names.index(stem + ".jpg")
+        out[stem] = ostitch.cylindrical(frames[i], focals[i])
+    return out
+
+
+def _kp_table(kps):
+    return {"x": np.array([k.pt[0] for k in kps], np.float32),
+            "y": np.array([k.pt[1] for k in kps], np.float32),
+            "size": np.array([k.size for k in kps], np.float32),
+            "angle": np.array([k.angle for k in kps], np.float32),
+            "response": np.array([k.response for k in kps], np.float32),
+            "octave": np.array([k.octave for k in kps], np.int64)}
+
+
+def _gold_table(g, stem, part):
+    return {k: g[f"{stem}_{part}_{k}"] for k in ("x", "y", "size", "angle", "response", "octave")}
+
+
+def _compare_raw(t, gold):
+    """Raw keypoints come out in the reference's scan order; a histogram bin flip (numpy's SIMD
+    atan2f, see test_gpu_parity._compare_features) may add or drop one orientation of a
+    candidate, so rows are matched on (x, y, octave, response) in order."""
+    n = len(t["x"])
+    m = len(gold["x"])
+    assert abs(n - m) <= max(2, m // 1000), (n, m)
+    if n == m:
+        for k in ("x", "y", "response", "octave"):
+            np.testing.assert_array_equal(t[k], gold[k].astype(t[k].dtype), err_msg=k)
+        np.testing.assert_allclose(t["size"], gold["size"], rtol=3e-7, atol=0)
+        da = np.abs(t["angle"].astype(np.float64) - gold["angle"])
+        da = np.minimum(da, 360 - da)
+        assert (da > 2e-3).mean() <= 1e-3 and da.max() < 1.0
+    else:
+        key = lambda tb, i: (float(tb["x"][i]), float(tb["y"][i]), int(tb["octave"][i]))
+        a = {key(t, i) for i in range(n)}
+        b = {key(gold, i) for i in range(m)}
+        assert a == b, "raw keypoint positions differ beyond orientation flips"
+
+
+@pytest.mark.parametrize("stem", ["prtn00", "prtn01"])
+def test_gui_stage_sequence(gpu, frames00, gold_npz, stem):
+    """sift_visualizeUI.py:104-115 verbatim through the drop-in: base, octaves, kernels,
+    Gaussian and DoG pyramids, raw extrema, dedup, conversion, descriptors."""
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import sift_impl
+    g = gold_npz("sift_pair.npz")
+    img = bgr_to_gray_u8(frames00[stem]).astype("float32")
+    base = sift_impl.generate_base_image(img, sigma=1.6, assumed_blur=0.5)
+    assert base.dtype == np.float32 and base.shape == (2 * img.shape[0], 2 * img.shape[1])
+    num_octaves = sift_impl.compute_number_of_octaves(base.shape)
+    kernels = sift_impl.generate_gaussian_kernels(1.6, num_intervals=3)
+    gauss = sift_impl.generate_gaussian_images(base, num_octaves, kernels)
+    dogs = sift_impl.generate_DoG_images(gauss)
+    assert gauss.shape == (num_octaves, 6) and dogs.shape == (num_octaves, 5)
+    for o in range(num_octaves):
+        for l in range(6):
+            want = bytes(g[f"{stem}_g{o}_{l}_digest"]).decode()
+            assert digest(gauss[o, l]) == want, (o, l)
+        for l in range(5):
+            np.testing.assert_array_equal(dogs[o, l], gauss[o, l + 1] - gauss[o, l])
+    raw = sift_impl.find_scale_space_extrema(gauss, dogs, num_intervals=3, sigma=1.6, border=5)
+    _compare_raw(_kp_table(raw), _gold_table(g, stem, "raw"))
+    no_dup = sift_impl.remove_duplicate_keypoints(list(raw))
+    conv = sift_impl.convert_keypoints_to_input_image_size(no_dup)
+    desc = sift_impl.generate_descriptors(conv, gauss)
+    gold = _gold_table(g, stem, "kp")
+    t = _kp_table(conv)
+    assert len(conv) == len(gold["x"])
+    np.testing.assert_array_equal(t["x"], gold["x"])
+    np.testing.assert_array_equal(t["y"], gold["y"])
+    d = np.abs(desc - g[f"{stem}_desc"].astype(np.float32))
+    assert desc.dtype == np.float32 and desc.shape == (len(conv), 128)
+    assert (d.max(1) > 1).mean() <= 1e-3 and (d > 0).mean() < 1e-3
+
+
+def test_generate_descriptors_on_golden_keypoints(gpu, frames00, gold_npz):
+    """generate_descriptors on the reference's own converted keypoints (not ours)."""
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import sift_impl
+    from vfx_image_stitching_amd.keypoint import KeyPoint
+    g = gold_npz("sift_pair.npz")
+    stem = "prtn00"
+    img = bgr_to_gray_u8(frames00[stem]).astype("float32")
+    base = sift_impl.generate_base_image(img, 1.6, 0.5)
+    gauss = sift_impl.generate_gaussian_images(base, sift_impl.compute_number_of_octaves(base.shape),
+                                               sift_impl.generate_gaussian_kernels(1.6, 3))
+    t = _gold_table(g, stem, "kp")
+    kps = [KeyPoint(float(t["x"][i]), float(t["y"][i]), float(t["size"][i]), float(t["angle"][i]),
+                    float(t["response"][i]), int(t["octave"][i])) for i in range(len(t["x"]))]
+    desc = sift_impl.generate_descriptors(kps, gauss)
+    want = g[f"{stem}_desc"].astype(np.float32)
+    d = np.abs(desc - want)
+    assert d.max() <= 1 and (d > 0).mean() < 1e-3, (d.max(), (d > 0).mean())
+    # out-of-pyramid keypoints are refused like the reference's IndexError
+    bad = KeyPoint(10.0, 10.0, 2.0, 0.0, 0.1, (gauss.shape[0] + 3) & 255)
+    with pytest.raises(IndexError):
+        sift_impl.generate_descriptors([bad], gauss)
+    assert sift_impl.generate_descriptors([], gauss).shape == (0,)
+
+
+def test_pyramid_from_any_float_base(gpu, frames00):
+    """generate_gaussian_images takes any float32 base (a non-integer one here): its levels
+    equal the oracle's cascade on the same base, bit for bit."""
+    from oracle import cv2_compat, sift as osift
+    from vfx_image_stitching_amd import sift_impl
+    rng = np.random.default_rng(5)
+    base = (rng.random((96, 130)) * 200).astype(np.float32)
+    kernels = sift_impl.generate_gaussian_kernels(1.6, 3)
+    gauss = sift_impl.generate_gaussian_images(base, 4, kernels)
+    ref = osift.gaussian_pyramid(base, 4, kernels)
+    for o in range(4):
+        for l in range(6):
+            np.testing.assert_array_equal(gauss[o, l], ref[o][l], err_msg=f"{o},{l}")
+    with pytest.raises(NotImplementedError):
+        sift_impl.generate_gaussian_images(base, 2, [1.6, 1.0, 1.0, 1.0, 1.0, 1.0])
+
+
+def test_float_gray_base_image(gpu, frames00):
+    """generate_base_image on an f32 gray image equals the oracle's S1 (integer-valued: exact)."""
+    from oracle import sift as osift
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import sift_impl
+    img = bgr_to_gray_u8(frames00["prtn01"]).astype(np.float32)
+    np.testing.assert_array_equal(sift_impl.generate_base_image(img, 1.6, 0.5), osift.base_image(img))
+
+
+def test_scalar_helpers_match_the_batched_kernels(gpu, frames00):
+    """The per-pixel helpers (host) agree with the batched GPU stages on real extrema."""
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import sift_impl
+    img = bgr_to_gray_u8(frames00["prtn00"]).astype("float32")
+    base = sift_impl.generate_base_image(img, 1.6, 0.5)
+    gauss = sift_impl.generate_gaussian_images(base, sift_impl.compute_number_of_octaves(base.shape),
+                                               sift_impl.generate_gaussian_kernels(1.6, 3))
+    dogs = sift_impl.generate_DoG_images(gauss)
+    raw = sift_impl.find_scale_space_extrema(gauss, dogs, 3, 1.6, 5)
+    # re-localise the first few raw keypoints of octave 1 from their integer positions
+    checked = 0
+    for kp in raw:
+        o = kp.octave & 255
+        layer = (kp.octave >> 8) & 255
+        if o != 1:
+            continue
+        x = int(round(kp.pt[0] / 2 ** o))
+        y = int(round(kp.pt[1] / 2 ** o))
+        d = dogs[o]
+        thr = np.floor(0.5 * 0.04 / 3 * 255)
+        res = sift_impl.localize_extremum_via_quadratic_fit(x, y, layer, o, 3, d, 1.6, 0.04, 5)
+        if res is None or not sift_impl.is_pixel_an_extremum(d[layer - 1][y - 1:y + 2, x - 1:x + 2],
+                                                             d[layer][y - 1:y + 2, x - 1:x + 2],
+                                                             d[layer + 1][y - 1:y + 2, x - 1:x + 2], thr):
+            continue
+        k2, lyr = res
+        if (k2.pt, k2.octave) != (kp.pt, kp.octave):
+            continue                         # the fit moved: another candidate's keypoint
+        oris = sift_impl.compute_keypoints_with_orientations(k2, o, gauss[o][lyr])
+        assert any(abs(r.angle - kp.angle) < 1e-3 for r in oris)
+        checked += 1
+        if checked == 5:
+            break
+    assert checked >= 3

@@ -89,6 +89,14 @@ def test_oracle_ratio_filter_and_knn2():
     assert (d1 == brute.min(1)).all()
 
 
+def test_ratio_boundary_is_the_float32_distance_form():
+    """(1078, 2200): the squared form 1078 < 0.49 * 2200 is False (equal), the visualiser's
+    float32 L2 form sqrt(1078) < 0.7 * sqrt(2200) is True; good_matches follows the latter."""
+    best = np.array([0], np.int32)
+    assert ohom.good_matches(best, np.array([1078], np.float32), np.array([2200], np.float32)).tolist() == [0]
+    assert not 1078 < 0.49 * 2200
+
+
 # ------------------------------------------------------------------ GPU: pano_pair_homography
 def _device_pairs(torch, sets, cap):
     """Frames 2p (source points) and 2p+1 (destination points) with best = identity."""
@@ -154,6 +162,36 @@ def test_pair_homography_vs_oracle_known_homographies(gpu):
 
 
 @pytest.mark.gpu
+def test_pair_homography_more_than_256_pairs(gpu):
+    """Batches above one 256-pair chunk: the sample hash takes the GLOBAL pair index, so pair
+    p + 256 draws its own hypotheses and matches the oracle at pair = p + 256."""
+    import torch
+    S, D = _correspondences(31, 60, 0.3)[1:3]
+    P = 300
+    sets = [(S, D)] * P
+    cap = 64
+    dev = _device_pairs(torch, sets, cap)
+    recs, mask = _run_device(gpu, torch, *dev, cap, [(2 * p, 2 * p + 1) for p in range(P)], n_hyp=64,
+                             seed=5)
+    for p in (0, 1, 255, 256, 257, 299):
+        ref = ohom.find_homography(S, D, thr=5.0, n_hyp=64, seed=5, pair=p)
+        _assert_rec_matches_oracle(recs[p], mask[p], ref, len(S))
+
+
+@pytest.mark.gpu
+def test_pair_homography_ratio_boundary(gpu):
+    """The kernel's ratio test at the (1078, 2200) boundary keeps the match (float32 L2 form)."""
+    import torch
+    S, D = _correspondences(41, 30, 0.0)[1:3]
+    cap = 64
+    kps, counts, best, d1, d2 = _device_pairs(torch, [(S, D)], cap)
+    d1.fill_(1078.0)
+    d2.fill_(2200.0)
+    recs, _ = _run_device(gpu, torch, kps, counts, best, d1, d2, cap, [(0, 1)], n_hyp=64)
+    assert int(recs["n_matches"][0]) == 30
+
+
+@pytest.mark.gpu
 def test_pair_homography_degenerate_and_overflow(gpu):
     import torch
     rng = np.random.default_rng(3)
@@ -175,7 +213,7 @@ def test_pair_homography_degenerate_and_overflow(gpu):
     recs2, _ = _run_device(gpu, torch, kps2, counts2, best2, d12, d22, cap, [(0, 1)])
     assert recs2["status"][0] == -4 and recs2["n_matches"][0] == 0
     kps3, counts3, best3, d13, d23 = _device_pairs(torch, [ok], cap)
-    d23.fill_(11.0)                          # 10 < 0.49 * 11 fails
+    d23.fill_(11.0)                          # sqrt(10) < 0.7 sqrt(11) fails
     recs3, _ = _run_device(gpu, torch, kps3, counts3, best3, d13, d23, cap, [(0, 1)])
     assert recs3["status"][0] == -4 and recs3["n_matches"][0] == 0
 

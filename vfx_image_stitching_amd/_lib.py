@@ -106,6 +106,13 @@ SIGNATURES = {
     "pano_sift": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P, _P, _I, _P]),
     "pano_sift_u8": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P, _P, _P, _I, _P]),
     "pano_sift_pyramid": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams)]),
+    "pano_sift_base": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P]),
+    "pano_sift_pyramid_base": (_I, [_P, _P, _I, _I, _I, _I, ctypes.POINTER(SiftParams)]),
+    "pano_sift_reserve_levels": (_I, [_P, _I, _I, _I, _I, _I]),
+    "pano_sift_set_level": (_I, [_P, _I, _I, _I, _I, _P]),
+    "pano_sift_dog": (_I, [_P]),
+    "pano_sift_extrema": (_I, [_P, ctypes.POINTER(SiftParams), _P, _I, _P]),
+    "pano_sift_describe": (_I, [_P, ctypes.POINTER(SiftParams), _P, _P, _I, _P]),
     "pano_sift_level_shape": (_I, [_P, _I, _PI32, _PI32, _PI32]),
     "pano_sift_copy_level": (_I, [_P, _I, _I, _I, _I, _P]),
     "pano_harris": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),

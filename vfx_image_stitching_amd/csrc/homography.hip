@@ -127,7 +127,7 @@ gather_points(const pano_kp *__restrict__ kps, int cap, PairArg pairs, const int
 __global__ void __launch_bounds__(HB)
 homography_hyp(const double2 *__restrict__ src, const double2 *__restrict__ dst,
                const int32_t *__restrict__ kcount, int cap, int n_hyp, int min_good,
-               unsigned long long seed, double thr2, int32_t *__restrict__ score) {
+               unsigned long long seed, double thr2, int32_t *__restrict__ score, int p0) {
     __shared__ double2 ts[HB], td[HB];
     const int p = blockIdx.y, tid = threadIdx.x;
     const int hyp = blockIdx.x * HB + tid;
@@ -142,7 +142,7 @@ homography_hyp(const double2 *__restrict__ src, const double2 *__restrict__ dst,
         for (int q = 0; q < 4; ++q) {
             for (;;) {                                    // distinct indices, deterministic
                 const unsigned long long r =
-                    splitmix64(seed ^ ((unsigned long long)p << 48) ^ ((unsigned long long)hyp << 16) ^ (unsigned long long)draw++);
+                    splitmix64(seed ^ ((unsigned long long)(p0 + p) << 48) ^ ((unsigned long long)hyp << 16) ^ (unsigned long long)draw++);
                 const int c = (int)(r % (unsigned long long)K);
                 bool dup = false;
                 for (int e = 0; e < q; ++e) dup |= idx[e] == c;
@@ -172,7 +172,7 @@ homography_select(const double2 *__restrict__ src, const double2 *__restrict__ d
                   const int32_t *__restrict__ kcount, int cap, int n_hyp, int min_good,
                   unsigned long long seed, double thr2, const int32_t *__restrict__ score,
                   const int32_t *__restrict__ counts, PairArg pairs,
-                  pano_homography_rec *__restrict__ recs, uint8_t *__restrict__ mask) {
+                  pano_homography_rec *__restrict__ recs, uint8_t *__restrict__ mask, int p0) {
     __shared__ int sv[HB], si[HB];
     __shared__ double red[HB];
     __shared__ double Hs[9];
@@ -227,7 +227,7 @@ homography_select(const double2 *__restrict__ src, const double2 *__restrict__ d
         for (int q = 0; q < 4; ++q) {
             for (;;) {
                 const unsigned long long rr =
-                    splitmix64(seed ^ ((unsigned long long)p << 48) ^ ((unsigned long long)hi << 16) ^ (unsigned long long)draw++);
+                    splitmix64(seed ^ ((unsigned long long)(p0 + p) << 48) ^ ((unsigned long long)hi << 16) ^ (unsigned long long)draw++);
                 const int c = (int)(rr % (unsigned long long)K);
                 bool dup = false;
                 for (int e = 0; e < q; ++e) dup |= idx[e] == c;
@@ -388,14 +388,14 @@ int launch_pair_homography(pano_ctx *ctx, const pano_kp *kps, const int32_t *cou
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
             homography_hyp<<<dim3((n_hyp + HB - 1) / HB, np), HB, 0, ctx->stream>>>(
-                src + o, dst + o, kcount + p0, cap, n_hyp, min_good, seed, thr2, score + (size_t)p0 * n_hyp);
+                src + o, dst + o, kcount + p0, cap, n_hyp, min_good, seed, thr2, score + (size_t)p0 * n_hyp, p0);
         }
         PANO_LAUNCH_CHECK(ctx, "homography_hyp");
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
             homography_select<<<np, HB, 0, ctx->stream>>>(src + o, dst + o, kcount + p0, cap, n_hyp,
                                                           min_good, seed, thr2, score + (size_t)p0 * n_hyp,
-                                                          counts, pa, recs + p0, mask ? mask + o : nullptr);
+                                                          counts, pa, recs + p0, mask ? mask + o : nullptr, p0);
         }
         PANO_LAUNCH_CHECK(ctx, "homography_select");
     }

@@ -180,6 +180,85 @@ int pano_sift_u8(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     return rc;
 }
 
+int pano_sift_base(pano_ctx *ctx, const float *gray, int n, int h, int w, const pano_sift_params *params,
+                   float *base) {
+    if (!ctx || !gray || !base || n <= 0 || h <= 0 || w <= 0)
+        return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_base") : PANO_E_ARG;
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    PyrSource src;
+    src.grayf = gray;
+    src.base_only = true;
+    int rc = launch_sift_pyramid_src(ctx, src, n, h, w, &p, false, false);
+    if (rc) return rc;
+    PANO_HIP(ctx, hipMemcpyAsync(base, ctx->pyr + ctx->gauss_off[0][0],
+                                 (size_t)n * ctx->oct_h[0] * ctx->oct_w[0] * sizeof(float),
+                                 hipMemcpyDeviceToDevice, ctx->stream));
+    return PANO_OK;
+}
+
+int pano_sift_pyramid_base(pano_ctx *ctx, const float *base, int n, int H0, int W0, int n_octaves,
+                           const pano_sift_params *params) {
+    if (!ctx || !base || n <= 0 || H0 <= 0 || W0 <= 0 || n_octaves <= 0)
+        return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_pyramid_base") : PANO_E_ARG;
+    if (n_octaves > PANO_MAX_OCTAVES)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_pyramid_base: more than PANO_MAX_OCTAVES octaves");
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    PyrSource src;
+    src.base = base;
+    src.max_oct = n_octaves;
+    return launch_sift_pyramid_src(ctx, src, n, H0, W0, &p, false, true);
+}
+
+int pano_sift_reserve_levels(pano_ctx *ctx, int n, int H0, int W0, int n_octaves, int n_levels) {
+    if (!ctx || n <= 0 || H0 <= 0 || W0 <= 0 || n_octaves <= 0 || n_levels < 3 || n_levels > PANO_MAX_LEVELS)
+        return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_reserve_levels") : PANO_E_ARG;
+    if (n_octaves > PANO_MAX_OCTAVES)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_reserve_levels: more than PANO_MAX_OCTAVES octaves");
+    sift_join_tail(ctx);
+    const int rc = sift_reserve_dims(ctx, n, H0, W0, n_octaves, n_levels);
+    if (rc == PANO_OK) ctx->pyr_full = true;
+    return rc;
+}
+
+int pano_sift_set_level(pano_ctx *ctx, int frame, int octave, int level, int dog, const float *in) {
+    if (!ctx || !in || frame < 0 || frame >= ctx->n || octave < 0 || octave >= ctx->n_oct) return PANO_E_ARG;
+    const int nl = dog ? ctx->n_lvl - 1 : ctx->n_lvl;
+    if (level < 0 || level >= nl) return PANO_E_ARG;
+    const size_t plane = (size_t)ctx->oct_h[octave] * ctx->oct_w[octave];
+    float *dst = dog ? ctx->dog + ctx->dog_off[octave][level] : ctx->pyr + ctx->gauss_off[octave][level];
+    PANO_HIP(ctx, hipMemcpyAsync(dst + (size_t)frame * plane, in, plane * sizeof(float),
+                                 hipMemcpyDeviceToDevice, ctx->stream));
+    return PANO_OK;
+}
+
+int pano_sift_dog(pano_ctx *ctx) {
+    if (!ctx) return PANO_E_ARG;
+    sift_join_tail(ctx);
+    return launch_sift_dog(ctx);
+}
+
+int pano_sift_extrema(pano_ctx *ctx, const pano_sift_params *params, pano_kp *raw, int cap, int32_t *counts) {
+    if (!ctx) return PANO_E_ARG;
+    if (!ctx->pyr || ctx->n <= 0) return pano_fail(ctx, PANO_E_ARG, "pano_sift_extrema: no resident pyramid");
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    if (p.num_intervals + 3 != ctx->n_lvl)
+        return pano_fail(ctx, PANO_E_ARG, "pano_sift_extrema: num_intervals does not match the pyramid");
+    const int rc = launch_sift_extrema(ctx, &p, raw, cap, counts);
+    sift_join_tail(ctx);
+    return rc;
+}
+
+int pano_sift_describe(pano_ctx *ctx, const pano_sift_params *params, const pano_kp *kps, const int32_t *counts,
+                       int cap, float *desc) {
+    if (!ctx) return PANO_E_ARG;
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    return launch_sift_describe(ctx, &p, kps, counts, cap, desc);
+}
+
 int pano_sift_level_shape(pano_ctx *ctx, int octave, int *h_out, int *w_out, int *n_octaves) {
     if (!ctx || octave < 0 || octave >= ctx->n_oct) return PANO_E_ARG;
     if (h_out) *h_out = ctx->oct_h[octave];

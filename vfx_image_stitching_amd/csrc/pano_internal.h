@@ -2,9 +2,9 @@
 //
 // Numerics policy (DESIGN.md "Parity"): every translation unit is compiled with
 // -ffp-contract=off so that a*b+c is two roundings unless a kernel asks for fma()
-// explicitly.  fma() is used only where the product is exact (f32 x f32 in double: the
-// separable Gaussian taps) or where the reference's own arithmetic is an FMA (the OpenBLAS
-// sdot order numpy uses).
+// explicitly.  fma() is used only where the reference's own arithmetic is an FMA (OpenCV's
+// float32 separable Gaussian under FMA3, the OpenBLAS sdot order numpy uses) or where the
+// product is exact.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -85,8 +85,8 @@ struct pano_ctx {
     size_t ext_bytes = 0;
     RawKp *raw_sorted = nullptr;
     uint32_t *sorted = nullptr; size_t sorted_bytes = 0;   // per-frame sorted raw indices
-    double *taps = nullptr;              // device Gaussian taps, per level [L][PANO_MAX_TAPS]
-    double taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // what *taps holds
+    float *taps = nullptr;               // device Gaussian taps (f32), per level [L][PANO_MAX_TAPS]
+    float taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];    // what *taps holds
     bool taps_valid = false;
     uint8_t *gray = nullptr; size_t gray_bytes = 0;   // u8 gray frames (base blur input)
     int32_t *boxslots = nullptr; size_t boxslots_bytes = 0;   // crop-box partials (kBoxSlots x 4)
@@ -177,6 +177,24 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
 // the top level (only its DoG is used).
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                         const pano_sift_params *p, bool defer_tail = false, bool full = true);
+// Pyramid input of the stage functions (sift_impl.py:45-97): exactly one source is set.
+struct PyrSource {
+    const uint8_t *bgr = nullptr;    // [n][h][w][3] u8 BGR (compute_keypoints_and_descriptors)
+    const float *grayf = nullptr;    // [n][h][w] f32 gray (generate_base_image)
+    const float *base = nullptr;     // [n][h][w] f32 base = octave 0, level 0 (generate_gaussian_images)
+    int max_oct = 0;                 // base source: the caller's num_octaves
+    bool base_only = false;          // stop after level 0 of octave 0 (generate_base_image)
+};
+int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, int w,
+                            const pano_sift_params *p, bool defer_tail, bool full);
+int sift_reserve_dims(pano_ctx *ctx, int n, int H0, int W0, int max_oct, int nl);
+int launch_sift_dog(pano_ctx *ctx);
+// Raw oriented keypoints (find_scale_space_extrema) of the resident pyramid in the
+// reference's scan order, base coordinates: d_raw [n][cap], d_counts [n].
+int launch_sift_extrema(pano_ctx *ctx, const pano_sift_params *p, pano_kp *raw, int cap, int32_t *counts);
+// generate_descriptors for caller keypoints on the resident pyramid: d_desc f32 [n][cap][128].
+int launch_sift_describe(pano_ctx *ctx, const pano_sift_params *p, const pano_kp *kps,
+                         const int32_t *counts, int cap, float *desc);
 // desc: f32 [n][cap][128] (drop-in form) or, when NULL, desc_u8 [n][cap][128] + norms [n][cap]
 int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
                           uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts);

@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(RB)
 pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
              const int32_t *__restrict__ counts, int cap, PairArg pairs,
              const int32_t *__restrict__ best, const float *__restrict__ d1,
-             const float *__restrict__ d2, float desc_thresh, double ratio2,
+             const float *__restrict__ d2, float desc_thresh, double ratio,
              double2 *__restrict__ moves, int32_t *__restrict__ midx, int32_t *__restrict__ kcount,
              int32_t *__restrict__ votes) {
     __shared__ int ish[2 * RB];
@@ -106,7 +106,10 @@ pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
         const int i = base + tid;
         int acc = 0;
         if (i < NA && bp[i] >= 0 && bp[i] < NB && p1[i] < desc_thresh)
-            acc = ratio2 > 0.0 ? ((double)p1[i] < ratio2 * (double)p2[i]) : 1;
+            // the visualiser's test m.distance < ratio * n.distance (sift_visualizeUI.py:252-257):
+            // FLANN / BFMatcher distances are float32 L2 norms, sqrtf of the exact squared
+            // distance (correctly rounded), compared in Python doubles
+            acc = ratio > 0.0 ? ((double)sqrtf(p1[i]) < ratio * (double)sqrtf(p2[i])) : 1;
         int tot;
         const int pos = block_excl_scan(acc, ish, tot);
         if (acc) {
@@ -296,7 +299,7 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
             pair_compact<<<np, RB, 0, ctx->stream>>>(
                 kps, xy_i32, counts, cap, pa, best + o, d1 + o, d2 ? d2 + o : nullptr,
-                (float)desc_thresh, ratio > 0 ? ratio * ratio : 0.0, moves + o, midx + o, kcount + p0, votes + o);
+                (float)desc_thresh, ratio > 0 ? ratio : 0.0, moves + o, midx + o, kcount + p0, votes + o);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_compact");
         {
@@ -331,7 +334,7 @@ int launch_match_compact(pano_ctx *ctx, const pano_kp *kps, const int32_t *count
         PanoProf prof_(ctx, PK_PAIR_SHIFTS);
         pair_compact<<<np, RB, 0, ctx->stream>>>(kps, nullptr, counts, cap, pa, best, d1, d2,
                                                 desc_thresh > 0 ? (float)desc_thresh : INFINITY,
-                                                ratio > 0 ? ratio * ratio : 0.0,
+                                                ratio > 0 ? ratio : 0.0,
                                                 (double2 *)moves, midx, kcount, nullptr);
     }
     PANO_LAUNCH_CHECK(ctx, "pair_compact");

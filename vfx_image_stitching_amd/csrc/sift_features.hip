@@ -59,7 +59,7 @@ constexpr int kCandMin = 8192;
 struct PyrArgs {   // all octaves, for the descriptor (level pointers are per frame batch)
     const float *gauss[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
     int H[PANO_MAX_OCTAVES], W[PANO_MAX_OCTAVES];
-    int n_oct;
+    int n_oct, n_lvl;
 };
 
 struct LocParams {
@@ -1184,6 +1184,20 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         const int lyr = (kp.octave >> 8) & 255;
         const float scl = oct >= 0 ? 1.0f / (float)(1 << oct) : (float)(1 << -oct);
         const int O = oct + 1;
+        const size_t row = (size_t)f * cap + k;
+        if (O < 0 || O >= pa.n_oct || lyr >= pa.n_lvl) {
+            // a caller keypoint (pano_sift_describe) whose octave / layer is outside the pyramid:
+            // zero descriptor (the Python boundary rejects these before the call)
+            if constexpr (OUT_U8) {
+                desc_u8[row * PANO_DESC_DIM + lane] = 0;
+                desc_u8[row * PANO_DESC_DIM + 64 + lane] = 0;
+                if (lane == 0) norms[row] = 0;
+            } else {
+                desc[row * PANO_DESC_DIM + lane] = 0.0f;
+                desc[row * PANO_DESC_DIM + 64 + lane] = 0.0f;
+            }
+            continue;
+        }
         const int rows = pa.H[O], cols = pa.W[O];
         const float *img = pa.gauss[O][lyr] + (size_t)f * rows * cols;
         const int px = (int)rint((double)scl * (double)kp.x);
@@ -1423,7 +1437,6 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         float dlo = rintf(512.0f * (lo / nv)), dhi = rintf(512.0f * (hi / nv));
         dlo = dlo < 0.0f ? 0.0f : (dlo > 255.0f ? 255.0f : dlo);
         dhi = dhi < 0.0f ? 0.0f : (dhi > 255.0f ? 255.0f : dhi);
-        const size_t row = (size_t)f * cap + k;
         if constexpr (OUT_U8) {
             desc_u8[row * PANO_DESC_DIM + lane] = (uint8_t)dlo;
             desc_u8[row * PANO_DESC_DIM + 64 + lane] = (uint8_t)dhi;
@@ -1441,14 +1454,64 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     }
 }
 
+// find_scale_space_extrema's output order (sift_impl.py:117-140): candidates in scan order
+// (octave, layer, y, x), each one's orientations in peak-bin order.  The RawKp order keys are
+// that order and unique per frame, so a record's position is the number of smaller keys;
+// the keys of the frame stream through LDS in tiles of 256.  Keypoints stay in base
+// coordinates (no dedup, no conversion).  counts[f] = raw count (> cap: dropped entries) or
+// -1 when an earlier stage overflowed its scratch.
+__global__ void __launch_bounds__(256)
+raw_scan_order(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap,
+               pano_kp *__restrict__ out, int cap, int32_t *__restrict__ counts, int32_t *__restrict__ err,
+               const int32_t *__restrict__ ext_cnt, int ext_cap, const int32_t *__restrict__ cand_cnt,
+               int cand_cap) {
+    __shared__ uint64_t keys[256];
+    const int f = blockIdx.y, tid = threadIdx.x, i = blockIdx.x * 256 + tid;
+    const int cnt = raw_cnt[f * kCntStride];
+    if (cnt > raw_cap || ext_cnt[f * kCntStride] > ext_cap || cand_cnt[f * kCntStride] > cand_cap) {
+        if (blockIdx.x == 0 && tid == 0) { err[0] = PANO_E_OVERFLOW; counts[f] = -1; }
+        return;
+    }
+    if (blockIdx.x == 0 && tid == 0) counts[f] = cnt;
+    if (blockIdx.x * 256 >= cnt) return;                 // uniform per workgroup
+    const RawKp *rec = raw + (size_t)f * raw_cap;
+    const uint64_t mine = i < cnt ? rec[i].order : ~0ull;
+    int rank = 0;
+    for (int t0 = 0; t0 < cnt; t0 += 256) {
+        __syncthreads();
+        keys[tid] = t0 + tid < cnt ? rec[t0 + tid].order : ~0ull;
+        __syncthreads();
+        const int m = min(256, cnt - t0);
+        for (int j = 0; j < m; ++j) rank += keys[j] < mine;
+    }
+    if (i < cnt && rank < cap) {
+        const RawKp q = rec[i];
+        pano_kp o;
+        o.x = q.x;
+        o.y = q.y;
+        o.size = q.size;
+        o.angle = q.angle;
+        o.response = q.response;
+        o.octave = q.octave;
+        out[(size_t)f * cap + rank] = o;
+    }
+}
+
 }  // namespace
 
 int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p);
 
-int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
-                          uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts) {
+namespace {
+int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &pa, const pano_kp *kps,
+                       const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
+                       int32_t *norms);
+
+// raw_out != NULL: find_scale_space_extrema only (stops after the orientations and writes the
+// raw keypoints in scan order to raw_out [n][cap]; kps / desc unused)
+int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
+                        uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts, pano_kp *raw_out) {
     const int n = ctx->n, no = ctx->n_oct, nl = ctx->n_lvl, ni = p->num_intervals;
-    if (cap <= 0 || !kps || !counts || (!desc && !(desc_u8 && norms)))
+    if (cap <= 0 || !counts || (!raw_out && (!kps || (!desc && !(desc_u8 && norms)))))
         return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
     if (n > PANO_MAX_FRAMES) return pano_fail(ctx, PANO_E_ARG, "pano_sift: more than PANO_MAX_FRAMES frames");
     // per-frame candidate / raw capacities, scaled with the pyramid (see kExtMin)
@@ -1592,6 +1655,7 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
     sift_join_tail(ctx);                  // orientation / descriptors read every octave
     PyrArgs pa{};
     pa.n_oct = no;
+    pa.n_lvl = nl;
     for (int o = 0; o < no; ++o) {
         pa.H[o] = ctx->oct_h[o];
         pa.W[o] = ctx->oct_w[o];
@@ -1625,6 +1689,16 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         }
         PANO_LAUNCH_CHECK(ctx, "orientation");
     }
+    if (raw_out) {
+        dim3 grid((unsigned)((raw_cap + 255) / 256), n);
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            raw_scan_order<<<grid, 256, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, raw_out, cap, counts, err,
+                                                          ext_cnt, (int)ext_cap, cand_cnt, (int)cand_cap);
+        }
+        PANO_LAUNCH_CHECK(ctx, "raw_scan_order");
+        return PANO_OK;
+    }
     {
         dim3 grid((unsigned)((raw_cap + 255) / 256), n);
         if (nb > kSortMaxBuckets) return pano_fail(ctx, PANO_E_UNSUPPORTED, "frame too wide for the keypoint sort");
@@ -1647,33 +1721,75 @@ int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps
         }
         PANO_LAUNCH_CHECK(ctx, "emit_keypoints");
     }
-    {
-        DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
-        // persistent waves over the batch's keypoints: exactly the workgroups that are
-        // resident at once (a second partial round would leave the first round's CUs idle)
-        static int resident = 0;
-        if (!resident) {
-            int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, descriptor_wave<true>, 64 * kDescWaves, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
-                per_cu <= 0 || cus <= 0)
-                per_cu = 4, cus = 256;
-            resident = per_cu * cus;
-        }
-        const size_t slots = ((size_t)n * cap + kDescWaves - 1) / kDescWaves;
-        const unsigned blocks = (unsigned)std::min<size_t>((slots + 7) & ~size_t(7), (size_t)resident & ~size_t(7));
-        {
-            PanoProf prof_(ctx, PK_DESC);
-            if (desc_u8)
-                descriptor_wave<true><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
-                    pa, dp, kps, counts, n, cap, desc_work, nullptr, desc_u8, norms);
-            else
-                descriptor_wave<false><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
-                    pa, dp, kps, counts, n, cap, desc_work, desc, nullptr, nullptr);
-        }
-        PANO_LAUNCH_CHECK(ctx, "descriptor");
+    return launch_descriptors(ctx, p, pa, kps, counts, cap, desc_work, desc, desc_u8, norms);
+}
+
+// generate_descriptors over kps [n][cap] / counts [n] on the pyramid pa: persistent waves over
+// the batch's keypoints, exactly the workgroups that are resident at once (a second partial
+// round would leave the first round's CUs idle).  desc_work: 8 zeroed per-XCD queue counters.
+int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &pa, const pano_kp *kps,
+                       const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
+                       int32_t *norms) {
+    const int n = ctx->n;
+    DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
+    static int resident = 0;
+    if (!resident) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, descriptor_wave<true>, 64 * kDescWaves, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+            per_cu <= 0 || cus <= 0)
+            per_cu = 4, cus = 256;
+        resident = per_cu * cus;
     }
+    const size_t slots = ((size_t)n * cap + kDescWaves - 1) / kDescWaves;
+    const unsigned blocks = (unsigned)std::max<size_t>(
+        8, std::min<size_t>((slots + 7) & ~size_t(7), (size_t)resident & ~size_t(7)));
+    {
+        PanoProf prof_(ctx, PK_DESC);
+        if (desc_u8)
+            descriptor_wave<true><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                pa, dp, kps, counts, n, cap, desc_work, nullptr, desc_u8, norms);
+        else
+            descriptor_wave<false><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                pa, dp, kps, counts, n, cap, desc_work, desc, nullptr, nullptr);
+    }
+    PANO_LAUNCH_CHECK(ctx, "descriptor");
     return PANO_OK;
+}
+}  // namespace
+
+int launch_sift_keypoints(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
+                          uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts) {
+    return sift_keypoints_impl(ctx, p, kps, desc, desc_u8, norms, cap, counts, nullptr);
+}
+
+int launch_sift_extrema(pano_ctx *ctx, const pano_sift_params *p, pano_kp *raw, int cap, int32_t *counts) {
+    if (!raw) return pano_fail(ctx, PANO_E_ARG, "pano_sift_extrema: bad outputs");
+    return sift_keypoints_impl(ctx, p, nullptr, nullptr, nullptr, nullptr, cap, counts, raw);
+}
+
+int launch_sift_describe(pano_ctx *ctx, const pano_sift_params *p, const pano_kp *kps, const int32_t *counts,
+                         int cap, float *desc) {
+    if (!kps || !counts || !desc || cap <= 0) return pano_fail(ctx, PANO_E_ARG, "pano_sift_describe: bad arguments");
+    if (!ctx->pyr || ctx->n <= 0) return pano_fail(ctx, PANO_E_ARG, "pano_sift_describe: no resident pyramid");
+    if (!ctx->pyr_full)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_describe needs every Gaussian level (pano_sift_pyramid)");
+    sift_join_tail(ctx);
+    const size_t cnt_ints = (3 * (size_t)ctx->n + 1 + 16) * kCntStride;
+    int rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, cnt_ints * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *desc_work = ctx->counters + (3 * (size_t)ctx->n + 1) * kCntStride;
+    rc = launch_fill(ctx, desc_work, 0, 8 * kCntStride * sizeof(int32_t));
+    if (rc) return rc;
+    PyrArgs pa{};
+    pa.n_oct = ctx->n_oct;
+    pa.n_lvl = ctx->n_lvl;
+    for (int o = 0; o < ctx->n_oct; ++o) {
+        pa.H[o] = ctx->oct_h[o];
+        pa.W[o] = ctx->oct_w[o];
+        for (int l = 0; l < ctx->n_lvl; ++l) pa.gauss[o][l] = ctx->pyr + ctx->gauss_off[o][l];
+    }
+    return launch_descriptors(ctx, p, pa, kps, counts, cap, desc_work, desc, nullptr, nullptr);
 }
 
 int sift_set_attributes(pano_ctx *) { return PANO_OK; }

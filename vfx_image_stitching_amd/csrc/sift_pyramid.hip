@@ -11,10 +11,14 @@
 // octave for level 1 of octave o>0, plain for the rest), runs the row pass into a second
 // LDS tile and the column pass to HBM, writing the DoG level in the same epilogue.
 //
-// Exactness (oracle/cv2_compat.py): taps are float32, pixels float32, so each
-// product is exact in double; acc = fma(tap_i, x_i, acc) in tap order i = 0..n-1 is
-// therefore bit-identical to the oracle's sequential double sum, and one rounding to f32
-// per pass reproduces it exactly.  The x2 bilinear upsample of integer gray levels is exact.
+// Exactness (oracle/cv2_compat.py, oracle/cv_blur.c): the arithmetic is OpenCV
+// 4.x's float32 separable filter, which the author's published SIFT panoramas pin (grail
+// pixel-identical).  Taps are getGaussianKernelBitExact's, cast to f32.  Row pass
+// (RowVec_32f): s = x0*k0, then s = fma(x_i, k_i, s) for i = 1..n-1 in f32.  Column pass
+// (SymmColumnVec_32f): s = S0*kc, then s = fma(S[+i] + S[-i], k_i, s) for i = 1..r outward,
+// the pair sum rounded to f32 first.  One rounding per operation, so any thread / tile /
+// register mapping that keeps this per-output operation order is bit-identical.  The x2
+// bilinear upsample of integer gray levels is exact.
 #include "pano_internal.h"
 
 #include <algorithm>
@@ -27,14 +31,15 @@ constexpr int TY = 64;
 constexpr int TXP = TX + 1;   // odd trow pitch: row-pass stores are conflict-free
 
 struct Taps {
-    double k[PANO_MAX_TAPS];
+    float k[PANO_MAX_TAPS];
     int n;
 };
 
-enum Mode { MODE_BASE = 0, MODE_LEVEL = 1, MODE_DOWN = 2 };
+enum Mode { MODE_BASE = 0, MODE_LEVEL = 1, MODE_DOWN = 2, MODE_BASEF = 3 };   // BASEF: f32 gray input
 
 struct LoadArgs {
     const uint8_t *gray;  // MODE_BASE: [n][sh][sw] u8 gray (cvtColor BGR2GRAY)
+    const float *grayf;   // MODE_BASEF: [n][sh][sw] f32 gray (generate_base_image on any f32 image)
     const float *src;     // MODE_LEVEL: [n][H][W]; MODE_DOWN: [n][sh][sw]
     int sh, sw;           // source size (BASE: gray size; DOWN: previous octave size)
     double ifx, ify;      // DOWN: 1 / (dst / src), OpenCV resizeNN
@@ -115,6 +120,31 @@ template <> struct Stager<MODE_BASE> {    // gray (u8) -> x2 INTER_LINEAR, exact
         const float wx0 = 1.0f - c.w1;
         const float h0 = g00 * wx0 + g01 * c.w1;
         const float h1 = g10 * wx0 + g11 * c.w1;
+        return h0 * (1.0f - wy) + h1 * wy;
+    }
+};
+
+// f32 gray -> x2 INTER_LINEAR (the stage function generate_base_image on a caller's f32
+// image): the same expression as Stager<MODE_BASE>; exact for integer-valued inputs, the
+// reference's OpenCV rounding otherwise unpinned.
+template <> struct Stager<MODE_BASEF> {
+    const float *fr;
+    int W, H, sh, sw;
+    __device__ Stager(const LoadArgs &a, int f, int H_, int W_)
+        : fr(a.grayf + (size_t)f * a.sh * a.sw), W(W_), H(H_), sh(a.sh), sw(a.sw) {}
+    __device__ __forceinline__ ColMap col(int x) const {
+        ColMap c;
+        lin_map(reflect_fast(x, W), sw, c.c0, c.c1, c.w1);
+        return c;
+    }
+    __device__ __forceinline__ float get(int y, const ColMap &c) const {
+        int y0, y1;
+        float wy;
+        lin_map(reflect_fast(y, H), sh, y0, y1, wy);
+        const float *r0 = fr + (size_t)y0 * sw, *r1 = fr + (size_t)y1 * sw;
+        const float wx0 = 1.0f - c.w1;
+        const float h0 = r0[c.c0] * wx0 + r0[c.c1] * c.w1;
+        const float h1 = r1[c.c0] * wx0 + r1[c.c1] * c.w1;
         return h0 * (1.0f - wy) + h1 * wy;
     }
 };
@@ -263,41 +293,58 @@ gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t 
     }
 }
 
-// Register-blocked sliding window: SEG consecutive outputs of one row (or column) from
-// SEG + NT - 1 staged inputs; output j receives taps t = 0..NT-1 in order (the oracle's
-// sequential sum), all index arithmetic compile-time after unrolling.
+// Register-blocked passes: SEG consecutive outputs of one row (or column) from SEG + NT - 1
+// staged inputs, all index arithmetic compile-time after unrolling.
 #ifndef PANO_TAIL_SYNC
 #define PANO_TAIL_SYNC 0    // 1: full __syncthreads in blur_tail (A/B of lds_barrier)
 #endif
 #ifndef PANO_BLUR_ABL
-#define PANO_BLUR_ABL 0     // timing ablations of blur_fast only: bit 1 no FMAs, 2 no stores, 4 no loads
+#define PANO_BLUR_ABL 0     // timing ablations of blur_fast only: bit 2 no stores, 4 no loads
 #endif
+// Row pass, RowVec_32f: output j takes taps t = 0..NT-1 in order, the first as a product.
 template <int NT, int SEG>
-__device__ __forceinline__ void conv_seg(const float *__restrict__ p, int stride,
-                                         const double *__restrict__ k, double (&acc)[SEG]) {
-#pragma unroll
-    for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
-    if constexpr ((PANO_BLUR_ABL & 1) != 0) {
-#pragma unroll
-        for (int j = 0; j < SEG; ++j) acc[j] = (double)p[(j + NT / 2) * stride];
-        return;
-    }
+__device__ __forceinline__ void row_seg(const float *__restrict__ p, const float *__restrict__ k,
+                                        float (&acc)[SEG]) {
 #pragma unroll
     for (int i = 0; i < SEG + NT - 1; ++i) {
-        const double v = (double)p[i * stride];
+        const float v = p[i];
 #pragma unroll
         for (int j = 0; j < SEG; ++j) {
             const int t = i - j;
-            if (t >= 0 && t < NT) acc[j] = fma(k[t], v, acc[j]);
+            if (t == 0) acc[j] = v * k[0];
+            else if (t > 0 && t < NT) acc[j] = __builtin_fmaf(v, k[t], acc[j]);
         }
     }
 }
 
+// Column pass, SymmColumnVec_32f: output j = centre product, then the pairs at distance
+// d = 1..R outward, each pair summed in f32 before its fused multiply-add.
+template <int NT, int SEG>
+__device__ __forceinline__ void col_seg(const float *__restrict__ p, int stride, const float *__restrict__ k,
+                                        float (&acc)[SEG]) {
+    constexpr int R = (NT - 1) / 2;
+    float v[SEG + NT - 1];
+#pragma unroll
+    for (int i = 0; i < SEG + NT - 1; ++i) v[i] = p[i * stride];
+#pragma unroll
+    for (int j = 0; j < SEG; ++j) acc[j] = v[j + R] * k[R];
+#pragma unroll
+    for (int d = 1; d <= R; ++d)
+#pragma unroll
+        for (int j = 0; j < SEG; ++j) acc[j] = __builtin_fmaf(v[j + R + d] + v[j + R - d], k[R + d], acc[j]);
+}
+
 // Runtime tap count fallback (sigma values other than the reference defaults).
-__device__ __forceinline__ double conv_one(const float *__restrict__ p, int stride,
-                                           const double *__restrict__ k, int n) {
-    double acc = 0.0;
-    for (int t = 0; t < n; ++t) acc = fma(k[t], (double)p[t * stride], acc);
+__device__ __forceinline__ float row_one(const float *__restrict__ p, const float *__restrict__ k, int n) {
+    float acc = p[0] * k[0];
+    for (int t = 1; t < n; ++t) acc = __builtin_fmaf(p[t], k[t], acc);
+    return acc;
+}
+__device__ __forceinline__ float col_one(const float *__restrict__ p, int stride, const float *__restrict__ k,
+                                         int n) {
+    const int r = (n - 1) / 2;
+    float acc = p[r * stride] * k[r];
+    for (int d = 1; d <= r; ++d) acc = __builtin_fmaf(p[(r + d) * stride] + p[(r - d) * stride], k[r + d], acc);
     return acc;
 }
 
@@ -329,23 +376,23 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         const int nseg = (tw + SEG - 1) / SEG;
         for (int it = tid; it < ih * nseg; it += 256) {
             const int row = it % ih, sg = it / ih;
-            double acc[SEG];
-            conv_seg<NT, SEG>(tin + row * IWP + sg * SEG, 1, taps.k, acc);
+            float acc[SEG];
+            row_seg<NT, SEG>(tin + row * IWP + sg * SEG, taps.k, acc);
 #pragma unroll
-            for (int j = 0; j < SEG; ++j) trow[row * TXP + sg * SEG + j] = (float)acc[j];
+            for (int j = 0; j < SEG; ++j) trow[row * TXP + sg * SEG + j] = acc[j];
         }
         __syncthreads();
         // column pass: lanes walk consecutive columns, each SEG outputs down y
         const int nrs = (th + SEG - 1) / SEG;
         for (int it = tid; it < tw * nrs; it += 256) {
             const int x = it % tw, rs = it / tw;
-            double acc[SEG];
-            conv_seg<NT, SEG>(trow + rs * SEG * TXP + x, TXP, taps.k, acc);
+            float acc[SEG];
+            col_seg<NT, SEG>(trow + rs * SEG * TXP + x, TXP, taps.k, acc);
 #pragma unroll
             for (int j = 0; j < SEG; ++j) {
                 const int ty = rs * SEG + j;
                 if (ty >= th) break;
-                const float o = (float)acc[j];
+                const float o = acc[j];
                 const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + x;
                 if (out) out[gi] = o;
                 const float c = tin[(ty + r) * IWP + x + r];
@@ -356,12 +403,12 @@ blur_level(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     } else {
         for (int i = tid; i < ih * tw; i += 256) {
             const int ty = i / tw, tx = i - ty * tw;
-            trow[ty * TXP + tx] = (float)conv_one(tin + ty * IWP + tx, 1, taps.k, n);
+            trow[ty * TXP + tx] = row_one(tin + ty * IWP + tx, taps.k, n);
         }
         __syncthreads();
         for (int i = tid; i < th * tw; i += 256) {
             const int ty = i / tw, tx = i - ty * tw;
-            const float o = (float)conv_one(trow + ty * TXP + tx, TXP, taps.k, n);
+            const float o = col_one(trow + ty * TXP + tx, TXP, taps.k, n);
             const size_t gi = ((size_t)f * H + y0 + ty) * W + x0 + tx;
             if (out) out[gi] = o;
             const float c = tin[(ty + r) * IWP + tx + r];
@@ -393,7 +440,7 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     constexpr int R = (NT - 1) / 2;
     constexpr int IWP = (TXT + 2 * R) | 1;
     constexpr int SR = TXT == 64 ? 16 : 8, SC = TYT * TXT / NTHR;
-    constexpr bool CENTER = MODE != MODE_BASE;
+    constexpr bool CENTER = MODE != MODE_BASE && MODE != MODE_BASEF;
     static_assert((TYT + 2 * R) * (TXT / SR) <= NTHR && TXT * (TYT / SC) <= NTHR && TYT % SC == 0,
                   "one item per thread");
     extern __shared__ __attribute__((aligned(16))) float tin[];   // [TYT + 2R][IWP]
@@ -429,10 +476,10 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     const int row = roww ? tid % ih : 0, sg = roww ? tid / ih : 0;
     float ro[SR];
     if (roww) {
-        double acc[SR];
-        conv_seg<NT, SR>(tin + row * IWP + sg * SR, 1, taps.k, acc);
+        float acc[SR];
+        row_seg<NT, SR>(tin + row * IWP + sg * SR, taps.k, acc);
 #pragma unroll
-        for (int j = 0; j < SR; ++j) ro[j] = (float)acc[j];
+        for (int j = 0; j < SR; ++j) ro[j] = acc[j];
     }
     __syncthreads();
     if (roww) {
@@ -444,12 +491,12 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
     // all SC outputs first (the sliding window interleaves their FMA chains), then predicated
     // stores: an early exit in the store loop let the compiler compute one output at a time,
     // a dependent chain of NT FMAs each
-    double acc[SC];
-    conv_seg<NT, SC>(tin + crs * SC * IWP + cxp, IWP, taps.k, acc);
+    float acc[SC];
+    col_seg<NT, SC>(tin + crs * SC * IWP + cxp, IWP, taps.k, acc);
     float o[SC];
 #pragma unroll
     for (int j = 0; j < SC; ++j) {
-        o[j] = (float)acc[j];
+        o[j] = acc[j];
         asm volatile("" ::"v"(o[j]));                           // no sinking into the stores' branches
     }
     const int nvalid = th - crs * SC;                           // rows of this item inside the plane
@@ -520,10 +567,10 @@ blur_pair(LoadArgs la, float *__restrict__ out1, float *__restrict__ dog1, float
         const int nseg = (ow1 + SG - 1) / SG;
         for (int it = tid; it < ih * nseg; it += NTHR) {
             const int row = it % ih, sg = it / ih;
-            double acc[SG];
-            conv_seg<NT1, SG>(tin + row * IWP + sg * SG, 1, t1.k, acc);
+            float acc[SG];
+            row_seg<NT1, SG>(tin + row * IWP + sg * SG, t1.k, acc);
 #pragma unroll
-            for (int j = 0; j < SG; ++j) rb[row * RP + sg * SG + j] = (float)acc[j];
+            for (int j = 0; j < SG; ++j) rb[row * RP + sg * SG + j] = acc[j];
         }
     }
     __syncthreads();
@@ -532,11 +579,11 @@ blur_pair(LoadArgs la, float *__restrict__ out1, float *__restrict__ dog1, float
         const int nrs = (oh1 + SG - 1) / SG;
         for (int it = tid; it < ow1 * nrs; it += NTHR) {
             const int c = it % ow1, rs = it / ow1;
-            double acc[SG];
-            conv_seg<NT1, SG>(rb + rs * SG * RP + c, RP, t1.k, acc);
+            float acc[SG];
+            col_seg<NT1, SG>(rb + rs * SG * RP + c, RP, t1.k, acc);
 #pragma unroll
             for (int j = 0; j < SG; ++j)
-                if (rs * SG + j < oh1) tin[(rs * SG + j) * IWP + c] = (float)acc[j];
+                if (rs * SG + j < oh1) tin[(rs * SG + j) * IWP + c] = acc[j];
         }
     }
     __syncthreads();
@@ -567,10 +614,10 @@ blur_pair(LoadArgs la, float *__restrict__ out1, float *__restrict__ dog1, float
         const int nseg = (tw + SG - 1) / SG;
         for (int it = tid; it < oh1 * nseg; it += NTHR) {
             const int row = it % oh1, sg = it / oh1;
-            double acc[SG];
-            conv_seg<NT2, SG>(tin + row * IWP + sg * SG, 1, t2.k, acc);
+            float acc[SG];
+            row_seg<NT2, SG>(tin + row * IWP + sg * SG, t2.k, acc);
 #pragma unroll
-            for (int j = 0; j < SG; ++j) rb[row * RP + sg * SG + j] = (float)acc[j];
+            for (int j = 0; j < SG; ++j) rb[row * RP + sg * SG + j] = acc[j];
         }
     }
     __syncthreads();
@@ -579,13 +626,13 @@ blur_pair(LoadArgs la, float *__restrict__ out1, float *__restrict__ dog1, float
         const int nrs = (th + SG - 1) / SG;
         for (int it = tid; it < tw * nrs; it += NTHR) {
             const int x = it % tw, rs = it / tw;
-            double acc[SG];
-            conv_seg<NT2, SG>(rb + rs * SG * RP + x, RP, t2.k, acc);
+            float acc[SG];
+            col_seg<NT2, SG>(rb + rs * SG * RP + x, RP, t2.k, acc);
 #pragma unroll
             for (int j = 0; j < SG; ++j) {
                 const int y = rs * SG + j;
                 if (y >= th) break;
-                const float g = (float)acc[j];
+                const float g = acc[j];
                 const size_t gi = ((size_t)f * H + y0 + y) * W + x0 + x;
                 if (out2) out2[gi] = g;
                 dog2[gi] = g - side[y * SP + x];
@@ -624,7 +671,7 @@ struct TailArgs {
     int H[kTailOct], W[kTailOct];
     int n_oct, n_lvl;
     int full;                                   // write level 0 and the top level too
-    const double *taps;                         // [n_lvl][PANO_MAX_TAPS], level 0 unused
+    const float *taps;                          // [n_lvl][PANO_MAX_TAPS], level 0 unused
     int ntap[PANO_MAX_LEVELS];
 };
 
@@ -659,31 +706,30 @@ constexpr int kRowtRows = kTailDim + 8 + 2 * kRMax;
 
 template <int NT>
 __device__ __forceinline__ void tail_level(const float *in, float *outb, float *pad, float *rowt, int H,
-                                           int W, const double *__restrict__ taps_g, int n_rt, float *g,
+                                           int W, const float *__restrict__ taps_g, int n_rt, float *g,
                                            float *d, int tid) {
     constexpr int SG = 8;
     const int n = NT > 0 ? NT : n_rt;
     const int R = (n - 1) / 2;
-    double k[NT > 0 ? NT : 1];
+    float k[NT > 0 ? NT : 1];
     if constexpr (NT > 0) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) k[t] = taps_g[t];
     }
-    auto tap = [&](int t) -> double { if constexpr (NT > 0) return k[t]; else return taps_g[t]; };
-    auto conv = [&](const float *p, int stride, double (&acc)[SG]) {
+    auto row = [&](const float *p, float (&acc)[SG]) {
         if constexpr (NT > 0) {
-            conv_seg<NT, SG>(p, stride, k, acc);
+            row_seg<NT, SG>(p, k, acc);
         } else {
 #pragma unroll
-            for (int j = 0; j < SG; ++j) acc[j] = 0.0;
-            for (int i = 0; i < SG + n - 1; ++i) {
-                const double v = (double)p[i * stride];
+            for (int j = 0; j < SG; ++j) acc[j] = row_one(p + j, taps_g, n);
+        }
+    };
+    auto col = [&](const float *p, int stride, float (&acc)[SG]) {
+        if constexpr (NT > 0) {
+            col_seg<NT, SG>(p, stride, k, acc);
+        } else {
 #pragma unroll
-                for (int j = 0; j < SG; ++j) {
-                    const int t = i - j;
-                    if (t >= 0 && t < n) acc[j] = fma(tap(t), v, acc[j]);
-                }
-            }
+            for (int j = 0; j < SG; ++j) acc[j] = col_one(p + j * stride, stride, taps_g, n);
         }
     };
     // reflected columns
@@ -697,11 +743,11 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
     const int nseg = (W + SG - 1) / SG;
     for (int it = tid; it < H * nseg; it += kTailThreads) {
         const int y = it % H, x0 = (it / H) * SG;
-        double acc[SG];
-        conv(pad + y * kPP + x0, 1, acc);
+        float acc[SG];
+        row(pad + y * kPP + x0, acc);
 #pragma unroll
         for (int j = 0; j < SG; ++j)
-            if (x0 + j < W) rowt[(y + R) * kTP + x0 + j] = (float)acc[j];
+            if (x0 + j < W) rowt[(y + R) * kTP + x0 + j] = acc[j];
     }
     lds_barrier();
     // reflected rows of the row-pass output
@@ -715,13 +761,13 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
     const int nrs = (H + SG - 1) / SG;
     for (int it = tid; it < W * nrs; it += kTailThreads) {
         const int x = it % W, y0 = (it / W) * SG;
-        double acc[SG];
-        conv(rowt + y0 * kTP + x, kTP, acc);
+        float acc[SG];
+        col(rowt + y0 * kTP + x, kTP, acc);
 #pragma unroll
         for (int j = 0; j < SG; ++j) {
             const int y = y0 + j;
             if (y >= H) break;
-            const float o = (float)acc[j];
+            const float o = acc[j];
             outb[y * kTP + x] = o;
             if (g) g[y * W + x] = o;
             d[y * W + x] = o - in[y * kTP + x];
@@ -731,7 +777,7 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
 
 __global__ void __launch_bounds__(kTailThreads)
 blur_tail(TailArgs ta) {
-    __shared__ double taps_s[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // every level's taps, loaded once
+    __shared__ float taps_s[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // every level's taps, loaded once
     __shared__ float lv[3][kTailDim * kTP];      // current / next level, octave seed
     __shared__ float pad[kTailDim * kPP];         // level with reflected columns
     __shared__ float rowt[kRowtRows * kTP];       // row-pass output with reflected rows
@@ -772,7 +818,7 @@ blur_tail(TailArgs ta) {
             while (out == cur || out == keep) ++out;
             float *g = (ta.full || l < ta.n_lvl - 1) ? ta.G[oi][l] + (size_t)f * H * W : nullptr;
             float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
-            const double *tg = taps_s + l * PANO_MAX_TAPS;
+            const float *tg = taps_s + l * PANO_MAX_TAPS;
             switch (n) {   // the reference's kernel sizes; others take the runtime-count path
                 case 11: tail_level<11>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
                 case 13: tail_level<13>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
@@ -788,23 +834,33 @@ blur_tail(TailArgs ta) {
     }
 }
 
-// getGaussianKernel(ksize, sigma, CV_32F) (cv2_compat.getGaussianKernel): f32 taps widened.
+// getGaussianKernel(ksize, sigma, CV_32F) of OpenCV 4.x = getGaussianKernelBitExact cast to
+// f32 (cv2_compat.getGaussianKernelBitExact): exp(x*x * (-0.125 / s^2)) for the integer
+// x = 1-n, 3-n, ... (twice the offset), sum = 2 * sum(side taps) + 1, every tap times 1 / sum,
+// the centre tap 1 / sum itself.  ksize = cvRound(8 s + 1) | 1 (float images).
 Taps make_taps(double sigma) {
     Taps t;
     int n = (int)nearbyint(sigma * 4 * 2 + 1) | 1;
     if (n > PANO_MAX_TAPS) n = -1;
     t.n = n;
     if (n < 0) return t;
-    const double scale2x = -0.5 / (sigma * sigma);
-    float tf[PANO_MAX_TAPS];
+    const double scale2x = -0.125 / (sigma * sigma);
+    const int n2 = (n - 1) / 2;
+    double vals[PANO_MAX_TAPS];
     double s = 0.0;
-    for (int i = 0; i < n; ++i) {
-        const double x = i - (n - 1) * 0.5;
-        tf[i] = (float)exp(scale2x * x * x);
-        s += (double)tf[i];
+    for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
+        vals[i] = exp((double)(x * x) * scale2x);
+        s += vals[i];
     }
-    s = 1.0 / s;
-    for (int i = 0; i < n; ++i) t.k[i] = (double)(float)((double)tf[i] * s);
+    s *= 2.0;
+    s += 1.0;
+    const double mul1 = 1.0 / s;
+    t.k[n2] = (float)mul1;
+    for (int i = 0; i < n2; ++i) {
+        const double v = vals[i] * mul1;
+        t.k[i] = (float)v;
+        t.k[n - 1 - i] = (float)v;
+    }
     return t;
 }
 
@@ -971,13 +1027,11 @@ extern "C" int pano_sift_taps(double sigma, double *out, int *n) {
     return PANO_OK;
 }
 
-int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p) {
-    int no, nl;
-    double sb, sl[PANO_MAX_LEVELS];
-    int rc = sift_plan(p, h, w, &no, &nl, &sb, sl);
-    if (rc) return pano_fail(ctx, rc, "unsupported SIFT parameters");
+// Lay out the pyramid of n frames whose octave 0 is H0 x W0 (the 2x base), at most max_oct
+// octaves (fewer when a plane would shrink below 1 px), nl Gaussian levels per octave.
+int sift_reserve_dims(pano_ctx *ctx, int n, int H0, int W0, int max_oct, int nl) {
     size_t goff = 0, doff = 0;
-    int oh = 2 * h, ow = 2 * w;
+    int oh = H0, ow = W0, no = std::min(std::max(max_oct, 1), PANO_MAX_OCTAVES);
     for (int o = 0; o < no; ++o) {
         ctx->oct_h[o] = oh;
         ctx->oct_w[o] = ow;
@@ -1003,19 +1057,33 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
     }
     ctx->dog = ctx->pyr + goff;
     ctx->n = n;
-    ctx->h = h;
-    ctx->w = w;
+    ctx->h = (H0 + 1) / 2;
+    ctx->w = (W0 + 1) / 2;
     return PANO_OK;
 }
 
-int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
-                        const pano_sift_params *p, bool defer_tail, bool full) {
-    sift_join_tail(ctx);                  // a previous call's tail must finish first
+int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p) {
     int no, nl;
     double sb, sl[PANO_MAX_LEVELS];
     int rc = sift_plan(p, h, w, &no, &nl, &sb, sl);
     if (rc) return pano_fail(ctx, rc, "unsupported SIFT parameters");
-    rc = sift_reserve_pyramid(ctx, n, h, w, p);
+    return sift_reserve_dims(ctx, n, 2 * h, 2 * w, no, nl);
+}
+
+// The pyramid from one of three sources (PyrSource): BGR u8 frames (gray + x2 + base blur:
+// compute_keypoints_and_descriptors), f32 gray frames (generate_base_image on a caller's
+// image) or a caller's f32 base (generate_gaussian_images on any base: copied to level 0 of
+// octave 0).  n frames; h x w is the gray size, H0 x W0 = 2h x 2w the base size (base source:
+// the caller's base size, octave count capped at max_oct).
+int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, int w,
+                            const pano_sift_params *p, bool defer_tail, bool full) {
+    sift_join_tail(ctx);                  // a previous call's tail must finish first
+    int no, nl;
+    double sb, sl[PANO_MAX_LEVELS];
+    const int gh = src.base ? std::max(1, h / 2) : h, gw = src.base ? std::max(1, w / 2) : w;
+    int rc = sift_plan(p, gh, gw, &no, &nl, &sb, sl);
+    if (rc) return pano_fail(ctx, rc, "unsupported SIFT parameters");
+    rc = src.base ? sift_reserve_dims(ctx, n, h, w, src.max_oct, nl) : sift_reserve_pyramid(ctx, n, h, w, p);
     if (rc) return rc;
     no = ctx->n_oct;
     Taps tb = make_taps(sb);
@@ -1025,25 +1093,30 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     for (int l = 1; l < nl; ++l)
         if (tl[l].n < 0) return pano_fail(ctx, PANO_E_UNSUPPORTED, "Gaussian kernel too wide");
     float *G = ctx->pyr, *D = ctx->dog;
-    // gray frames (u8) for the base image
-    {
+    if (src.base) {
+        // generate_gaussian_images(base, ...): the caller's base is level 0 of octave 0
+        PANO_HIP(ctx, hipMemcpyAsync(G + ctx->gauss_off[0][0], src.base,
+                                     (size_t)n * ctx->oct_h[0] * ctx->oct_w[0] * sizeof(float),
+                                     hipMemcpyDeviceToDevice, ctx->stream));
+    } else if (src.grayf) {
+        LoadArgs la{};
+        la.grayf = src.grayf;
+        la.sh = h;
+        la.sw = w;
+        rc = launch_blur<MODE_BASEF>(ctx, la, G + ctx->gauss_off[0][0], nullptr, nullptr, n,
+                                     ctx->oct_h[0], ctx->oct_w[0], tb);
+        if (rc) return rc;
+    } else {
+        // gray frames (u8) for the base image
         const size_t npx = (size_t)n * h * w;
         rc = pano_grow(ctx, (void **)&ctx->gray, &ctx->gray_bytes, npx + 16);
         if (rc) return rc;
         const unsigned blocks = (unsigned)((npx + 1023) / 1024);
         {
             PanoProf prof_(ctx, PK_BLUR);
-            gray_frames<<<blocks, 256, 0, ctx->stream>>>(bgr, ctx->gray, npx);
+            gray_frames<<<blocks, 256, 0, ctx->stream>>>(src.bgr, ctx->gray, npx);
         }
         PANO_LAUNCH_CHECK(ctx, "gray_frames");
-    }
-    // first octave of the fused small-octave tail (every level fits one 64 x 64 tile)
-    int o_tail = no;
-    for (int o = 1; o < no; ++o)
-        if (ctx->oct_h[o] <= kTailDim && ctx->oct_w[o] <= kTailDim) { o_tail = o; break; }
-    if (no - o_tail > kTailOct) o_tail = no - kTailOct;
-    // octave 0, level 0: base image
-    {
         LoadArgs la{};
         la.gray = ctx->gray;
         la.sh = h;
@@ -1052,6 +1125,15 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                                     ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
     }
+    if (src.base_only) {
+        ctx->pyr_full = false;
+        return PANO_OK;
+    }
+    // first octave of the fused small-octave tail (every level fits one 64 x 64 tile)
+    int o_tail = no;
+    for (int o = 1; o < no; ++o)
+        if (ctx->oct_h[o] <= kTailDim && ctx->oct_w[o] <= kTailDim) { o_tail = o; break; }
+    if (no - o_tail > kTailOct) o_tail = no - kTailOct;
     // The small octaves run on a high-priority side stream, beside the main stream's last
     // large-octave levels and extrema scan: the last o_tail - o_side blur_fast octaves (their
     // launches are one workgroup's latency each) and then the fused tail (octaves <= 64 x 64,
@@ -1077,7 +1159,7 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     };
     auto launch_tail = [&]() -> int {
         // device copy of the level taps (uploaded only when they change)
-        double th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
+        float th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
         TailArgs ta{};
         for (int l = 1; l < nl; ++l) {
             for (int t = 0; t < tl[l].n; ++t) th[l * PANO_MAX_TAPS + t] = tl[l].k[t];
@@ -1197,5 +1279,36 @@ int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     }
     if (o_tail < no && !defer_tail) sift_join_tail(ctx);
     ctx->pyr_full = full;
+    return PANO_OK;
+}
+
+int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
+                        const pano_sift_params *p, bool defer_tail, bool full) {
+    PyrSource src{};
+    src.bgr = bgr;
+    return launch_sift_pyramid_src(ctx, src, n, h, w, p, defer_tail, full);
+}
+
+// ------------------------------------------------------------------ stage access
+// generate_DoG_images (sift_impl.py:100-111) over the resident Gaussian levels: DoG[o][l] =
+// G[o][l+1] - G[o][l] in f32, every octave and level of the batch.
+__global__ void __launch_bounds__(256)
+dog_from_levels(const float *__restrict__ g0, const float *__restrict__ g1, float *__restrict__ d, size_t npx) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < npx; i += (size_t)gridDim.x * 256)
+        d[i] = g1[i] - g0[i];
+}
+
+int launch_sift_dog(pano_ctx *ctx) {
+    if (!ctx->pyr || ctx->n_oct <= 0) return pano_fail(ctx, PANO_E_ARG, "pano_sift_dog: no resident pyramid");
+    for (int o = 0; o < ctx->n_oct; ++o) {
+        const size_t npx = (size_t)ctx->n * ctx->oct_h[o] * ctx->oct_w[o];
+        const unsigned blocks = (unsigned)std::min<size_t>((npx + 255) / 256, 4096);
+        for (int l = 0; l + 1 < ctx->n_lvl; ++l) {
+            dog_from_levels<<<blocks, 256, 0, ctx->stream>>>(ctx->pyr + ctx->gauss_off[o][l],
+                                                             ctx->pyr + ctx->gauss_off[o][l + 1],
+                                                             ctx->dog + ctx->dog_off[o][l], npx);
+            PANO_LAUNCH_CHECK(ctx, "dog_from_levels");
+        }
+    }
     return PANO_OK;
 }

@@ -18,6 +18,8 @@ GPU work is the libpano calls of pipeline.Stitcher.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 from . import _lib
@@ -25,8 +27,15 @@ from ._lib import PanoError
 
 
 class BandError(PanoError):
-    def __init__(self, msg):
+    """The device plan refused this rank's band.  ``plan_status`` is the global plan's status
+    (PANO_OK when the global plan is fine and only the band split failed), ``band_status``
+    the band plan's; ``records`` the gathered pair records (for a host-planned fallback)."""
+
+    def __init__(self, msg, plan_status=_lib.PANO_OK, band_status=_lib.PANO_OK, records=None):
         super().__init__(_lib.PANO_E_UNSUPPORTED, msg)
+        self.plan_status = int(plan_status)
+        self.band_status = int(band_status)
+        self.records = records
 
 
 def shard_ranges(n_pairs: int, world: int):
@@ -327,10 +336,14 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
     gst = head[off_gp:off_gp + 32].view(np.int32)
     if gst[0] == _lib.PANO_E_NOMATCH:
         raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+    if gst[0] != _lib.PANO_OK:
+        raise BandError(f"global device plan status {int(gst[0])}: the canvas exceeds the capacity "
+                        f"({Hcap} rows) or a column is covered by three frames",
+                        plan_status=gst[0], band_status=band[0], records=recs)
     if band[0] != _lib.PANO_OK:
-        raise BandError(f"device band plan refused the band (status {int(band[0])}): columns "
-                        "covered by three frames, a non-contiguous band or a band wider than the "
-                        "canvas capacity")
+        raise BandError(f"band plan status {int(band[0])} for frames {f0}..{f0 + n_local - 1}: the "
+                        "owned columns are not contiguous or wider than the band capacity "
+                        f"({Wcap} columns)", plan_status=gst[0], band_status=band[0], records=recs)
     H, W, own_lo, own_hi = int(gst[1]), int(gst[2]), int(band[1]), int(band[2])
     bw = own_hi - own_lo
     view = canvas[:H * bw * 3].view(H, bw, 3)
@@ -357,9 +370,18 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
     pmax = max(pair_counts)
     block, cyl, colnz = rank_records(st, frames_dev, focals, pmax, graph)
     gathered = gather_blocks(block, group)
-    recs, owned, own_lo, (H, W), box = rank_band(st, cyl, colnz, gathered, pair_counts, pair_start,
-                                                 margin, graph)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    try:
+        recs, owned, own_lo, (H, W), box = rank_band(st, cyl, colnz, gathered, pair_counts,
+                                                     pair_start, margin, graph)
+    except BandError as e:
+        if world != 1:
+            raise
+        # one rank holds every frame: composite with the host plan, as Stitcher.run does when
+        # the device plan refuses (three frames over a column, a canvas above the capacity)
+        res = st._finish(cyl, colnz, e.records, margin, graph, {}, time.perf_counter())
+        return {"records": res.records, "band": res.canvas, "x_offset": 0,
+                "canvas_hw": tuple(res.canvas.shape[:2]), "bbox": res.bbox}
     g = box if world == 1 else global_bbox(torch.tensor(box, dtype=torch.int64, device=owned.device), group)
     if g[1] >= 0:
         y0, y1 = max(0, g[0] + margin), min(H - 1, g[1] - margin)

@@ -79,12 +79,13 @@ def find_pair_homographies(st, feats, pairs, ratio=0.7, reproj_thr=5.0,
     for p, (a, b) in enumerate(pairs):
         na, nb = min(max(int(cnt[a]), 0), cap), min(max(int(cnt[b]), 0), cap)
         bp, p1, p2 = best_h[p, :na], d1_h[p, :na].astype(np.float64), d2_h[p, :na].astype(np.float64)
-        # the kernel's predicate (pair_compact): a valid neighbour and d1 < ratio^2 d2
+        # the kernel's predicate (pair_compact): a valid neighbour and the visualiser's
+        # m.distance < ratio * n.distance on float32 L2 distances
         ok = (bp >= 0) & (bp < nb)
         if desc_thresh > 0:
             ok &= d1_h[p, :na] < np.float32(desc_thresh)
         if ratio > 0:
-            ok &= p1 < (ratio * ratio) * p2
+            ok &= np.sqrt(d1_h[p, :na]).astype(np.float64) < ratio * np.sqrt(d2_h[p, :na]).astype(np.float64)
         qi = np.nonzero(ok)[0]
         G = len(qi)
         if G != int(r["n_matches"][p]):

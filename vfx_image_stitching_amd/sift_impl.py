@@ -19,7 +19,6 @@ from .keypoint import KeyPoint, from_records
 float_tolerance = 1e-7
 
 _stitchers: dict = {}
-_last_pyramid: dict = {}
 
 
 def _stitcher(sigma, num_intervals, assumed_blur, border):
@@ -58,8 +57,6 @@ def compute_keypoints_and_descriptors(image, sigma=1.6, num_intervals=3, assumed
     st.ctx.sync()
     rec = kps[0, :n].cpu().numpy().view(_lib.KP_NP).reshape(-1)
     d = desc[0, :n].cpu().numpy().astype(np.float32)
-    _last_pyramid["key"] = (bgr.shape, sigma, num_intervals, assumed_blur)
-    _last_pyramid["stitcher"] = st
     return from_records(rec), d
 
 
@@ -122,82 +119,317 @@ def unpack_octave(keypoint):
     return octave, layer, scale
 
 
-# ------------------------------------------------------------------ pyramid stages (GUI)
-class _DevicePyramid:
-    """Pyramid levels of one image built by libpano, read back on demand."""
-
-    def __init__(self, image_u8, sigma, num_intervals, assumed_blur):
-        import ctypes
-        self.st = _stitcher(sigma, num_intervals, assumed_blur, 5)
-        self.bgr = _as_bgr_u8(image_u8)
-        dev = self.st.upload(self.bgr[None])
-        ctx = self.st.ctx
-        ctx.check(ctx.lib.pano_sift_pyramid(ctx.h, _lib.ptr(dev), 1, self.bgr.shape[0],
-                                            self.bgr.shape[1], ctypes.byref(self.st.params)))
-        self._dev = dev
-        self.levels = num_intervals + 3
-
-    def level(self, octave, level, dog=False):
-        import ctypes
-        ctx = self.st.ctx
-        h, w, no = (ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32())
-        ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, octave, ctypes.byref(h), ctypes.byref(w),
-                                                ctypes.byref(no)))
-        out = self.st.torch.empty((h.value, w.value), dtype=self.st.torch.float32,
-                                  device=self.st.device)
-        ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, 0, octave, level, int(dog), _lib.ptr(out)))
-        return out.cpu().numpy()
-
-    def n_octaves(self):
-        import ctypes
-        ctx = self.st.ctx
-        h, w, no = (ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32())
-        ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, 0, ctypes.byref(h), ctypes.byref(w),
-                                                ctypes.byref(no)))
-        return no.value
+# ------------------------------------------------------------------ stage functions (GUI)
+# sift_visualizeUI.py:104-115 calls the stages one by one with numpy arrays in between.  Each
+# stage here is a pure function of its arguments computed by libpano: its inputs go to the
+# device, the stage's kernels run there (the same kernels as compute_keypoints_and_descriptors),
+# and the outputs come back as the reference's types.  Pyramids are ``np.ndarray`` of dtype
+# object, shape (octaves, levels), like the reference's np.array(pyramid, dtype=object).
+def _dev():
+    import torch
+    ctx = _lib.context()
+    return ctx, torch, torch.device("cuda", ctx.device)
 
 
-class _BaseImage(np.ndarray):
-    """ndarray carrying the device pyramid it was read from (for the next stage call)."""
-    pyramid = None
+def _f32_2d(a, what):
+    a = np.asarray(a)
+    if a.ndim != 2:
+        raise ValueError(f"{what}: expected a single-channel 2-D image, got shape {a.shape}")
+    return np.ascontiguousarray(a, np.float32)
 
 
-def generate_base_image(image, sigma, assumed_blur):
-    if sigma is None:
-        sigma = 1.6
-    pyr = _DevicePyramid(image, sigma, 3, assumed_blur)
-    base = pyr.level(0, 0).view(_BaseImage)
-    base.pyramid = pyr
-    return base
+def _params(sigma=1.6, num_intervals=3, assumed_blur=0.5, border=5, contrast_threshold=0.04):
+    return _lib.default_sift_params(sigma=float(sigma), num_intervals=int(num_intervals),
+                                    assumed_blur=float(assumed_blur), border=int(border),
+                                    contrast_threshold=float(contrast_threshold))
 
 
-def generate_gaussian_images(image, num_octaves, gaussian_kernels):
-    pyr = getattr(image, "pyramid", None)
-    if pyr is None:
-        raise NotImplementedError("generate_gaussian_images needs the base from generate_base_image")
-    no = min(num_octaves, pyr.n_octaves())
-    out = np.empty((no, pyr.levels), dtype=object)
+def _pyramid_shapes(pyr, what):
+    """(octaves, levels) and the octave-0 shape of an object pyramid; every octave must halve
+    the previous one (floor), as generate_gaussian_images builds them."""
+    pyr = np.asarray(pyr, dtype=object)
+    if pyr.ndim != 2:
+        raise ValueError(f"{what}: expected an (octaves, levels) object array")
+    no, nl = pyr.shape
+    h, w = np.asarray(pyr[0, 0]).shape
     for o in range(no):
-        for l in range(pyr.levels):
-            out[o, l] = pyr.level(o, l)
-    _last_pyramid["gauss"] = (out, pyr)
+        for l in range(nl):
+            if np.asarray(pyr[o, l]).shape != (h, w):
+                raise ValueError(f"{what}: level ({o}, {l}) has shape {np.asarray(pyr[o, l]).shape}, "
+                                 f"expected {(h, w)}")
+        h, w = h // 2, w // 2
+    return pyr, no, nl
+
+
+def _upload_pyramid(gauss, dogs=None):
+    """Reserve a resident pyramid shaped like `gauss` and copy its levels (and `dogs`) in."""
+    ctx, torch, dev = _dev()
+    g, no, nl = _pyramid_shapes(gauss, "gaussian_images")
+    H0, W0 = np.asarray(g[0, 0]).shape
+    ctx.check(ctx.lib.pano_sift_reserve_levels(ctx.h, 1, H0, W0, no, nl))
+    keep = []
+    for o in range(no):
+        for l in range(nl):
+            t = torch.from_numpy(_f32_2d(g[o, l], "gaussian_images")).to(dev)
+            keep.append(t)
+            ctx.check(ctx.lib.pano_sift_set_level(ctx.h, 0, o, l, 0, _lib.ptr(t)))
+    if dogs is not None:
+        d = np.asarray(dogs, dtype=object)
+        if d.ndim != 2 or d.shape != (no, nl - 1):
+            raise ValueError(f"dog_images: expected shape {(no, nl - 1)}, got {d.shape}")
+        for o in range(no):
+            for l in range(nl - 1):
+                a = _f32_2d(d[o, l], "dog_images")
+                if a.shape != np.asarray(g[o, 0]).shape:
+                    raise ValueError(f"dog_images: level ({o}, {l}) shape {a.shape}")
+                t = torch.from_numpy(a).to(dev)
+                keep.append(t)
+                ctx.check(ctx.lib.pano_sift_set_level(ctx.h, 0, o, l, 1, _lib.ptr(t)))
+    torch.cuda.current_stream(dev).synchronize()      # the host tensors may go now
+    return ctx, no, nl
+
+
+def _read_levels(ctx, no, nl, dog):
+    import ctypes
+    _, torch, dev = _dev()
+    out = np.empty((no, nl), dtype=object)
+    for o in range(no):
+        h, w = ctypes.c_int32(), ctypes.c_int32()
+        ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(h), ctypes.byref(w), None))
+        for l in range(nl):
+            t = torch.empty((h.value, w.value), dtype=torch.float32, device=dev)
+            ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, 0, o, l, int(dog), _lib.ptr(t)))
+            out[o, l] = t.cpu().numpy()
     return out
 
 
+def generate_base_image(image, sigma, assumed_blur):
+    """sift_impl.py:45-56: x2 INTER_LINEAR + GaussianBlur(sigma_diff) of a gray f32 image
+    (pano_sift_base).  Exact for integer-valued gray levels (every reference caller's case)."""
+    import ctypes
+    if sigma is None:
+        sigma = 1.6
+    g = _f32_2d(image, "generate_base_image")
+    ctx, torch, dev = _dev()
+    src = torch.from_numpy(g).to(dev)
+    h, w = g.shape
+    out = torch.empty((2 * h, 2 * w), dtype=torch.float32, device=dev)
+    p = _params(sigma=sigma, assumed_blur=assumed_blur)
+    ctx.check(ctx.lib.pano_sift_base(ctx.h, _lib.ptr(src), 1, h, w, ctypes.byref(p), _lib.ptr(out)))
+    return out.cpu().numpy()
+
+
+def _kernel_params(gaussian_kernels):
+    """(sigma, num_intervals) of a generate_gaussian_kernels list; libpano derives the level
+    sigmas itself, so other lists are refused rather than silently replaced."""
+    k = np.asarray(gaussian_kernels, np.float64).ravel()
+    ni = len(k) - 3
+    if ni < 1 or not np.array_equal(k, generate_gaussian_kernels(float(k[0]), ni)):
+        raise NotImplementedError("gaussian_kernels must come from generate_gaussian_kernels(sigma, n)")
+    return float(k[0]), ni
+
+
+def generate_gaussian_images(image, num_octaves, gaussian_kernels):
+    """sift_impl.py:82-97 on any f32 base image (pano_sift_pyramid_base): per octave the
+    cascaded blurs of gaussian_kernels[1:], next base = INTER_NEAREST 1/2 of level -3."""
+    import ctypes
+    sigma, ni = _kernel_params(gaussian_kernels)
+    base = _f32_2d(image, "generate_gaussian_images")
+    ctx, torch, dev = _dev()
+    src = torch.from_numpy(base).to(dev)
+    H0, W0 = base.shape
+    p = _params(sigma=sigma, num_intervals=ni)
+    ctx.check(ctx.lib.pano_sift_pyramid_base(ctx.h, _lib.ptr(src), 1, H0, W0, int(num_octaves),
+                                             ctypes.byref(p)))
+    no = ctypes.c_int32()
+    ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, 0, None, None, ctypes.byref(no)))
+    return _read_levels(ctx, no.value, ni + 3, dog=False)
+
+
 def generate_DoG_images(gaussian_images):
-    ent = _last_pyramid.get("gauss")
-    if ent is None or ent[0] is not gaussian_images:
-        return np.array([[b - a for a, b in zip(o, o[1:])] for o in gaussian_images], dtype=object)
-    _, pyr = ent
-    no = gaussian_images.shape[0]
-    out = np.empty((no, pyr.levels - 1), dtype=object)
-    for o in range(no):
-        for l in range(pyr.levels - 1):
-            out[o, l] = pyr.level(o, l, dog=True)
+    """sift_impl.py:100-111: G[l+1] - G[l] per octave (pano_sift_dog on the uploaded levels)."""
+    ctx, no, nl = _upload_pyramid(gaussian_images)
+    ctx.check(ctx.lib.pano_sift_dog(ctx.h))
+    return _read_levels(ctx, no, nl - 1, dog=True)
+
+
+def _raw_keypoints(ctx, p, cap=8192):
+    import ctypes
+    _, torch, dev = _dev()
+    while True:
+        raw = torch.empty((1, cap, 6), dtype=torch.int32, device=dev)
+        counts = torch.zeros((1,), dtype=torch.int32, device=dev)
+        ctx.check(ctx.lib.pano_sift_extrema(ctx.h, ctypes.byref(p), _lib.ptr(raw), cap, _lib.ptr(counts)))
+        ctx.sync()
+        n = int(counts.cpu()[0])
+        if n < 0:
+            raise _lib.PanoError(_lib.PANO_E_OVERFLOW, "pano_sift_extrema: scratch capacity exceeded")
+        if n <= cap:
+            return raw[0, :n].cpu().numpy().view(_lib.KP_NP).reshape(-1)
+        cap = 1 << int(n - 1).bit_length()
+
+
+def find_scale_space_extrema(gaussian_images, dog_images, num_intervals, sigma, border,
+                             contrast_threshold=0.04):
+    """sift_impl.py:117-140: extrema -> quadratic-fit localisation -> orientations, every
+    candidate of every octave (pano_sift_extrema).  Returns the oriented keypoints before
+    remove_duplicate_keypoints, in the reference's scan order, base-image coordinates."""
+    ctx, no, nl = _upload_pyramid(gaussian_images, dog_images)
+    if nl != int(num_intervals) + 3:
+        raise ValueError(f"{nl} levels per octave do not fit num_intervals={num_intervals}")
+    p = _params(sigma=sigma, num_intervals=num_intervals, border=border,
+                contrast_threshold=contrast_threshold)
+    return from_records(_raw_keypoints(ctx, p))
+
+
+def generate_descriptors(keypoints, gaussian_images, window_width=4, num_bins=8, scale_multiplier=3,
+                         descriptor_max_value=0.2):
+    """sift_impl.py:361-526 for the given keypoints (input-image coordinates, converted octave
+    field) on the given pyramid (pano_sift_describe).  float32 [N, 128]."""
+    import ctypes
+    if window_width != 4 or num_bins != 8:
+        raise NotImplementedError("libpano's descriptor is the reference's 4 x 4 x 8 layout")
+    kps = list(keypoints)
+    if not kps:
+        return np.array([], dtype="float32")
+    g, no, nl = _pyramid_shapes(gaussian_images, "gaussian_images")
+    rec = np.zeros(len(kps), _lib.KP_NP)
+    for i, kp in enumerate(kps):
+        octv, lyr, _ = unpack_octave(kp)
+        if not (0 <= octv + 1 < no and 0 <= lyr < nl):
+            raise IndexError(f"keypoint {i}: octave {octv}, layer {lyr} outside the pyramid "
+                             f"({no} octaves, {nl} levels)")
+        vals = (kp.pt[0], kp.pt[1], kp.size, kp.angle, kp.response)
+        if not np.all(np.isfinite(vals)):
+            raise ValueError(f"keypoint {i}: non-finite fields {vals}")
+        rec[i] = (*vals, kp.octave)
+    ctx, _, _ = _upload_pyramid(g)
+    _, torch, dev = _dev()
+    n = len(kps)
+    k_dev = torch.from_numpy(rec.view(np.int32).reshape(1, n, 6).copy()).to(dev)
+    counts = torch.tensor([n], dtype=torch.int32, device=dev)
+    desc = torch.empty((1, n, 128), dtype=torch.float32, device=dev)
+    p = _lib.default_sift_params(scale_multiplier=float(scale_multiplier),
+                                 descriptor_max=float(descriptor_max_value))
+    ctx.check(ctx.lib.pano_sift_describe(ctx.h, ctypes.byref(p), _lib.ptr(k_dev), _lib.ptr(counts), n,
+                                         _lib.ptr(desc)))
+    return desc[0].cpu().numpy()
+
+
+# ------------------------------------------------------------------ per-pixel helpers
+# The reference's scalar helpers (one pixel / one keypoint at a time).  libpano evaluates the
+# same definitions batched inside find_scale_space_extrema; these host versions keep the
+# reference's per-call API for callers that use them directly.
+def is_pixel_an_extremum(prev_patch, curr_patch, next_patch, threshold):
+    """sift_impl.py:143-163: v >= (<=) all 26 neighbours, |v| > threshold."""
+    val = curr_patch[1, 1]
+    if abs(val) <= threshold:
+        return False
+    cube = np.stack([np.asarray(prev_patch), np.asarray(curr_patch), np.asarray(next_patch)])
+    return bool(np.all(val >= cube)) if val > 0 else bool(np.all(val <= cube))
+
+
+def compute_gradient_at_center_pixel(cube):
+    """sift_impl.py:217-224: central differences (dx, dy, ds)."""
+    return np.array([0.5 * (cube[1, 1, 2] - cube[1, 1, 0]),
+                     0.5 * (cube[1, 2, 1] - cube[1, 0, 1]),
+                     0.5 * (cube[2, 1, 1] - cube[0, 1, 1])])
+
+
+def compute_hessian_at_center_pixel(cube):
+    """sift_impl.py:227-240: the 3 x 3 Hessian by central differences."""
+    v = cube[1, 1, 1]
+    dxx = cube[1, 1, 2] - 2 * v + cube[1, 1, 0]
+    dyy = cube[1, 2, 1] - 2 * v + cube[1, 0, 1]
+    dss = cube[2, 1, 1] - 2 * v + cube[0, 1, 1]
+    dxy = 0.25 * (cube[1, 2, 2] - cube[1, 2, 0] - cube[1, 0, 2] + cube[1, 0, 0])
+    dxs = 0.25 * (cube[2, 1, 2] - cube[2, 1, 0] - cube[0, 1, 2] + cube[0, 1, 0])
+    dys = 0.25 * (cube[2, 2, 1] - cube[2, 0, 1] - cube[0, 2, 1] + cube[0, 0, 1])
+    return np.array([[dxx, dxy, dxs], [dxy, dyy, dys], [dxs, dys, dss]])
+
+
+def localize_extremum_via_quadratic_fit(x, y, layer, octave, num_intervals, dog_octave, sigma,
+                                        contrast_threshold, border, eigen_ratio=10, max_iter=5):
+    """sift_impl.py:169-211 for one extremum: <= max_iter Newton steps on the 3x3x3 cube / 255
+    (np.linalg.lstsq), contrast and edge tests; (KeyPoint, layer) or None.  Keeps the
+    reference's quirk of using the last cube after max_iter non-converged steps."""
+    shape = np.asarray(dog_octave[0]).shape
+    for _ in range(max_iter):
+        prev, curr, nxt = dog_octave[layer - 1:layer + 2]
+        cube = np.stack([prev[y - 1:y + 2, x - 1:x + 2], curr[y - 1:y + 2, x - 1:x + 2],
+                         nxt[y - 1:y + 2, x - 1:x + 2]]).astype("float32") / 255.
+        grad = compute_gradient_at_center_pixel(cube)
+        hess = compute_hessian_at_center_pixel(cube)
+        update = -np.linalg.lstsq(hess, grad, rcond=None)[0]
+        if np.all(np.abs(update) < 0.5):
+            break
+        x += int(np.round(update[0]))
+        y += int(np.round(update[1]))
+        layer += int(np.round(update[2]))
+        if y < border or y >= shape[0] - border or x < border or x >= shape[1] - border \
+                or layer < 1 or layer > num_intervals:
+            return None
+    val = cube[1, 1, 1] + 0.5 * np.dot(grad, update)
+    if abs(val) * num_intervals < contrast_threshold:
+        return None
+    h2 = hess[:2, :2]
+    tr = np.trace(h2)
+    d = np.linalg.det(h2)
+    if d <= 0 or eigen_ratio * (tr ** 2) >= ((eigen_ratio + 1) ** 2) * d:
+        return None
+    kp = KeyPoint()
+    kp.pt = ((x + update[0]) * (2 ** octave), (y + update[1]) * (2 ** octave))
+    kp.octave = octave + layer * (2 ** 8) + int(np.round((update[2] + 0.5) * 255)) * (2 ** 16)
+    kp.size = sigma * (2 ** ((layer + update[2]) / np.float32(num_intervals))) * (2 ** (octave + 1))
+    kp.response = abs(val)
+    return kp, layer
+
+
+def compute_keypoints_with_orientations(keypoint, octave, gauss_img, radius_factor=3, num_bins=36,
+                                        peak_ratio=0.8, scale_factor=1.5):
+    """sift_impl.py:246-293 for one keypoint: the 36-bin weighted gradient-orientation
+    histogram, [1 4 6 4 1]/16 smoothing, peaks >= peak_ratio * max with parabolic
+    interpolation; one KeyPoint per peak."""
+    gauss_img = np.asarray(gauss_img)
+    scale = scale_factor * keypoint.size / np.float32(2 ** (octave + 1))
+    radius = int(np.round(radius_factor * scale))
+    weight_fac = -0.5 / (scale ** 2)
+    cy = int(np.round(keypoint.pt[1] / np.float32(2 ** octave)))
+    cx = int(np.round(keypoint.pt[0] / np.float32(2 ** octave)))
+    dy, dx = np.mgrid[-radius:radius + 1, -radius:radius + 1]
+    dy, dx = dy.ravel(), dx.ravel()                # the reference's dy-outer, dx-inner order
+    yy, xx = cy + dy, cx + dx
+    ok = (xx > 0) & (xx < gauss_img.shape[1] - 1) & (yy > 0) & (yy < gauss_img.shape[0] - 1)
+    raw_hist = np.zeros(num_bins)
+    for ddy, ddx, y, x in zip(dy[ok].tolist(), dx[ok].tolist(), yy[ok].tolist(), xx[ok].tolist()):
+        gx = gauss_img[y, x + 1] - gauss_img[y, x - 1]
+        gy = gauss_img[y - 1, x] - gauss_img[y + 1, x]
+        mag = np.sqrt(gx * gx + gy * gy)
+        ang = np.rad2deg(np.arctan2(gy, gx)) % 360
+        w = np.exp(weight_fac * (ddx * ddx + ddy * ddy))
+        raw_hist[int(np.round(ang * num_bins / 360.)) % num_bins] += w * mag
+    smooth = np.zeros(num_bins)
+    for i in range(num_bins):
+        smooth[i] = (6 * raw_hist[i] + 4 * (raw_hist[i - 1] + raw_hist[(i + 1) % num_bins]) +
+                     raw_hist[i - 2] + raw_hist[(i + 2) % num_bins]) / 16.
+    maxv = np.max(smooth)
+    peaks = np.where(np.logical_and(smooth > np.roll(smooth, 1), smooth > np.roll(smooth, -1)))[0]
+    out = []
+    for p in peaks:
+        if smooth[p] >= peak_ratio * maxv:
+            left, right = smooth[(p - 1) % num_bins], smooth[(p + 1) % num_bins]
+            interp = (p + 0.5 * (left - right) / (left - 2 * smooth[p] + right)) % num_bins
+            angle = 360. - interp * 360. / num_bins
+            if abs(angle - 360.) < float_tolerance:
+                angle = 0
+            out.append(KeyPoint(*keypoint.pt, keypoint.size, angle, keypoint.response, keypoint.octave))
     return out
 
 
 __all__ = ["KeyPoint", "compute_keypoints_and_descriptors", "compute_number_of_octaves",
            "generate_gaussian_kernels", "compare_keypoints", "remove_duplicate_keypoints",
            "convert_keypoints_to_input_image_size", "unpack_octave", "generate_base_image",
-           "generate_gaussian_images", "generate_DoG_images"]
+           "generate_gaussian_images", "generate_DoG_images", "find_scale_space_extrema",
+           "is_pixel_an_extremum", "localize_extremum_via_quadratic_fit",
+           "compute_gradient_at_center_pixel", "compute_hessian_at_center_pixel",
+           "compute_keypoints_with_orientations", "generate_descriptors"]
