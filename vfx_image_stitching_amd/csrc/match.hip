@@ -537,11 +537,26 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 constexpr int BPI = PANO_DESC_DIM + 16;          // LDS row pitch in bytes (rows 36 banks apart)
 constexpr int kBig = 0x3fffffff;                 // "no distance" (padding rows, empty pairs)
+// Packed distance keys: key = 32 (C_j - 2 a'.b') + idx(j), idx = the candidate's rank among
+// the 32 rows one lane reads per tile (monotone in j).  One v_mad_i32_i24 forms the key from
+// the accumulator and C32[j] = 32 C_j + idx(j) (LDS), so min / med3 on keys give the least
+// distance with the first index, and the second-least distance, in one VALU op each.
+// |32 (C - 2 a'.b')| < 2^29 + 2^27 for real rows; padding rows carry C = kPadC, whose keys
+// (>= 2^30 - 2^27) never beat a real one; decoded distances >= kNone mean "no candidate".
+constexpr int kPadC = 1 << 25;
+constexpr int kNone = kPadC - (1 << 22);
+__device__ __forceinline__ int key_idx(int j) { return ((j >> 5) & 1) * 16 + ((j >> 3) & 3) * 4 + (j & 3); }
+__device__ __forceinline__ int med3_i32(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
-// c + a * b in one VALU op (|a|, |b| < 2^23 here: a'.b' is within +-2^21)
+// c + a * b in one VALU op (|a|, |b| < 2^23 here: a'.b' is within +-2^21); b in an SGPR
+// (-64 is not an inline constant, and VOP3 takes no literal)
 __device__ __forceinline__ int mad_i24(int a, int b, int c) {
     int r;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(b), "v"(c));
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
     return r;
 }
 
@@ -629,11 +644,11 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
     // the sign flip; the first quarter also its C
     const int sr = tid & (BT - 1), sp = tid / BT;
     uint4 pre[2];
-    int pre_c = kBig;
+    int pre_c = kPadC;
     auto fetch = [&](int jt) {
         const int row = jt * BT + sr;
         pre[0] = pre[1] = make_uint4(0u, 0u, 0u, 0u);
-        pre_c = kBig;                                   // past the count: never a best
+        pre_c = kPadC;                                  // past the count: never a best
         if (row < NB) {
             const uint4 *src = (const uint4 *)(dB + (size_t)row * PANO_DESC_DIM + 32 * sp);
             pre[0] = src[0];
@@ -647,7 +662,7 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
         for (int q = 0; q < 2; ++q)
             d4[q] = make_uint4(pre[q].x ^ 0x80808080u, pre[q].y ^ 0x80808080u, pre[q].z ^ 0x80808080u,
                                pre[q].w ^ 0x80808080u);
-        if (sp == 0) Cs2[buf][sr] = pre_c;
+        if (sp == 0) Cs2[buf][sr] = pre_c * 32 + key_idx(sr);      // C32: the key's base
     };
     int best[2] = {kBig, kBig}, second[2] = {kBig, kBig};
     int bj[2] = {0x7fffffff, 0x7fffffff};
@@ -679,9 +694,11 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
             if (jt + 2 * n_split < n_jt) fetch(jt + 2 * n_split);
         }
         const int jb = jt * BT + wj * 64 + 4 * lh;
+        // this tile's least / second-least key per query row (keys are unique per lane)
+        int tb[2] = {0x7fffffff, 0x7fffffff}, ts[2] = {0x7fffffff, 0x7fffffff};
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
-            // C of this lane's 16 candidate rows: rows (r & 3) + 8 (r >> 2) + 4 lh of block a
+            // C32 of this lane's 16 candidate rows: rows (r & 3) + 8 (r >> 2) + 4 lh of block a
             int cj[16];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
@@ -689,31 +706,26 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
                 cj[4 * g] = c4.x; cj[4 * g + 1] = c4.y; cj[4 * g + 2] = c4.z; cj[4 * g + 3] = c4.w;
             }
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                int v[16];
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = mad_i24(acc[a][b][r], -2, cj[r]);
-                if (SECOND) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {   // j increasing within the lane: strict <
-                        second[b] = min(second[b], max(best[b], v[r]));
-                        const bool lt = v[r] < best[b];
-                        bj[b] = lt ? jb + a * 32 + (r & 3) + 8 * (r >> 2) : bj[b];
-                        best[b] = lt ? v[r] : best[b];
-                    }
-                } else {
-                    int m = v[0];
-#pragma unroll
-                    for (int r = 1; r < 16; ++r) m = min(m, v[r]);
-                    if (m < best[b]) {
-                        int ri = 15;
-#pragma unroll
-                        for (int r = 14; r >= 0; --r) ri = v[r] == m ? r : ri;   // first r
-                        best[b] = m;
-                        bj[b] = jb + a * 32 + (ri & 3) + 8 * (ri >> 2);
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    const int key = mad_i24(acc[a][b][r], -64, cj[r]);
+                    if (SECOND) ts[b] = med3_i32(tb[b], key, ts[b]);
+                    tb[b] = min(tb[b], key);
                 }
+        }
+        // fold the tile into the running state: tiles come in increasing j, so strict < keeps
+        // the first index on a tie
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int d1 = tb[b] >> 5, idx = tb[b] & 31;   // arithmetic shift: floor(key / 32)
+            const int j = jb + (idx >> 4) * 32 + ((idx >> 2) & 3) * 8 + (idx & 3);
+            if (SECOND) {
+                const int d2 = ts[b] >> 5;
+                second[b] = d1 < best[b] ? min(best[b], d2) : min(second[b], d1);
             }
+            bj[b] = d1 < best[b] ? j : bj[b];
+            best[b] = min(best[b], d1);
         }
     }
     auto imerge = [](int &b, int &j, int &s, int b2, int j2, int s2) {
@@ -740,8 +752,8 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
         const int gi = i0 + tid;
         if (gi < NA) {
             const int ra = cst[(size_t)fa * cap + gi];
-            const float db = x.best >= kBig ? INFINITY : (float)(ra + x.best);
-            const float ds = x.second >= kBig ? INFINITY : (float)(ra + x.second);
+            const float db = x.best >= kNone ? INFINITY : (float)(ra + x.best);
+            const float ds = x.second >= kNone ? INFINITY : (float)(ra + x.second);
             parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{db, x.idx, ds};
         }
     }

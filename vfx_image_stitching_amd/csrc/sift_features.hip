@@ -1225,11 +1225,16 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             ob = ob < 0.0f ? ob + 8.0f : ob;
             const float wm = w * mag;
             const float fr = floorf(rbin), fc = floorf(cbin), fo = floorf(ob);
-            const float rf = rbin - fr, cf = cbin - fc, of = ob - fo;
+            const float rf = rbin - fr, cf = cbin - fc;
+            // (the reference's o0 = floor(ob) % 8, of = ob - o0 gives of = 8 when np.mod rounds a
+            // tiny negative offset to 8.0; numpy's SIMD f32 arctan2 / rad2deg decide that case at
+            // the ulp level, which no other arithmetic reproduces: here of = ob - floor(ob), the
+            // continuous form -- DESIGN.md 4, "descriptor outliers")
             const int o0 = (int)fo & 7, o1 = (o0 + 1) & 7;
             const int base = ((int)fr + 1) * 48 + ((int)fc + 1) * 8;   // (r0 + 1, c0 + 1) bin
             const float c1 = wm * rf, c0w = wm - c1;
             const float v00 = c0w * (1.0f - cf), v01 = c0w * cf, v10 = c1 * (1.0f - cf), v11 = c1 * cf;
+            const float of = ob - fo;
             const float nof = 1.0f - of;
             auto fix = [](float v) { return (unsigned long long)(uint32_t)fmaf(v, kFix, 0.5f); };
             unsigned long long *hA = h + base + o0, *hB = h + base + o1;
