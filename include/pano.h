@@ -131,8 +131,7 @@ int pano_sift_u8(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
  * after pano_sift_pyramid the Gaussian / DoG pyramid of frame `frame` stays in the
  * context: level 0..num_intervals+2 (Gaussian) / 0..num_intervals+1 (DoG).  After pano_sift
  * every DoG level is there too, but of the Gaussian levels only those the keypoint stages
- * read (level 0 of octave 0 and levels 1..num_intervals+1): copying the others returns
- * PANO_E_UNSUPPORTED.
+ * read (levels 1..num_intervals): copying the others returns PANO_E_UNSUPPORTED.
  * Copies one level to d_out (h_o x w_o float32); pano_sift_level_shape reports its size. */
 int pano_sift_pyramid(pano_ctx *ctx, const uint8_t *d_bgr, int n, int h, int w,
                       const pano_sift_params *params);

@@ -272,7 +272,7 @@ int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int do
         return PANO_E_ARG;
     const int nl = dog ? ctx->n_lvl - 1 : ctx->n_lvl;
     if (level < 0 || level >= nl) return PANO_E_ARG;
-    if (!dog && !ctx->pyr_full && ((level == 0 && octave > 0) || level == nl - 1))
+    if (!dog && !ctx->pyr_full && (level == 0 || level > nl - 3))
         return pano_fail(ctx, PANO_E_UNSUPPORTED,
                          "pano_sift does not materialise this Gaussian level; use pano_sift_pyramid");
     const size_t plane = (size_t)ctx->oct_h[octave] * ctx->oct_w[octave];

@@ -641,6 +641,227 @@ blur_pair(LoadArgs la, float *__restrict__ out1, float *__restrict__ dog1, float
     }
 }
 
+// Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global stores (__syncthreads' release fence drains every outstanding HBM write of the wave,
+// a few microseconds per barrier; the tail writes each level's planes while it cascades and
+// nothing in the kernel reads them back).
+__device__ __forceinline__ void lds_barrier() {
+#if PANO_TAIL_SYNC
+    __syncthreads();
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#endif
+}
+
+// ------------------------------------------------------------------ fused level chains
+// Two or three consecutive levels of an octave in ONE launch (the "cascade": the octave's
+// levels are written once and the intermediate level planes are never read back from HBM).
+// A 64 x 64 output tile stages its input level over the tile plus the chain's cumulative
+// halo HT (sum of the levels' radii), then, level by level in LDS, computes the level on the
+// tile plus the halo the REMAINING levels still need, in place: a row pass (RowVec_32f order)
+// and a column pass (SymmColumnVec_32f order), each reading all of a thread's inputs before a
+// barrier and writing its outputs after it.  Positions of the computed region outside the
+// image are then replaced by their BORDER_REFLECT_101 image inside the region (the next level
+// must read reflected values; a blur of reflected inputs runs its taps in the opposite order
+// and rounds differently).  The column pass writes the tile's outputs: the level (when a
+// later stage reads it) and its DoG against the previous level's centre values, which the
+// same thread read before the row pass.  Per output the arithmetic is blur_fast's, hence
+// bit-identical.  HBM per octave pixel: the input plane (chain A: a quarter-size u8 gray or
+// the previous octave's level read at half resolution; chain B: G2) and the written planes,
+// ~36-44 B against ~64 B for the level-by-level form.
+constexpr int kCT = 64;          // output tile side
+constexpr int kChainThreads = 512;
+
+struct ChainOut {
+    float *g[3];                 // the chain's levels (nullptr: not written)
+    float *d[3];                 // DoG of each level against the previous (nullptr: none)
+    float *gin;                  // MODE_DOWN, full pyramid: the staged level 0 (G0) plane
+};
+
+__host__ __device__ constexpr int chain_r(int nt) { return nt > 0 ? (nt - 1) / 2 : 0; }
+constexpr int kChainSR = 16;     // row-pass outputs per item
+constexpr int kChainSC = 10;     // column-pass outputs per item
+// LDS floats of a chain whose input halo is HT: the region, plus the rows / columns the last
+// (partial) segments of every level read past it (their outputs are discarded)
+__host__ __device__ constexpr int chain_rows(int ht, int nt0, int nt1, int nt2) {
+    int rows = kCT + 2 * ht, hin = ht;
+    const int nts[3] = {nt0, nt1, nt2};
+    for (int k = 0; k < 3 && nts[k] > 0; ++k) {
+        const int hout = hin - chain_r(nts[k]), nout = kCT + 2 * hout;
+        const int need = ((nout + kChainSC - 1) / kChainSC) * kChainSC + nts[k] - 1;
+        rows = rows > need ? rows : need;
+        hin = hout;
+    }
+    return rows + 1;
+}
+
+// One level of a chain: the region of side kCT + 2 HIN in A (pitch P, origin (y0 - HIN,
+// x0 - HIN) in image coordinates) -> the level on side kCT + 2 (HIN - R), stored top-left
+// aligned (origin (y0 - HOUT, x0 - HOUT)).
+template <int NT, int HIN, int P, bool DOG>
+__device__ __forceinline__ void chain_step(float *A, const float *__restrict__ kg, int y0, int x0, int H,
+                                           int W, int th, int tw, size_t fo, float *gout, float *dout,
+                                           bool border) {
+    constexpr int R = (NT - 1) / 2, HOUT = HIN - R;
+    // this level's taps: uniform loads into scalar registers (three Taps structs as kernel
+    // arguments spilled the scalar file into VGPR lanes)
+    float k[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) k[t] = kg[t];
+    constexpr int NIN = kCT + 2 * HIN, NOUT = kCT + 2 * HOUT;
+    constexpr int SR = kChainSR, SC = kChainSC, NT_ = kChainThreads;
+    constexpr int NSR = (NOUT + SR - 1) / SR, ITR = NIN * NSR, IR = (ITR + NT_ - 1) / NT_;
+    constexpr int NSC = (NOUT + SC - 1) / SC, ITC = NOUT * NSC, IC = (ITC + NT_ - 1) / NT_;
+    static_assert(IR <= 2 && IC <= 3, "chain items per thread");
+    const int tid = threadIdx.x;
+    // (1) DoG centres: the previous level at this thread's column-pass outputs inside the
+    // tile, read before the row pass overwrites the region
+    float cen[IC][SC];
+    if constexpr (DOG) {
+#pragma unroll
+        for (int it = 0; it < IC; ++it) {
+            const int item = tid + it * NT_;
+            const int c = item % NOUT, q = item / NOUT;
+#pragma unroll
+            for (int j = 0; j < SC; ++j) {
+                const int rr = q * SC + j;
+                const bool in = item < ITC && rr >= HOUT && rr < HOUT + kCT && c >= HOUT && c < HOUT + kCT;
+                cen[it][j] = in ? A[(rr + R) * P + c + R] : 0.0f;
+            }
+        }
+    }
+    // (2) row pass, in place (left-aligned): every item's inputs are read before the barrier
+    float ro[IR][SR];
+#pragma unroll
+    for (int it = 0; it < IR; ++it) {
+        const int item = tid + it * NT_;
+        if (item < ITR) {
+            const int r = item % NIN, sg = item / NIN;
+            row_seg<NT, SR>(A + r * P + sg * SR, k, ro[it]);
+        }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int it = 0; it < IR; ++it) {
+        const int item = tid + it * NT_;
+        if (item < ITR) {
+            const int r = item % NIN, sg = item / NIN;
+#pragma unroll
+            for (int j = 0; j < SR; ++j)
+                if (sg * SR + j < NOUT) A[r * P + sg * SR + j] = ro[it][j];
+        }
+    }
+    lds_barrier();
+    // (3) column pass, in place (top-aligned), with the tile's outputs
+    float co[IC][SC];
+#pragma unroll
+    for (int it = 0; it < IC; ++it) {
+        const int item = tid + it * NT_;
+        if (item < ITC) {
+            const int c = item % NOUT, q = item / NOUT;
+            col_seg<NT, SC>(A + q * SC * P + c, P, k, co[it]);
+        }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int it = 0; it < IC; ++it) {
+        const int item = tid + it * NT_;
+        if (item < ITC) {
+            const int c = item % NOUT, q = item / NOUT;
+            const int tx = c - HOUT;
+#pragma unroll
+            for (int j = 0; j < SC; ++j) {
+                const int rr = q * SC + j;
+                if (rr >= NOUT) break;
+                A[rr * P + c] = co[it][j];
+                const int ty = rr - HOUT;
+                if (ty >= 0 && ty < th && tx >= 0 && tx < tw) {
+                    const size_t gi = fo + (size_t)(y0 + ty) * W + x0 + tx;
+                    if (gout) gout[gi] = co[it][j];
+                    if constexpr (DOG) dout[gi] = co[it][j] - cen[it][j];
+                }
+            }
+        }
+    }
+    lds_barrier();
+    // (4) BORDER_REFLECT_101 of the region positions outside the image (reads inside
+    // positions, writes outside ones: one pass).  Positions whose reflection falls outside the
+    // region lie beyond what any later output reads, and are left as they are.
+    if constexpr (HOUT > 0) {
+        if (border) {
+            const int oy = y0 - HOUT, ox = x0 - HOUT;
+            for (int i = tid; i < NOUT * NOUT; i += NT_) {
+                const int r = i / NOUT, c = i - r * NOUT;
+                const int y = oy + r, x = ox + c;
+                if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) continue;
+                const int sr = reflect101(y, H) - oy, sc = reflect101(x, W) - ox;
+                if ((unsigned)sr < (unsigned)NOUT && (unsigned)sc < (unsigned)NOUT) A[r * P + c] = A[sr * P + sc];
+            }
+            lds_barrier();
+        }
+    }
+}
+
+// MODE_BASE chains start at the base level (no DoG for it); the other modes' first level
+// has a DoG against the staged level 0.
+template <int MODE, int NT0, int NT1, int NT2>
+__global__ void __launch_bounds__(kChainThreads, 4)
+blur_chain(LoadArgs la, ChainOut co, int H, int W, const float *__restrict__ taps, int l0) {
+    constexpr int HT = chain_r(NT0) + chain_r(NT1) + chain_r(NT2);
+    constexpr int RS = kCT + 2 * HT, P = RS | 1;
+    static_assert(RS <= 128, "stage_tile covers 128 columns");
+    extern __shared__ __attribute__((aligned(16))) float A[];
+    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
+    const int x0 = (int)(tb % gridDim.x) * kCT, y0 = (int)((tb / gridDim.x) % gridDim.y) * kCT;
+    const int f = (int)(tb / (gridDim.x * gridDim.y));
+    const int tw = min(kCT, W - x0), th = min(kCT, H - y0);
+    const size_t fo = (size_t)f * H * W;
+    constexpr int NW = kChainThreads / 64;
+    // the whole region, reflected at the image borders (partial tiles included: every level
+    // then computes finite values everywhere)
+    stage_tile<MODE, NW, (RS + NW - 1) / NW>(la, f, H, W, x0, y0, HT, RS, RS, P, A);
+    lds_barrier();
+    if (MODE == MODE_DOWN && co.gin) {
+        for (int i = threadIdx.x; i < kCT * kCT; i += kChainThreads) {
+            const int ty = i / kCT, tx = i - ty * kCT;
+            if (ty < th && tx < tw) co.gin[fo + (size_t)(y0 + ty) * W + x0 + tx] = A[(ty + HT) * P + tx + HT];
+        }
+    }
+    const bool border = y0 - HT < 0 || x0 - HT < 0 || y0 + kCT + HT > H || x0 + kCT + HT > W;
+    constexpr bool FIRST_DOG = MODE != MODE_BASE && MODE != MODE_BASEF;
+    // taps rows: [level][PANO_MAX_TAPS], the chain's levels l0, l0 + 1, l0 + 2 (row 0 = the base)
+    const float *k0 = taps + l0 * PANO_MAX_TAPS;
+    chain_step<NT0, HT, P, FIRST_DOG>(A, k0, y0, x0, H, W, th, tw, fo, co.g[0], co.d[0], border);
+    if constexpr (NT1 > 0)
+        chain_step<NT1, HT - chain_r(NT0), P, true>(A, k0 + PANO_MAX_TAPS, y0, x0, H, W, th, tw, fo, co.g[1],
+                                                    co.d[1], border);
+    if constexpr (NT2 > 0)
+        chain_step<NT2, HT - chain_r(NT0) - chain_r(NT1), P, true>(A, k0 + 2 * PANO_MAX_TAPS, y0, x0, H, W, th,
+                                                                  tw, fo, co.g[2], co.d[2], border);
+}
+
+template <int MODE, int NT0, int NT1, int NT2>
+int launch_chain(pano_ctx *ctx, const LoadArgs &la, const ChainOut &co, int n, int H, int W, int l0) {
+    constexpr int HT = chain_r(NT0) + chain_r(NT1) + chain_r(NT2);
+    constexpr int P = (kCT + 2 * HT) | 1;
+    const size_t sm = (size_t)chain_rows(HT, NT0, NT1, NT2) * P * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_chain<MODE, NT0, NT1, NT2>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        attr = true;
+    }
+    dim3 grid((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, n);
+    {
+        PanoProf prof_(ctx, PK_BLUR);
+        blur_chain<MODE, NT0, NT1, NT2><<<grid, kChainThreads, sm, ctx->stream>>>(la, co, H, W, ctx->taps, l0);
+    }
+    PANO_LAUNCH_CHECK(ctx, "blur_chain");
+    return PANO_OK;
+}
+
 // ------------------------------------------------------------------ small-octave tail
 // Octaves whose levels fit one 64 x 64 tile are latency-bound as separate launches (one
 // tiny workgroup per frame, ~7 us each, 5 per octave).  blur_tail runs them all in ONE
@@ -677,20 +898,6 @@ struct TailArgs {
 
 __device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_NEAREST
     return (int)floor(d * inv);
-}
-
-// Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
-// global stores (__syncthreads' release fence drains every outstanding HBM write of the wave,
-// a few microseconds per barrier; the tail writes each level's planes while it cascades and
-// nothing in the kernel reads them back).
-__device__ __forceinline__ void lds_barrier() {
-#if PANO_TAIL_SYNC
-    __syncthreads();
-#else
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#endif
 }
 
 // One tail level, compile-time tap count (NT = 0: runtime count n).  in / outb are [64][kTP]
@@ -1093,6 +1300,17 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     for (int l = 1; l < nl; ++l)
         if (tl[l].n < 0) return pano_fail(ctx, PANO_E_UNSUPPORTED, "Gaussian kernel too wide");
     float *G = ctx->pyr, *D = ctx->dog;
+    // fused level chains (blur_chain, PANO_BLUR_CHAIN=1) for the octaves whose planes hold the
+    // (3, 4, 5) chain's halo, with the reference's tap counts.  Measured on MI355X:
+    // bit-exact, ~40 % less HBM traffic, but 1.6x slower than the level-by-level launches at
+    // octave 0 (the halo recompute and the two resident workgroups per CU leave the VALU ~30 %
+    // busy), so off by default.  Read per call so tests can compare both forms.
+    const char *chain_env = getenv("PANO_BLUR_CHAIN");
+    const bool chain_on = chain_env && atoi(chain_env) != 0;
+    const bool chain_taps = chain_on && nl == 6 && tl[1].n == 11 && tl[2].n == 13 && tl[3].n == 17 &&
+                            tl[4].n == 21 && tl[5].n == 27;
+    auto chain_ok = [&](int o) { return chain_taps && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= 64; };
+    const bool chain_base = src.bgr && !src.base_only && chain_ok(0) && tb.n == 11;
     if (src.base) {
         // generate_gaussian_images(base, ...): the caller's base is level 0 of octave 0
         PANO_HIP(ctx, hipMemcpyAsync(G + ctx->gauss_off[0][0], src.base,
@@ -1106,6 +1324,17 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         rc = launch_blur<MODE_BASEF>(ctx, la, G + ctx->gauss_off[0][0], nullptr, nullptr, n,
                                      ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
+    } else if (chain_base) {
+        // gray frames only: the base level is the first level of octave 0's first chain
+        const size_t npx = (size_t)n * h * w;
+        rc = pano_grow(ctx, (void **)&ctx->gray, &ctx->gray_bytes, npx + 16);
+        if (rc) return rc;
+        const unsigned blocks = (unsigned)((npx + 1023) / 1024);
+        {
+            PanoProf prof_(ctx, PK_BLUR);
+            gray_frames<<<blocks, 256, 0, ctx->stream>>>(src.bgr, ctx->gray, npx);
+        }
+        PANO_LAUNCH_CHECK(ctx, "gray_frames");
     } else {
         // gray frames (u8) for the base image
         const size_t npx = (size_t)n * h * w;
@@ -1158,22 +1387,8 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         return PANO_OK;
     };
     auto launch_tail = [&]() -> int {
-        // device copy of the level taps (uploaded only when they change)
-        float th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
         TailArgs ta{};
-        for (int l = 1; l < nl; ++l) {
-            for (int t = 0; t < tl[l].n; ++t) th[l * PANO_MAX_TAPS + t] = tl[l].k[t];
-            ta.ntap[l] = tl[l].n;
-        }
-        if (!ctx->taps) {
-            PANO_HIP(ctx, hipMalloc((void **)&ctx->taps, sizeof(th)));
-            ctx->taps_valid = false;
-        }
-        if (!ctx->taps_valid || memcmp(th, ctx->taps_host, sizeof(th)) != 0) {
-            memcpy(ctx->taps_host, th, sizeof(th));
-            PANO_HIP(ctx, hipMemcpy(ctx->taps, ctx->taps_host, sizeof(th), hipMemcpyHostToDevice));
-            ctx->taps_valid = true;
-        }
+        for (int l = 1; l < nl; ++l) ta.ntap[l] = tl[l].n;
         ta.taps = ctx->taps;
         ta.prev = G + ctx->gauss_off[o_tail - 1][nl - 3];
         ta.ph = ctx->oct_h[o_tail - 1];
@@ -1198,6 +1413,25 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         ctx->o_tail = o_side;
         return PANO_OK;
     };
+    // device copy of the taps, [level][PANO_MAX_TAPS] with row 0 the base's (the tail and the
+    // chains read them); uploaded only when they change, so never inside a graph capture after
+    // the eager first call
+    {
+        float th[PANO_MAX_LEVELS * PANO_MAX_TAPS] = {};
+        for (int t = 0; t < tb.n; ++t) th[t] = tb.k[t];
+        for (int l = 1; l < nl; ++l)
+            for (int t = 0; t < tl[l].n; ++t) th[l * PANO_MAX_TAPS + t] = tl[l].k[t];
+        if (!ctx->taps) {
+            PANO_HIP(ctx, hipMalloc((void **)&ctx->taps, sizeof(th)));
+            ctx->taps_valid = false;
+        }
+        if (!ctx->taps_valid || memcmp(th, ctx->taps_host, sizeof(th)) != 0) {
+            if (ctx->capturing) return pano_fail(ctx, PANO_E_UNSUPPORTED, "tap upload inside a graph capture");
+            memcpy(ctx->taps_host, th, sizeof(th));
+            PANO_HIP(ctx, hipMemcpy(ctx->taps, ctx->taps_host, sizeof(th), hipMemcpyHostToDevice));
+            ctx->taps_valid = true;
+        }
+    }
     // fused level pairs (blur_pair, PANO_BLUR_PAIR) on the latency-bound octaves: (1, 2) and
     // (4, 5) of every octave o >= 1 whose plane has fewer than PANO_BLUR_PAIR_TILES 64 x 64
     // tiles per batch; level 3 alone keeps the next octave's (and the tail's) start after it
@@ -1215,6 +1449,52 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
         ctx->stream = o >= o_side ? ctx->side : main_stream;     // side-stream octaves
+        if (chain_ok(o)) {
+            // chain A: levels 1-2 (octave 0 from gray: base, 1, 2); chain B: levels 3-5 from G2.
+            // Written: G1-G3 and DoG 0-4 (every level in a full pyramid)
+            auto Gp = [&](int l) { return G + ctx->gauss_off[o][l]; };
+            auto Dp = [&](int l) { return D + ctx->dog_off[o][l]; };
+            LoadArgs la{};
+            ChainOut ca{};
+            if (o == 0 && chain_base) {
+                la.gray = ctx->gray;
+                la.sh = h;
+                la.sw = w;
+                ca.g[0] = full ? Gp(0) : nullptr;
+                ca.g[1] = Gp(1); ca.d[1] = Dp(0);
+                ca.g[2] = Gp(2); ca.d[2] = Dp(1);
+                rc = launch_chain<MODE_BASE, 11, 11, 13>(ctx, la, ca, n, H, W, 0);
+            } else if (o == 0) {
+                la.src = Gp(0);
+                ca.g[0] = Gp(1); ca.d[0] = Dp(0);
+                ca.g[1] = Gp(2); ca.d[1] = Dp(1);
+                rc = launch_chain<MODE_LEVEL, 11, 13, 0>(ctx, la, ca, n, H, W, 1);
+            } else {
+                la.src = G + ctx->gauss_off[o - 1][nl - 3];
+                la.sh = ctx->oct_h[o - 1];
+                la.sw = ctx->oct_w[o - 1];
+                la.ifx = 1.0 / ((double)W / la.sw);
+                la.ify = 1.0 / ((double)H / la.sh);
+                ca.gin = full ? Gp(0) : nullptr;
+                ca.g[0] = Gp(1); ca.d[0] = Dp(0);
+                ca.g[1] = Gp(2); ca.d[1] = Dp(1);
+                rc = launch_chain<MODE_DOWN, 11, 13, 0>(ctx, la, ca, n, H, W, 1);
+            }
+            if (rc) { ctx->stream = main_stream; return rc; }
+            LoadArgs lb{};
+            lb.src = Gp(2);
+            ChainOut cb{};
+            cb.g[0] = Gp(3); cb.d[0] = Dp(2);
+            cb.g[1] = full ? Gp(4) : nullptr; cb.d[1] = Dp(3);
+            cb.g[2] = full ? Gp(5) : nullptr; cb.d[2] = Dp(4);
+            rc = launch_chain<MODE_LEVEL, 17, 21, 27>(ctx, lb, cb, n, H, W, 3);
+            if (rc) { ctx->stream = main_stream; return rc; }
+            if (o == o_side - 1 && o_tail < no) {
+                rc = fork();
+                if (rc) { ctx->stream = main_stream; return rc; }
+            }
+            continue;
+        }
         const bool pairs_here = o >= 1 && nl == 6 && H >= 32 && W >= 32 &&
                                 (long)((W + 63) / 64) * ((H + 63) / 64) * n < pair_tiles;
         for (int l = 1; l < nl; ++l) {
