@@ -47,17 +47,18 @@ def match_dtype(st):
         return "i8"
     return "bf16"
 MFMA_F32_PEAK_TFLOPS = 157.3    # dense f32 MFMA
-FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec (the blur's arithmetic)
+F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X f32 vector peak (v_pk_fma_f32), the blur's arithmetic
 
 
 def pmc_traffic(kernel, workload, method):
     """HBM bytes per launch of a kernel class from the newest committed PMC traffic profile
     (tools/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over the same
-    parrington SIFT step, corrected per profiles/r01_fetch_calibration.txt)."""
+    SIFT step -- parrington, or the 19-frame synthetic 1080p one -- corrected per
+    profiles/r01_fetch_calibration.txt)."""
     import glob
-    if workload != "parrington" or method != "sift":
+    if workload not in ("parrington", "synthetic") or method != "sift":
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_parrington.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_traffic_{workload}.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -67,9 +68,10 @@ def pmc_traffic(kernel, workload, method):
     return c["hbm_bytes_per_step"] / c["launches_per_step"], os.path.relpath(files[-1], ROOT)
 
 
-def blur_fp64_flops(st, n_frames):
-    """Algorithmic fp64 FMA flops of the blur class per step: every Gaussian level output is
-    two separable passes of NT taps (no tile-halo recompute), 2 flop per tap."""
+def blur_f32_flops(st, n_frames):
+    """Algorithmic f32 flops of the blur class per step: every Gaussian level output is a row
+    pass of NT fused multiply-adds and a symmetric column pass of R + 1 fused multiply-adds and
+    R pair additions (OpenCV's float32 filter), no tile-halo recompute."""
     import ctypes
     import math
     ctx = st.ctx
@@ -82,17 +84,19 @@ def blur_fp64_flops(st, n_frames):
     buf = (ctypes.c_double * 64)()
     nt = ctypes.c_int()
 
-    def taps(s):
+    def flops_per_px(s):
         ctx.lib.pano_sift_taps(ctypes.c_double(s), buf, ctypes.byref(nt))
-        return nt.value
+        n = nt.value
+        r = (n - 1) // 2
+        return 2 * n + 2 * (r + 1) + r
     no = ctypes.c_int32()
     hh, ww = ctypes.c_int32(), ctypes.c_int32()
     ctx.lib.pano_sift_level_shape(ctx.h, 0, ctypes.byref(hh), ctypes.byref(ww), ctypes.byref(no))
-    fl = 2 * 2 * taps(base) * hh.value * ww.value
+    fl = flops_per_px(base) * hh.value * ww.value
     for o in range(no.value):
         ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(hh), ctypes.byref(ww), None)
         for l in range(1, p.num_intervals + 3):
-            fl += 2 * 2 * taps(sig_l[l]) * hh.value * ww.value
+            fl += flops_per_px(sig_l[l]) * hh.value * ww.value
     return fl * n_frames
 
 
@@ -322,12 +326,12 @@ def main():
                     "avg_launch_ms": round(per_launch_ms, 5), "launches_per_step": launches_per_step,
                     "kernel_ms_per_step": round(per_step_ms, 4)}
             if rk == "blur_level" and args.method == "sift":
-                fl = blur_fp64_flops(st, n_local)
+                fl = blur_f32_flops(st, n_local)
                 tf = fl / (per_step_ms * 1e-3) / 1e12
-                roof["fp64_fma"] = {"note": "the blur is bit-exact fp64 FMA work (DESIGN.md 3): "
-                                            "its compute roofline", "achieved": round(tf, 2),
-                                    "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                    "frac": round(tf / FP64_PEAK_TFLOPS, 4)}
+                roof["f32_vector"] = {"note": "the blur's arithmetic: OpenCV's float32 FMA filter "
+                                              "(DESIGN.md 4), its compute roofline",
+                                      "achieved": round(tf, 2), "peak": F32_VECTOR_PEAK_TFLOPS,
+                                      "unit": "TFLOP/s", "frac": round(tf / F32_VECTOR_PEAK_TFLOPS, 4)}
         else:
             roof = {"bound": "latency", "kernel": rk, "achieved": None, "peak": None, "unit": None,
                     "frac": None, "traffic": None, "avg_launch_ms": round(per_launch_ms, 5),
@@ -369,7 +373,7 @@ def main():
         "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": args.scaling, "vs_baseline": None,
-        "dtype": ("u8 frames; f32 pyramid (fp64-accumulated blur); match " +
+        "dtype": ("u8 frames; f32 pyramid (OpenCV's float32 FMA blur order); match " +
                   {"f32": "f32 MFMA", "bf16": "bf16 MFMA, exact for integer descriptors",
                    "i8": "i8 MFMA on u8 descriptors - 128, exact integer distances"}[match_dtype(st)]
                   if args.method == "sift" else "u8 frames; f64 Harris response; f32 descriptors"),

@@ -379,7 +379,8 @@ int pano_graph_launch(pano_ctx *ctx, pano_graph *g);
  * stitch's whole per-call GPU work as one call (its last node copies the result header to
  * pinned host memory, pano_copy_async). */
 int pano_graph_launch_sync(pano_ctx *ctx, pano_graph *g, void *hip_stream);
-/* hipMemcpyAsync on the context's stream (device or pinned host pointers; capturable). */
+/* Copy on the context's stream (device or pinned host pointers; capturable): up to 1 MiB as
+ * a copy kernel (the GPU writes pinned host memory directly), larger as hipMemcpyAsync. */
 int pano_copy_async(pano_ctx *ctx, void *dst, const void *src, size_t bytes);
 int pano_graph_prof(pano_graph *g, int kernel_class, int *launches, double *total_ms);
 int pano_graph_destroy(pano_graph *g);

@@ -11,13 +11,13 @@ import sys
 
 # device kernel name -> libpano profiler class (_lib.KERNELS)
 CLASSES = [
-    (r"^(gray_frames|blur_fast|blur_level|blur_tail)", "blur_level"),
+    (r"^(gray_frames|blur_fast|blur_level|blur_tail|blur_chain|blur_pair)", "blur_level"),
     (r"^(extrema_scan|extrema_stream|localize)", "extrema_localize"),
     (r"^orientation", "orientation"),
     (r"^(rank_keys|bucket_|emit_keypoints)", "sort_dedup"),
-    (r"^descriptor", "descriptor"),
-    (r"^(pack_rows|row_norms)", "row_norms"),
-    (r"^(dist_bf16|dist_mfma|dist_u8)", "dist_mfma"),
+    (r"^(descriptor|desc_order)", "descriptor"),
+    (r"^(pack_rows|row_norms|row_consts)", "row_norms"),
+    (r"^(dist_bf16|dist_mfma|dist_u8|dist_i8)", "dist_mfma"),
     (r"^reduce_parts", "reduce_parts"),
     (r"^(pair_shifts|pair_compact|pair_votes|pair_select)", "pair_shifts"),
     (r"^(composite|plan_device)", "composite_step"),
@@ -39,7 +39,8 @@ def cls(name):
 
 
 root, runs = sys.argv[1], int(sys.argv[2])
-out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, tools/pmc_traffic.sh, parrington SIFT step",
+work = sys.argv[3] if len(sys.argv) > 3 else "parrington"
+out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, tools/pmc_traffic.sh, {work} SIFT step",
        "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (profiles/r01_fetch_calibration.txt)",
        "steps": runs - 1, "classes": {}}
 acc = collections.defaultdict(lambda: collections.defaultdict(float))

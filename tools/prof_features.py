@@ -1,5 +1,8 @@
 #!/usr/bin/env python3
-"""Run the parrington SIFT pipeline N times (for rocprofv3 counter collection)."""
+"""Run the SIFT stitch N times (for rocprofv3 counter collection).
+
+    python tools/prof_features.py N [parrington|synthetic]
+synthetic = BASELINE config 5's 1080p frames, 19 frames (the bench's N=1 weak workload)."""
 import os
 import sys
 
@@ -11,13 +14,19 @@ from vfx_image_stitching_amd import data  # noqa: E402
 from vfx_image_stitching_amd.pipeline import Stitcher  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-names, frames, focals, margin = data.load_set("parrington")
-st = Stitcher("sift", match=os.environ.get("PANO_MATCH"))     # None: the Stitcher default (u8)
+work = sys.argv[2] if len(sys.argv) > 2 else "parrington"
+if work == "synthetic":
+    frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920, start=0, count=19)
+    margin, cap = 15, 65536
+else:
+    names, frames, focals, margin = data.load_set(work)
+    cap = 4096
+st = Stitcher("sift", cap=cap, match=os.environ.get("PANO_MATCH"))  # None: the default (u8)
 d = st.upload(frames)
 for _ in range(n):
     try:
         st.run(d, focals, margin=margin)
-    except Exception as e:          # ablation builds (PANO_BLUR_DBG) produce garbage features
+    except Exception as e:          # ablation builds produce garbage features
         print("run failed:", e)
         torch.cuda.synchronize()
 torch.cuda.synchronize()

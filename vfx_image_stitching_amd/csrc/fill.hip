@@ -34,3 +34,25 @@ int launch_fill(pano_ctx *ctx, void *dst, uint8_t value, size_t bytes) {
     PANO_LAUNCH_CHECK(ctx, "fill_bytes");
     return PANO_OK;
 }
+
+// Small copies as a kernel (graph kernel node) instead of a hipMemcpyAsync (a blit / SDMA
+// node): the batched stitch's one device -> pinned-host read of its ~1.3 KB result head is
+// written by the GPU straight into the mapped host buffer (round 2 timeline: ~30 us around
+// the copy node).  Both pointers must be device-addressable (device or pinned host memory).
+__global__ void __launch_bounds__(256)
+copy_bytes(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, size_t bytes) {
+    const size_t n16 = ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) ? bytes / 16 : 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+        ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+    for (size_t i = n16 * 16 + (size_t)blockIdx.x * 256 + threadIdx.x; i < bytes; i += (size_t)gridDim.x * 256)
+        dst[i] = src[i];
+}
+
+int launch_copy(pano_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!bytes) return PANO_OK;
+    const size_t items = ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) ? bytes / 16 + 16 : bytes;
+    const unsigned blocks = (unsigned)std::min<size_t>((items + 255) / 256, 1024);
+    copy_bytes<<<blocks, 256, 0, ctx->stream>>>((const uint8_t *)src, (uint8_t *)dst, bytes);
+    PANO_LAUNCH_CHECK(ctx, "copy_bytes");
+    return PANO_OK;
+}

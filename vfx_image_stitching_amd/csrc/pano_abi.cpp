@@ -45,6 +45,20 @@ int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need) {
     return PANO_OK;
 }
 
+// The device address of p when the GPU may dereference it (device memory, or pinned host
+// memory mapped into the device's address space), else nullptr.
+static void *device_address(void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();               // pageable host memory: clear the sticky error
+        return nullptr;
+    }
+    if (a.type == hipMemoryTypeDevice) return p;
+    // pinned host memory: only when the GPU sees it at the same address (no offset to trust)
+    if (a.type == hipMemoryTypeHost && a.devicePointer == p) return p;
+    return nullptr;
+}
+
 extern "C" {
 
 const char *pano_version(void) { return "libpano 0.1 gfx950"; }
@@ -103,7 +117,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
-                    ctx->boxslots, ctx->hmscratch};
+                    ctx->boxslots, ctx->hmscratch, ctx->dorder};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
@@ -476,6 +490,13 @@ int pano_graph_launch_sync(pano_ctx *ctx, pano_graph *g, void *stream) {
 
 int pano_copy_async(pano_ctx *ctx, void *dst, const void *src, size_t bytes) {
     if (!ctx || (bytes && (!dst || !src))) return PANO_E_ARG;
+    // small copies run as a kernel: a graph kernel node, no blit / SDMA node; large ones stay
+    // hipMemcpyAsync.  Only when both pointers are device memory or registered (pinned) host
+    // memory with a device address -- anything else (pageable memory) takes the memcpy path
+    if (bytes && bytes <= (1u << 20)) {
+        void *dd = device_address(dst), *ds = device_address(const_cast<void *>(src));
+        if (dd && ds) return launch_copy(ctx, dd, ds, bytes);
+    }
     if (bytes) PANO_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream));
     return PANO_OK;
 }

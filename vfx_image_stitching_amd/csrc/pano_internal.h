@@ -85,6 +85,7 @@ struct pano_ctx {
     size_t ext_bytes = 0;
     RawKp *raw_sorted = nullptr;
     uint32_t *sorted = nullptr; size_t sorted_bytes = 0;   // per-frame sorted raw indices
+    int32_t *dorder = nullptr; size_t dorder_bytes = 0;    // descriptor processing order
     float *taps = nullptr;               // device Gaussian taps (f32), per level [L][PANO_MAX_TAPS]
     float taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];    // what *taps holds
     bool taps_valid = false;
@@ -170,6 +171,7 @@ int pano_grow(pano_ctx *ctx, void **p, size_t *have, size_t need);
 
 // ---- host launchers implemented in the .hip translation units
 int launch_fill(pano_ctx *ctx, void *dst, uint8_t value, size_t bytes);   // graph-safe memset
+int launch_copy(pano_ctx *ctx, void *dst, const void *src, size_t bytes);  // kernel copy (device-addressable)
 int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, int h, int w,
                        const double *h_focal, uint8_t *colnz);
 // full = true materialises every Gaussian level (stage access, pano_sift_pyramid); the
