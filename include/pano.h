@@ -332,6 +332,23 @@ int pano_blend_two(pano_ctx *ctx, const uint8_t *d_A, int hA, int wA, const uint
 int pano_gray_bbox(pano_ctx *ctx, const uint8_t *d_img, int H, int W, int black_threshold,
                    int32_t *d_bbox);
 
+/* ---------------------------------------------------------------- JPEG
+ * The reference reads every frame with cv2.imread (image_stitching_sift.py:282,
+ * image_stitching_harris.py:394): libjpeg-turbo's default decode.  pano_jpeg_decode runs it on
+ * the GPU for a batch of baseline (SOF0/SOF1, Huffman, 8-bit) files of one size, 1 or 3
+ * components, 4:4:4 / 4:2:2 / 4:2:0, no restart intervals: islow IDCT, fancy upsampling,
+ * fixed-point YCbCr -> RGB, bit-identical to libjpeg-turbo (and PIL / cv2.imread).
+ *   h_bufs[i], lens[i]: the files in host memory (read on the host for headers only; the
+ *                       entropy-coded bytes are uploaded in one copy);
+ *   d_bgr:              device u8 [n][h][w][3] BGR (cv2.imread's channel order);
+ *   d_status:           optional device int32 [n]: per-frame PANO_OK, PANO_E_ARG (corrupt or
+ *                       truncated scan) or PANO_E_UNSUPPORTED (a marker inside the scan).
+ * Header problems (not a JPEG, progressive, arithmetic coding, other sampling, size differs
+ * from h x w) fail the call itself.  pano_jpeg_info is host-only. */
+int pano_jpeg_info(const uint8_t *h_buf, size_t len, int *h, int *w, int *ncomp);
+int pano_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *h_bufs, const size_t *lens,
+                     uint8_t *d_bgr, int h, int w, int32_t *d_status);
+
 /* ---------------------------------------------------------------- live kernel timing
  * pano_prof_enable(ctx, k) records a hipEvent pair on the context's stream around every
  * launch of kernel class k (PANO_K_*; PANO_K_ALL = every class; -1 = off).
@@ -357,7 +374,8 @@ int pano_gray_bbox(pano_ctx *ctx, const uint8_t *d_img, int H, int W, int black_
 #define PANO_K_H_NMS 17
 #define PANO_K_H_SELECT 18
 #define PANO_K_H_DESC 19
-#define PANO_K_ALL 20
+#define PANO_K_JPEG 20
+#define PANO_K_ALL 21
 int pano_prof_enable(pano_ctx *ctx, int kernel_class);
 int pano_prof_read(pano_ctx *ctx, int kernel_class, int *launches, double *total_ms,
                    double *min_ms, double *max_ms);

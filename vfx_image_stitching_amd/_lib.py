@@ -135,6 +135,8 @@ SIGNATURES = {
     "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),
     "pano_blend_two": (_I, [_P, _P, _I, _I, _P, _I, _I, _PI32, _D, _P]),
     "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),
+    "pano_jpeg_info": (_I, [_P, ctypes.c_size_t, _PI32, _PI32, _PI32]),
+    "pano_jpeg_decode": (_I, [_P, _I, _P, _P, _P, _I, _I, _P]),
     "pano_prof_enable": (_I, [_P, _I]),
     "pano_prof_read": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int), _PD, _PD, _PD]),
     "pano_graph_begin": (_I, [_P]),
@@ -150,7 +152,7 @@ SIGNATURES = {
 KERNELS = ["cyl_scatter", "cyl_gather", "blur_level", "extrema_localize", "orientation",
            "sort_dedup", "descriptor", "row_norms", "dist_mfma", "dist_direct", "reduce_parts",
            "pair_shifts", "composite_step", "gray_bbox", "to_gray", "structure_blur", "response",
-           "nms", "select_top", "harris_desc"]
+           "nms", "select_top", "harris_desc", "jpeg_decode"]
 K_ALL = len(KERNELS)
 
 _lib = None

@@ -1,0 +1,402 @@
+// jpeg_core.h -- baseline JPEG decode: the per-thread pieces the HIP
+// kernels of jpeg.hip run, written once as __host__ __device__ functions so that
+// tools/jpeg_sim.cpp can replay the same arithmetic on the CPU while the kernels are developed.
+//
+// What is being reproduced: the reference reads every frame with cv2.imread
+// (image_stitching_sift.py:282, image_stitching_harris.py:394); the harness decodes with
+// PIL (vfx_image_stitching_amd/data.py), which SURVEY.md section 8(c) measured pixel-identical
+// to cv2.imread on these files.  Both are libjpeg-turbo with its defaults:
+//   - Huffman entropy decoding, sequential baseline / extended 8-bit DCT (jdhuff.c),
+//   - the accurate integer inverse DCT, JDCT_ISLOW (jidctint.c: 13-bit constants, 2 extra
+//     bits after the column pass, range limit through a 1024-entry wrap table),
+//   - "fancy" triangular chroma upsampling for h2v1 / h2v2 (jdsample.c) with the context rows
+//     of jdmainct.c (rows above the top / below the bottom replicate the edge row),
+//   - YCbCr -> RGB with 16-bit fixed-point tables (jdcolor.c).
+// Everything here is integer arithmetic and is bit-exact by construction; tests compare the
+// GPU output with PIL's decode byte for byte.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+namespace pj {
+
+constexpr int kMaxComp = 3;     // gray or YCbCr
+constexpr int kMaxBpm = 10;     // blocks per MCU (JPEG limit)
+constexpr int kSubBits = 1024;  // bits per subsequence of the self-synchronising decode
+constexpr int kChunk = 4096;    // stuffed bytes per unstuff chunk
+constexpr int kStreamPad = 64;  // zero bytes after each unstuffed stream
+
+// One Huffman table in decode form (jdhuff.c jpeg_make_d_derived_tbl restated).
+struct Huff {
+    uint16_t lut[512];    // 9-bit peek -> (code length << 8) | symbol; 0 = code longer than 9
+    int32_t maxcode[18];  // per length 1..16: largest code of that length, -1 none
+    int32_t valoff[18];   // symbol index = valoff[l] + code
+    uint8_t vals[256];
+};
+
+// Everything a kernel needs about one frame (built on the host by jpeg_plan).
+struct Frame {
+    int32_t h, w, ncomp;
+    int32_t hmax, vmax;
+    int32_t mcus_x, mcus_y, bpm, total_blocks;
+    int32_t comp_h[kMaxComp], comp_v[kMaxComp];     // sampling factors (1/1 for a gray scan)
+    int32_t comp_bw[kMaxComp], comp_bh[kMaxComp];   // block grid of each component plane
+    int32_t comp_dw[kMaxComp], comp_dh[kMaxComp];   // libjpeg downsampled_width / _height
+    int32_t dc_tab[kMaxComp], ac_tab[kMaxComp];     // indices into the batch's table array
+    int32_t q_tab[kMaxComp];                        // index into the batch's quant array
+    int8_t mcu_comp[kMaxBpm], mcu_bx[kMaxBpm], mcu_by[kMaxBpm];
+    int32_t upsample;     // 0: 4:4:4 or gray, 1: h2v1, 2: h2v2
+    uint64_t coef_off[kMaxComp];   // int16 element offset of the component's coefficients
+    uint64_t samp_off[kMaxComp];   // byte offset of the component's sample plane
+    uint64_t src_off;     // stuffed entropy-coded segment: byte offset in the upload
+    uint32_t src_len;
+    uint32_t chunk0, nchunk;       // unstuff chunks
+    uint64_t bits_off;    // unstuffed stream: byte offset (16-aligned) in the stream arena
+    uint32_t sub0, nsub;  // subsequences reserved (from the stuffed length, an upper bound)
+    uint32_t warm;        // warm-up window (bits) of the subsequence start search
+};
+
+// ---------------------------------------------------------------------------------------------
+// Bit reader over an unstuffed stream (big-endian bytes read as 32-bit words).
+struct Bits {
+    const uint32_t *w;
+    uint32_t nw;       // words readable; beyond them the stream reads as zeros (libjpeg pads
+                       // with zeros after the last marker, jdhuff.c jpeg_fill_bit_buffer)
+    uint32_t wi;       // next word to load
+    int cnt;           // valid bits in buf
+    uint64_t buf;      // left-aligned: the next bit is bit 63
+
+    __host__ __device__ __forceinline__ uint32_t load(uint32_t i) const {
+        return i < nw ? __builtin_bswap32(w[i]) : 0u;
+    }
+    __host__ __device__ __forceinline__ void fill() {   // requires cnt <= 32
+        buf |= (uint64_t)load(wi++) << (32 - cnt);
+        cnt += 32;
+    }
+    __host__ __device__ __forceinline__ void init(const uint32_t *words, uint32_t nwords, uint32_t pos) {
+        w = words; nw = nwords; wi = pos >> 5; buf = 0; cnt = 0;
+        fill(); fill();
+        const int s = (int)(pos & 31);
+        buf <<= s; cnt -= s;
+    }
+    __host__ __device__ __forceinline__ void ensure32() { if (cnt < 32) fill(); }
+    __host__ __device__ __forceinline__ uint32_t pos() const { return wi * 32u - (uint32_t)cnt; }
+    __host__ __device__ __forceinline__ void skip(int n) { buf <<= n; cnt -= n; }
+    __host__ __device__ __forceinline__ int get(int n) {   // 1 <= n <= 16
+        const int v = (int)(buf >> (64 - n));
+        skip(n);
+        return v;
+    }
+};
+
+// Decode one Huffman symbol (jdhuff.c jpeg_huff_decode).  An invalid code consumes 16 bits
+// and returns -1 (libjpeg warns and yields symbol 0); that only happens off-sync.
+__host__ __device__ __forceinline__ int huff_decode(const Huff *T, Bits &br) {
+    const uint32_t p = (uint32_t)(br.buf >> 48);
+    const uint32_t e = T->lut[p >> 7];
+    if (e) {
+        br.skip((int)(e >> 8));
+        return (int)(e & 0xFF);
+    }
+    for (int l = 10; l <= 16; ++l) {
+        const int32_t code = (int32_t)(p >> (16 - l));
+        if (code <= T->maxcode[l]) {
+            br.skip(l);
+            return T->vals[(T->valoff[l] + code) & 0xFF];
+        }
+    }
+    br.skip(16);
+    return -1;
+}
+
+// HUFF_EXTEND (jdhuff.h)
+__host__ __device__ __forceinline__ int huff_extend(int v, int s) {
+    return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v;
+}
+
+// Decoder state at a codeword boundary: bit position, block of the MCU, zig-zag index
+// (0 = the block's DC code is next).  Two decodes that reach the same state decode the same
+// symbols from there on: that is what the self-synchronising passes compare.
+__host__ __device__ __forceinline__ uint64_t pack_state(uint32_t pos, int b, int k) {
+    return (uint64_t)pos << 16 | (uint64_t)(uint32_t)b << 8 | (uint64_t)(uint32_t)k;
+}
+__host__ __device__ __forceinline__ uint32_t state_pos(uint64_t s) { return (uint32_t)(s >> 16); }
+__host__ __device__ __forceinline__ int state_b(uint64_t s) { return (int)((s >> 8) & 0xFF); }
+__host__ __device__ __forceinline__ int state_k(uint64_t s) { return (int)(s & 0xFF); }
+
+// Per-subsequence statistics of a decode: DC codes seen (= blocks started) and the sum of
+// the DC differences per component (the DC predictor is a running sum, jdhuff.c decode_mcu).
+struct SubStats {
+    int32_t blocks;
+    int32_t dc[kMaxComp];
+};
+
+// Sinks for walk(): what to do with each decoded value.
+struct SinkNone {
+    __host__ __device__ __forceinline__ bool dc(int, int) { return true; }
+    __host__ __device__ __forceinline__ void ac(int, int) {}
+    __host__ __device__ __forceinline__ void end_block() {}
+};
+struct SinkCount {
+    // per-component sums kept in three scalars (a dynamically indexed array would live in
+    // scratch memory on the GPU)
+    int32_t blocks = 0, d0 = 0, d1 = 0, d2 = 0;
+    __host__ __device__ __forceinline__ bool dc(int c, int diff) {
+        ++blocks;
+        d0 += c == 0 ? diff : 0;
+        d1 += c == 1 ? diff : 0;
+        d2 += c == 2 ? diff : 0;
+        return true;
+    }
+    __host__ __device__ __forceinline__ void ac(int, int) {}
+    __host__ __device__ __forceinline__ void end_block() {}
+    __host__ __device__ __forceinline__ SubStats stats() const {
+        SubStats s;
+        s.blocks = blocks; s.dc[0] = d0; s.dc[1] = d1; s.dc[2] = d2;
+        return s;
+    }
+};
+
+// The zig-zag -> natural order map with libjpeg's 16 guard entries (jutils.c
+// jpeg_natural_order: a corrupt run past 63 lands on 63).
+__host__ __device__ __forceinline__ int natural_order(int k) {
+    // Row-major position of the k-th zig-zag coefficient, computed (no table) from the
+    // anti-diagonal it lies on: diagonal d holds k in [d(d+1)/2 ...) for d < 8 and mirrors
+    // for the lower-right half.
+    if (k > 63) return 63;
+    int d, i;
+    if (k < 36) {                       // upper-left triangle, diagonals 0..7
+        d = 0; while ((d + 1) * (d + 2) / 2 <= k) ++d;
+        i = k - d * (d + 1) / 2;        // index along the diagonal
+        const int r = (d & 1) ? i : d - i;
+        return r * 8 + (d - r);
+    }
+    const int kk = 63 - k;              // mirror: lower-right triangle
+    d = 0; while ((d + 1) * (d + 2) / 2 <= kk) ++d;
+    i = kk - d * (d + 1) / 2;
+    const int r = (d & 1) ? i : d - i;  // position in the mirrored block
+    return 63 - (r * 8 + (d - r));
+}
+
+// Walk the codewords that start in [start, end): from state `start` decode until the bit
+// position reaches `end`; returns the state at the first boundary >= end.  The sink sees
+// every DC difference (dc returns false to stop early) and AC coefficient.  dcT / acT: the
+// DC / AC tables of components 0..2.
+template <class Sink>
+__host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_t nwords, uint64_t start,
+                                                  uint32_t end, const Huff *dcT, const Huff *acT,
+                                                  const int8_t *mcu_comp, int bpm, Sink &sink) {
+    Bits br;
+    br.init(words, nwords, state_pos(start));
+    int b = state_b(start), k = state_k(start);
+    uint32_t guard = end - state_pos(start) + 64;   // every codeword consumes >= 1 bit
+    while (br.pos() < end && guard--) {
+        br.ensure32();
+        const int c = mcu_comp[b];
+        if (k == 0) {
+            int s = huff_decode(dcT + c, br);
+            int diff = 0;
+            if (s > 0) {
+                if (s > 16) s = 16;
+                diff = huff_extend(br.get(s), s);
+            }
+            if (!sink.dc(c, diff)) break;
+            k = 1;
+        } else {
+            int rs = huff_decode(acT + c, br);
+            if (rs < 0) rs = 0;
+            const int r = rs >> 4, s = rs & 15;
+            if (s) {
+                k += r;
+                sink.ac(k, huff_extend(br.get(s), s));
+                ++k;
+            } else if (r == 15) {
+                k += 16;
+            } else {
+                k = 64;
+            }
+        }
+        if (k >= 64) {
+            k = 0;
+            if (++b == bpm) b = 0;
+            sink.end_block();
+        }
+    }
+    return pack_state(br.pos(), b, k);
+}
+
+// Block index (MCU order) -> coefficient block address (int16 elements).
+__host__ __device__ __forceinline__ uint64_t block_addr(const Frame &F, int32_t blk) {
+    const int32_t m = blk / F.bpm, bb = blk - m * F.bpm;
+    const int32_t mx = m % F.mcus_x, my = m / F.mcus_x;
+    const int c = F.mcu_comp[bb];
+    const int32_t bx = mx * F.comp_h[c] + F.mcu_bx[bb];
+    const int32_t by = my * F.comp_v[c] + F.mcu_by[bb];
+    return F.coef_off[c] + ((uint64_t)by * F.comp_bw[c] + bx) * 64;
+}
+
+// Writes coefficients of the blocks a subsequence decodes (natural order, DC predicted).
+struct SinkWrite {
+    int16_t *coef;
+    const Frame *F;
+    const uint8_t *nat;           // natural_order(k) for k < 80 (a table in LDS / host memory)
+    int32_t blk;                  // current block index (MCU order)
+    int32_t p0, p1, p2;           // DC predictors of components 0..2
+    uint64_t addr;                // current block's address
+    bool live;
+    __host__ __device__ __forceinline__ bool dc(int c, int diff) {
+        if (blk >= F->total_blocks) return false;
+        p0 += c == 0 ? diff : 0;
+        p1 += c == 1 ? diff : 0;
+        p2 += c == 2 ? diff : 0;
+        addr = block_addr(*F, blk);
+        live = true;
+        coef[addr] = (int16_t)(c == 0 ? p0 : (c == 1 ? p1 : p2));
+        return true;
+    }
+    __host__ __device__ __forceinline__ void ac(int k, int v) {
+        if (live) coef[addr + nat[k < 80 ? k : 79]] = (int16_t)v;
+    }
+    __host__ __device__ __forceinline__ void end_block() { ++blk; live = false; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Inverse DCT: jidctint.c jpeg_idct_islow (CONST_BITS 13, PASS1_BITS 2), 64-bit JLONG math.
+__host__ __device__ __forceinline__ int range_limit_idct(int64_t x) {
+    // sample_range_limit + CENTERJSAMPLE indexed by (x & RANGE_MASK) (jdmaster.c
+    // prepare_range_limit_table): [0,128) -> x+128, [128,512) -> 255, [512,896) -> 0,
+    // [896,1024) -> x-896 (i.e. x+128 for x in [-128,0)).
+    const int i = (int)x & 1023;
+    if (i < 128) return i + 128;
+    if (i < 512) return 255;
+    if (i < 896) return 0;
+    return i - 896;
+}
+
+// One 8-point pass.  in[0..7] (stride s), out8: the 8 results before descale.
+__host__ __device__ __forceinline__ void idct8(const int64_t *z, int64_t *o) {
+    const int64_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373,
+                  F1175 = 9633, F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819,
+                  F2562 = 20995, F3072 = 25172;
+    // even part
+    int64_t z2 = z[2], z3 = z[6];
+    int64_t z1 = (z2 + z3) * F0541;
+    int64_t tmp2 = z1 + z3 * (-F1847);
+    int64_t tmp3 = z1 + z2 * F0765;
+    int64_t tmp0 = (z[0] + z[4]) * 8192;
+    int64_t tmp1 = (z[0] - z[4]) * 8192;
+    const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    // odd part
+    tmp0 = z[7]; tmp1 = z[5]; tmp2 = z[3]; tmp3 = z[1];
+    z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2;
+    int64_t z4 = tmp1 + tmp3;
+    const int64_t z5 = (z3 + z4) * F1175;
+    tmp0 *= F0298; tmp1 *= F2053; tmp2 *= F3072; tmp3 *= F1501;
+    z1 *= -F0899; z2 *= -F2562; z3 *= -F1961; z4 *= -F0390;
+    z3 += z5; z4 += z5;
+    tmp0 += z1 + z3; tmp1 += z2 + z4; tmp2 += z2 + z3; tmp3 += z1 + z4;
+    o[0] = tmp10 + tmp3; o[7] = tmp10 - tmp3;
+    o[1] = tmp11 + tmp2; o[6] = tmp11 - tmp2;
+    o[2] = tmp12 + tmp1; o[5] = tmp12 - tmp1;
+    o[3] = tmp13 + tmp0; o[4] = tmp13 - tmp0;
+}
+
+__host__ __device__ __forceinline__ int64_t descale(int64_t x, int n) {
+    return (x + ((int64_t)1 << (n - 1))) >> n;
+}
+
+// Column pass of one column: coef column c (natural order) x quant -> ws column (int).
+__host__ __device__ __forceinline__ void idct_col(const int16_t *blk, const uint16_t *q, int c, int32_t *ws) {
+    int64_t z[8], o[8];
+    for (int r = 0; r < 8; ++r) z[r] = (int64_t)((int32_t)blk[r * 8 + c] * (int32_t)q[r * 8 + c]);
+    idct8(z, o);
+    for (int r = 0; r < 8; ++r) ws[r * 8 + c] = (int32_t)descale(o[r], 11);
+}
+// Row pass of one row: ws row r -> 8 samples.
+__host__ __device__ __forceinline__ void idct_row(const int32_t *ws, int r, uint8_t *out) {
+    int64_t z[8], o[8];
+    for (int c = 0; c < 8; ++c) z[c] = ws[r * 8 + c];
+    idct8(z, o);
+    for (int c = 0; c < 8; ++c) out[c] = (uint8_t)range_limit_idct(descale(o[c], 18));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Upsampling (jdsample.c) and colour conversion (jdcolor.c), per output pixel.
+// Chroma sample at output (x, y) of a component plane p (pitch ppitch) with downsampled size
+// (dw, dh).  mode 0: full size; 1: h2v1 fancy; 2: h2v2 fancy.
+__host__ __device__ __forceinline__ int chroma_at(const uint8_t *p, int ppitch, int dw, int dh, int mode, int x, int y) {
+    if (mode == 0) return p[(size_t)y * ppitch + x];
+    if (mode == 1) {
+        // h2v1_fancy_upsample: first output = in[0], last output = in[dw-1]; else 3/4 nearer
+        // + 1/4 farther, biased +1 (left) / +2 (right).
+        const uint8_t *row = p + (size_t)y * ppitch;
+        const int j = x >> 1;
+        if ((x & 1) == 0) {
+            if (j == 0) return row[0];
+            return (row[j] * 3 + row[j - 1] + 1) >> 2;
+        }
+        if (j == dw - 1) return row[j];
+        return (row[j] * 3 + row[j + 1] + 2) >> 2;
+    }
+    // h2v2_fancy_upsample: colsum = 3 * nearer row + farther row (rows outside replicate the
+    // edge row, jdmainct.c context pointers); output = (3 * this + neighbour colsum + 8 | 7) >> 4.
+    const int i = y >> 1;
+    int i1 = (y & 1) ? i + 1 : i - 1;
+    if (i1 < 0) i1 = 0;
+    if (i1 > dh - 1) i1 = dh - 1;
+    const uint8_t *r0 = p + (size_t)i * ppitch, *r1 = p + (size_t)i1 * ppitch;
+    const int j = x >> 1;
+    const int cs = r0[j] * 3 + r1[j];
+    if ((x & 1) == 0) {
+        if (j == 0) return (cs * 4 + 8) >> 4;
+        return (cs * 3 + (r0[j - 1] * 3 + r1[j - 1]) + 8) >> 4;
+    }
+    if (j == dw - 1) return (cs * 4 + 7) >> 4;
+    return (cs * 3 + (r0[j + 1] * 3 + r1[j + 1]) + 7) >> 4;
+}
+
+__host__ __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// ycc_rgb_convert (jdcolor.c build_ycc_rgb_table, SCALEBITS 16) -> B, G, R.
+__host__ __device__ __forceinline__ void ycc_to_bgr(int y, int cb, int cr, uint8_t *bgr) {
+    const int x_cb = cb - 128, x_cr = cr - 128;
+    const int cr_r = (91881 * x_cr + 32768) >> 16;
+    const int cb_b = (116130 * x_cb + 32768) >> 16;
+    const int g = (-22554 * x_cb + 32768 + (-46802) * x_cr) >> 16;
+    bgr[0] = (uint8_t)clamp255(y + cb_b);
+    bgr[1] = (uint8_t)clamp255(y + g);
+    bgr[2] = (uint8_t)clamp255(y + cr_r);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host side: marker parsing (jdmarker.c restated for the markers a baseline file carries) and
+// the decode-form tables.
+struct Parsed {
+    int h = 0, w = 0, ncomp = 0, restart = 0, sof = 0;
+    int comp_id[kMaxComp] = {0}, comp_h[kMaxComp] = {0}, comp_v[kMaxComp] = {0}, comp_q[kMaxComp] = {0};
+    int comp_dc[kMaxComp] = {0}, comp_ac[kMaxComp] = {0};
+    uint16_t qt[4][64];            // natural order
+    bool qt_ok[4] = {false, false, false, false};
+    uint8_t hbits[2][4][17];       // [class][id][length 1..16]
+    uint8_t hvals[2][4][256];
+    bool h_ok[2][4] = {{false, false, false, false}, {false, false, false, false}};
+    const uint8_t *ecs = nullptr;  // entropy-coded segment (stuffed bytes)
+    size_t ecs_len = 0;
+};
+
+// Standard tables of JPEG Annex K.3 (libjpeg uses them when a file has no DHT).
+void std_huff(int cls, int id, uint8_t *bits17, uint8_t *vals256);
+// Returns 0 or a PANO_E_* code; *err gets a message.
+int parse(const uint8_t *buf, size_t len, Parsed *out, std::string *err);
+// Builds the decode form of a (bits, vals) table; false if the code lengths are invalid.
+bool make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *out);
+// Frame geometry (MCU layout, component planes, upsampling mode) of a parsed file; the
+// arena offsets and table indices are filled in by the caller.
+int plan_frame(const Parsed &P, Frame *F, std::string *err);
+
+}  // namespace pj

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "jpeg_core.h"
 #include "pano_internal.h"
 
 int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_params *p);
@@ -120,6 +121,9 @@ int pano_ctx_destroy(pano_ctx *ctx) {
                     ctx->boxslots, ctx->hmscratch, ctx->dorder};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (ctx->jscratch) (void)hipFree(ctx->jscratch);
+    if (ctx->jpin) (void)hipHostFree(ctx->jpin);
+    if (ctx->jev) (void)hipEventDestroy(ctx->jev);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
     delete ctx;
     return PANO_OK;
@@ -391,6 +395,30 @@ int pano_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_
 int pano_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox) {
     if (!ctx) return PANO_E_ARG;
     return launch_gray_bbox(ctx, img, H, W, thr, bbox);
+}
+
+int pano_jpeg_info(const uint8_t *buf, size_t len, int *h, int *w, int *ncomp) {
+    pj::Parsed P;
+    std::string err;
+    int rc = pj::parse(buf, len, &P, &err);
+    if (rc) return rc;
+    pj::Frame F;
+    rc = pj::plan_frame(P, &F, &err);
+    if (rc) return rc;
+    if (h) *h = P.h;
+    if (w) *w = P.w;
+    if (ncomp) *ncomp = P.ncomp;
+    return PANO_OK;
+}
+
+int pano_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const size_t *lens, uint8_t *bgr,
+                     int h, int w, int32_t *status) {
+    if (!ctx) return PANO_E_ARG;
+    if (n <= 0 || !bufs || !lens || !bgr || h <= 0 || w <= 0)
+        return pano_fail(ctx, PANO_E_ARG, "pano_jpeg_decode: bad arguments");
+    if (ctx->capturing)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_jpeg_decode reads host files: not capturable");
+    return launch_jpeg_decode(ctx, n, bufs, lens, bgr, h, w, status);
 }
 
 int pano_prof_enable(pano_ctx *ctx, int kernel_class) {

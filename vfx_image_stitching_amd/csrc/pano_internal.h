@@ -54,7 +54,7 @@ struct LevelView {
 enum PanoKernel {
     PK_CYL_SCATTER = 0, PK_CYL_GATHER, PK_BLUR, PK_EXTREMA, PK_ORIENT, PK_SORT, PK_DESC,
     PK_NORMS, PK_DIST_MFMA, PK_DIST_DIRECT, PK_REDUCE, PK_PAIR_SHIFTS, PK_COMPOSITE, PK_BBOX,
-    PK_H_GRAY, PK_H_BLUR, PK_H_RESP, PK_H_NMS, PK_H_SELECT, PK_H_DESC, PK_COUNT
+    PK_H_GRAY, PK_H_BLUR, PK_H_RESP, PK_H_NMS, PK_H_SELECT, PK_H_DESC, PK_JPEG, PK_COUNT
 };
 
 struct ProfState {
@@ -101,6 +101,11 @@ struct pano_ctx {
     void *hscratch = nullptr; size_t hscratch_bytes = 0;
     // ---- blend scratch
     void *bscratch = nullptr; size_t bscratch_bytes = 0;
+    // ---- JPEG decode (jpeg.hip): device scratch, pinned upload staging and the event that
+    // says when the last upload out of the staging buffer has completed
+    void *jscratch = nullptr; size_t jscratch_bytes = 0;
+    void *jpin = nullptr; size_t jpin_bytes = 0;
+    hipEvent_t jev = nullptr;
     // ---- side stream: the small-octave blur tail runs there, overlapped with the extrema
     // scan of the large octaves (fork / join by events; see launch_sift_pyramid)
     hipStream_t side = nullptr;
@@ -242,6 +247,9 @@ int launch_composite_seq(pano_ctx *ctx, const uint8_t *frames, const uint8_t *co
 int launch_blend_two(pano_ctx *ctx, const uint8_t *A, int hA, int wA, const uint8_t *B, int hB,
                      int wB, const int32_t *geom, double overlap, uint8_t *out);
 int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, int32_t *bbox);
+// Baseline JPEG files in host memory -> u8 BGR [n][h][w][3] on the device (jpeg.hip).
+int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const size_t *lens, uint8_t *bgr,
+                       int h, int w, int32_t *status);
 
 // ---- device helpers
 // XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"):
