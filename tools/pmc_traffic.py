@@ -26,6 +26,7 @@ CLASSES = [
     # fills the slots the scatter pair (cyl_scatter, cyl_gather) named first
     (r"^(cyl_scatter|cyl_columns)", "cyl_scatter"),
     (r"^(cyl_gather|cyl_inverse)", "cyl_gather"),
+    (r"^jpeg_", "jpeg_decode"),
 ]
 
 

@@ -33,6 +33,14 @@ def load_set(name: str, data_dir: str = DATA_DIR):
     return names, frames, z["focals"].astype(np.float64), int(z["margin"])
 
 
+def load_set_jpegs(name: str, data_dir: str = DATA_DIR):
+    """-> (names, JPEG file bytes) in pano.txt order: what cv2.imread reads
+    (image_stitching_sift.py:282), for the GPU decode (vfx_image_stitching_amd.jpeg)."""
+    z = np.load(os.path.join(data_dir, f"{name}_frames.npz"), allow_pickle=False)
+    names = [str(s) for s in z["order"]]
+    return names, [z[f"jpg_{n}"].tobytes() for n in names]
+
+
 def pair_frame(name: str, a: str, b: str, data_dir: str = DATA_DIR):
     """Two named frames of a set with their focals (config 2: prtn00 + prtn01)."""
     names, frames, focals, _ = load_set(name, data_dir)
