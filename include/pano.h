@@ -348,6 +348,14 @@ int pano_gray_bbox(pano_ctx *ctx, const uint8_t *d_img, int H, int W, int black_
 int pano_jpeg_info(const uint8_t *h_buf, size_t len, int *h, int *w, int *ncomp);
 int pano_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *h_bufs, const size_t *lens,
                      uint8_t *d_bgr, int h, int w, int32_t *d_status);
+/* cv2.imwrite(path, panorama) (image_stitching_sift.py:386; OpenCV's default quality 95): the
+ * u8 BGR image at d_bgr (h rows of w pixels, row pitch `pitch` bytes -- a crop view of a
+ * canvas works as is) encoded on the GPU as a baseline JFIF file, YCbCr 4:2:0, byte-identical
+ * to libjpeg-turbo's default encoder (PIL save(quality=q)).  Synchronous: the file is written to
+ * h_out (capacity cap) and its length to *out_len; PANO_E_OVERFLOW (with *out_len set) when
+ * cap is too small. */
+int pano_jpeg_encode(pano_ctx *ctx, const uint8_t *d_bgr, int h, int w, int64_t pitch, int quality,
+                     uint8_t *h_out, size_t cap, size_t *out_len);
 
 /* ---------------------------------------------------------------- live kernel timing
  * pano_prof_enable(ctx, k) records a hipEvent pair on the context's stream around every

@@ -103,7 +103,7 @@ def test_sim_decode_equals_pil_on_reference_frames(jpeg_sim, tmp_path, name):
         assert st["blocks"] >= st["total_blocks"]
         fixes += st["fixes"]
     # the start search resolves almost every subsequence from its candidates
-    assert fixes <= 0.002 * 20000
+    assert fixes <= 0.002 * 40000
 
 
 @pytest.mark.parametrize("i", range(len(VARIANTS)))
@@ -115,11 +115,12 @@ def test_sim_decode_equals_pil_on_variants(jpeg_sim, tmp_path, i):
 
 
 def test_sim_without_warmup_still_exact(jpeg_sim, tmp_path):
-    """Every candidate wrong (no warm-up window): the resolve fallback decodes every
-    subsequence from its true start, and the result is still exact."""
+    """No warm-up window (every warm candidate a guess at its subsequence's first bit): the
+    fix candidates and the resolve fallback decode the subsequences from their true starts,
+    and the result is still exact."""
     buf = _set_jpegs("parrington")[0]
     st, out = _sim(jpeg_sim, buf, tmp_path, env={"JPEG_SIM_W": "0"})
-    assert st["fixes"] >= st["nsub"] // 2
+    assert st["fix_slots"] + st["fixes"] >= st["nsub"] // 2 and st["fixes"] > 0
     assert np.array_equal(out, _pil_bgr(buf))
 
 
@@ -211,3 +212,66 @@ def test_gpu_decode_refuses_mixed_sizes(gpu):
     from vfx_image_stitching_amd._lib import PanoError
     with pytest.raises(PanoError):
         jpeg.decode_batch([_encode(_texture(32, 32, 0)), _encode(_texture(32, 48, 0))])
+
+
+# --------------------------------------------------------------------------------- encoder
+# cv2.imwrite(path, panorama) (image_stitching_sift.py:386): libjpeg-turbo's default encoder at
+# OpenCV's default quality 95; PIL's save(quality=q) runs the same encoder, byte for byte.
+ENC_CASES = [(37, 53, 95), (64, 64, 95), (16, 16, 75), (100, 33, 50), (1, 1, 95), (2, 3, 95),
+             (482, 700, 95), (17, 15, 10), (31, 47, 100)]
+
+
+def _enc_image(h, w, seed):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    a = 128 + 60 * np.sin(xx / 7.0)[..., None] * np.cos(yy / 5.0)[..., None] + rng.normal(0, 20, (h, w, 3))
+    return np.clip(a, 0, 255).astype(np.uint8)          # BGR
+
+
+def _pil_encode_bgr(bgr, quality):
+    return _encode(np.ascontiguousarray(bgr[..., ::-1]), quality=quality)
+
+
+@pytest.fixture(scope="module")
+def jpeg_enc_sim(tmp_path_factory):
+    out = tmp_path_factory.mktemp("jesim") / "jpeg_enc_sim"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-o", str(out),
+                    os.path.join(ROOT, "tools", "jpeg_enc_sim.cpp"),
+                    os.path.join(ROOT, "vfx_image_stitching_amd", "csrc", "jpeg_host.cpp")],
+                   check=True, capture_output=True)
+    return str(out)
+
+
+@pytest.mark.parametrize("case", range(len(ENC_CASES)))
+def test_sim_encode_equals_pil_bytes(jpeg_enc_sim, tmp_path, case):
+    h, w, q = ENC_CASES[case]
+    img = _enc_image(h, w, case)
+    (tmp_path / "in.bgr").write_bytes(img.tobytes())
+    subprocess.run([jpeg_enc_sim, str(tmp_path / "in.bgr"), str(h), str(w), str(q), str(tmp_path / "o.jpg")],
+                   check=True, capture_output=True)
+    assert (tmp_path / "o.jpg").read_bytes() == _pil_encode_bgr(img, q)
+
+
+@pytest.mark.gpu
+def test_gpu_encode_equals_pil_bytes(gpu):
+    import torch
+    from vfx_image_stitching_amd import jpeg
+    for case, (h, w, q) in enumerate(ENC_CASES):
+        img = _enc_image(h, w, case)
+        got = jpeg.encode(torch.from_numpy(img).cuda(), quality=q)
+        assert got == _pil_encode_bgr(img, q), (h, w, q)
+
+
+@pytest.mark.gpu
+def test_gpu_encode_strided_view_and_roundtrip(gpu):
+    """A crop view of a larger canvas (row pitch > 3 w) encodes like the contiguous crop, and
+    the GPU decoder reads the file back exactly as PIL does."""
+    import torch
+    from vfx_image_stitching_amd import jpeg
+    canvas = torch.from_numpy(_enc_image(300, 500, 9)).cuda()
+    view = canvas[13:13 + 211, 41:41 + 377]
+    got = jpeg.encode(view)
+    ref = _pil_encode_bgr(view.cpu().numpy(), 95)
+    assert got == ref
+    back = jpeg.decode_batch([got]).cpu().numpy()[0]
+    assert np.array_equal(back, _pil_bgr(got))

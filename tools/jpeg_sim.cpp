@@ -37,15 +37,17 @@ int main(int argc, char **argv) {
     if (rc == 0) rc = plan_frame(P, &F, &err);
     if (rc) { printf("{\"status\": %d, \"error\": \"%s\"}\n", rc, err.c_str()); return 1; }
 
-    // tables (std tables where the file has none, as libjpeg-turbo does)
-    Huff dcT[kMaxComp], acT[kMaxComp];
-    for (int c = 0; c < P.ncomp; ++c) {
-        uint8_t bits[17], vals[256];
-        const int d = P.comp_dc[c], q = P.comp_ac[c];
-        if (P.h_ok[0][d]) make_huff(P.hbits[0][d], P.hvals[0][d], &dcT[c]); else { std_huff(0, d, bits, vals); make_huff(bits, vals, &dcT[c]); }
-        if (P.h_ok[1][q]) make_huff(P.hbits[1][q], P.hvals[1][q], &acT[c]); else { std_huff(1, q, bits, vals); make_huff(bits, vals, &acT[c]); }
-    }
-    const Huff *dcp = dcT, *acp = acT;
+    // tables (std tables where the file has none, as libjpeg-turbo does): T[c] DC, T[3 + c] AC
+    Huff T[2 * kMaxComp];
+    for (int c = 0; c < P.ncomp; ++c)
+        for (int cls = 0; cls < 2; ++cls) {
+            uint8_t bits[17], vals[256];
+            const int id = cls ? P.comp_ac[c] : P.comp_dc[c];
+            if (P.h_ok[cls][id]) { memcpy(bits, P.hbits[cls][id], 17); memcpy(vals, P.hvals[cls][id], 256); }
+            else std_huff(cls, id, bits, vals);
+            const int hr = make_huff(bits, vals, &T[cls * 3 + c]);
+            if (hr) { printf("{\"status\": %d, \"error\": \"huffman table\"}\n", hr); return 1; }
+        }
 
     // unstuff (jpeg_unstuff_* kernels): drop the 0x00 after every 0xFF
     std::vector<uint8_t> st;
@@ -61,60 +63,77 @@ int main(int argc, char **argv) {
     const uint32_t nbits = (uint32_t)st.size() * 8;
     st.resize(st.size() + kStreamPad, 0);
     while (st.size() % 4) st.push_back(0);
-    const uint32_t *words = (const uint32_t *)st.data();
-    const uint32_t nw = (uint32_t)(st.size() / 4);
+    std::vector<uint32_t> wv(st.size() / 4);     // stream-order words, as the kernels stage them
+    for (size_t i = 0; i < wv.size(); ++i)
+        wv[i] = (uint32_t)st[4 * i] << 24 | (uint32_t)st[4 * i + 1] << 16 | (uint32_t)st[4 * i + 2] << 8 | st[4 * i + 3];
+    const uint32_t *words = wv.data();
+    const uint32_t nw = (uint32_t)wv.size();
     const uint32_t nsub = (nbits + L - 1) / L;
 
-    // pass A (jpeg_sync_warm): for every subsequence t and every MCU phase hypothesis j, a
-    // warm-up window of W bits before t is decoded from (t*L - W, block j, DC next) to find a
-    // candidate start c[t][j]; subsequences within W of the stream start decode from the exact
-    // start (bit 0).  Each candidate is then decoded over t with counting: exit x[t][j] and
-    // statistics.  A decode from a wrong bit position re-synchronises with the true decode
-    // only when it also lands in the right MCU phase; trying every phase makes one of them
-    // land in it early (the phase, not the bit alignment, dominates the sync distance).
+    // jpeg_sync_warm: for every subsequence t and MCU phase hypothesis j < bpm, a warm-up
+    // window of W bits before t is decoded from (t*L - W, block j, DC next) to a candidate start
+    // c[t][j] (subsequences within W of the stream start decode from the exact start, bit 0);
+    // each candidate is then decoded over t with counting: exit x[t][j] and statistics.  A
+    // decode from a wrong bit position re-synchronises with the true decode only when it also
+    // lands in the right block of the MCU; trying every phase makes one of them land early.
     const uint32_t W = getenv("JPEG_SIM_W") ? (uint32_t)atoi(getenv("JPEG_SIM_W")) : F.warm;
-    const int NP = F.bpm;
-    std::vector<uint64_t> cand((size_t)nsub * NP), ex((size_t)nsub * NP);
-    std::vector<SubStats> cstats((size_t)nsub * NP);
+    const int NP = F.bpm, NS = 2 * F.bpm;          // warm slots, + fix slots
+    const uint64_t kNoCand = ~0ull;
+    std::vector<uint64_t> cand((size_t)nsub * NS, kNoCand), ex((size_t)nsub * NS, kNoCand);
+    std::vector<SubStats> cstats((size_t)nsub * NS);
     auto end_of = [&](uint32_t t) { uint32_t e = (t + 1) * (uint32_t)L; return e < nbits ? e : nbits; };
     long decoded = 0;
     for (uint32_t t = 0; t < nsub; ++t)
         for (int j = 0; j < NP; ++j) {
             const uint32_t p0 = t * (uint32_t)L;
             SinkNone sn;
-            const size_t q = (size_t)t * NP + j;
-            cand[q] = p0 <= W ? walk(words, nw, pack_state(0, 0, 0), p0, dcp, acp, F.mcu_comp, F.bpm, sn)
-                              : walk(words, nw, pack_state(p0 - W, j, 0), p0, dcp, acp, F.mcu_comp, F.bpm, sn);
+            const size_t q = (size_t)t * NS + j;
+            cand[q] = p0 <= W ? walk(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, sn)
+                              : walk(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, sn);
             SinkCount sc;
-            ex[q] = walk(words, nw, cand[q], end_of(t), dcp, acp, F.mcu_comp, F.bpm, sc);
+            ex[q] = walk(words, 0, nw, cand[q], end_of(t), T, F.mcu_comp, F.bpm, sc);
             cstats[q] = sc.stats();
             ++decoded;
         }
-    // resolve (jpeg_sync_resolve): the chain J_t = index of the candidate of t equal to the
-    // true exit of t-1, starting from the exact t = 0; no match -> decode t from that exit.
+    // jpeg_sync_fix: where a warm exit of t-1 matches no warm candidate of t, decode t from that
+    // exit as an extra candidate (slot bpm + i)
+    int fix_slots = 0;
+    for (uint32_t t = 1; t < nsub; ++t)
+        for (int i = 0; i < NP; ++i) {
+            const uint64_t e = ex[(size_t)(t - 1) * NS + i];
+            bool hit = false;
+            for (int j = 0; j < NP; ++j) hit |= cand[(size_t)t * NS + j] == e;
+            if (hit) continue;
+            const size_t q = (size_t)t * NS + NP + i;
+            SinkCount sc;
+            cand[q] = e;
+            ex[q] = walk(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, sc);
+            cstats[q] = sc.stats();
+            ++fix_slots;
+        }
+    // jpeg_sync_resolve: J_t = the first candidate of t equal to the true exit of t-1 (t = 0
+    // exact); none -> decode t from that exit (serial fallback)
     std::vector<uint64_t> start(nsub);
     std::vector<SubStats> stats(nsub);
-    int fails = 0, rounds = 0, fixes = 0, serial_fixes = 0;
-    int J = 0;
+    int fails = 0;
     start[0] = cand[0]; stats[0] = cstats[0];
     uint64_t prev_exit = ex[0];
     for (uint32_t t = 1; t < nsub; ++t) {
         int jj = -1;
-        for (int j = 0; j < NP; ++j) if (cand[(size_t)t * NP + j] == prev_exit) { jj = j; break; }
+        for (int j = 0; j < NS; ++j) if (cand[(size_t)t * NS + j] == prev_exit) { jj = j; break; }
         if (jj < 0) {
             ++fails;
             SinkCount sc;
             start[t] = prev_exit;
-            prev_exit = walk(words, nw, start[t], end_of(t), dcp, acp, F.mcu_comp, F.bpm, sc);
+            prev_exit = walk(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, sc);
             stats[t] = sc.stats();
         } else {
-            start[t] = cand[(size_t)t * NP + jj];
-            stats[t] = cstats[(size_t)t * NP + jj];
-            prev_exit = ex[(size_t)t * NP + jj];
+            start[t] = cand[(size_t)t * NS + jj];
+            stats[t] = cstats[(size_t)t * NS + jj];
+            prev_exit = ex[(size_t)t * NS + jj];
         }
-        J = jj;
     }
-    (void)J; fixes = fails;
+    const int fixes = fails, serial_fixes = fails;
     // scan
     std::vector<SubStats> scan(nsub);
     SubStats acc = {0, {0, 0, 0}};
@@ -138,7 +157,7 @@ int main(int argc, char **argv) {
         w.p0 = scan[t].dc[0]; w.p1 = scan[t].dc[1]; w.p2 = scan[t].dc[2];
         w.live = k0 > 0 && w.blk >= 0 && w.blk < F.total_blocks;
         w.addr = w.live ? block_addr(F, w.blk) : 0;
-        walk(words, nw, start[t], end_of(t), dcp, acp, F.mcu_comp, F.bpm, w);
+        walk(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, w);
     }
     // IDCT
     std::vector<std::vector<uint8_t>> samp(F.ncomp);
@@ -170,9 +189,9 @@ int main(int argc, char **argv) {
     fwrite(out.data(), 1, out.size(), fo);
     fclose(fo);
     printf("{\"status\": 0, \"h\": %d, \"w\": %d, \"ncomp\": %d, \"upsample\": %d, \"nbits\": %u, \"nsub\": %u, "
-           "\"rounds\": %d, \"fixes\": %d, \"serial_fixes\": %d, \"walks\": %ld, \"blocks\": %d, \"total_blocks\": %d, "
+           "\"fix_slots\": %d, \"fixes\": %d, \"serial_fixes\": %d, \"walks\": %ld, \"blocks\": %d, \"total_blocks\": %d, "
            "\"markers\": %d}\n",
-           F.h, F.w, F.ncomp, F.upsample, nbits, nsub, rounds, fixes, serial_fixes, decoded,
+           F.h, F.w, F.ncomp, F.upsample, nbits, nsub, fix_slots, fixes, serial_fixes, decoded,
            acc.blocks, F.total_blocks, markers);
     return 0;
 }

@@ -2,7 +2,7 @@
 // cv2.imread of every frame (image_stitching_sift.py:282, image_stitching_harris.py:394),
 // bit-identical to libjpeg-turbo's default decode (what cv2.imread and PIL run).
 //
-// A batch of files is decoded by nine launches, all frames at once:
+// A batch of files is decoded by ten launches, all frames at once:
 //   jpeg_unstuff_count / jpeg_unstuff_write  remove the 0x00 stuffed after 0xFF bytes of the
 //        entropy-coded segments (a chunked stream compaction);
 //   jpeg_sync_warm   the Huffman stream has no restart markers, so it is cut into subsequences
@@ -11,6 +11,8 @@
 //        warm-up window before its subsequence from a guessed state, which converges on the
 //        true codeword boundaries; then it decodes its subsequence with counting (exit state,
 //        blocks started, DC difference sums);
+//   jpeg_sync_fix    where an exit of subsequence t-1 matches none of t's candidates, t is
+//        decoded from that exit as an extra candidate (all such (t, exit) pairs in parallel);
 //   jpeg_sync_resolve  one workgroup per frame chains the candidates: the true start of
 //        subsequence t is the exit of t-1's chosen candidate, found by a composition scan of
 //        the per-subsequence candidate maps; a subsequence whose candidates all missed is
@@ -20,7 +22,9 @@
 //        writes coefficients in natural order with the DC predicted;
 //   jpeg_idct        islow inverse DCT per 8x8 block into the component sample planes;
 //   jpeg_color       fancy chroma upsampling + YCbCr -> BGR, u8 [n][h][w][3].
-// The host parses headers only (jpeg_host.cpp) and uploads tables + entropy bytes once.
+// Every walk reads its bits from a window of the stream staged in LDS, and its Huffman tables
+// from LDS (two-level lookup, jpeg_core.h).  The host parses headers only (jpeg_host.cpp) and
+// uploads tables + entropy bytes once.
 #include <algorithm>
 #include <cstring>
 
@@ -44,18 +48,21 @@ struct Dev {
     uint32_t *nbits;
     int32_t *flags;
     int32_t *status;            // caller's, may be null
-    uint64_t *cand;             // [S][nps]
+    uint64_t *cand;             // [S][nps]: warm slots [0, np), fix slots [np, 2 np)
     uint64_t *cexit;            // [S][nps]
     SubStats *cstats;           // [S][nps]
     uint64_t *start;            // [S]
     SubStats *scan;             // [S] exclusive prefix
-    int n, nps;
+    int n, np, nps;             // candidate slots: np phases (max bpm), nps = 2 np
 };
+
+constexpr uint64_t kNoCand = ~0ull;
+constexpr int kMargin = 8;      // words staged past a window's last bit (Bits prefetch + one code)
 
 // ---------------------------------------------------------------------------------------- LDS
 // A frame's decode tables in LDS: DC / AC per component + the MCU layout.
 struct LdsTabs {
-    Huff dc[kMaxComp], ac[kMaxComp];
+    Huff T[2 * kMaxComp];       // DC tables of components 0..2, then their AC tables
     int8_t mcu_comp[kMaxBpm];
     uint8_t nat[80];
 };
@@ -66,7 +73,7 @@ __device__ __forceinline__ void stage_tabs(const Dev &D, const Frame &F, LdsTabs
     for (int c = 0; c < F.ncomp; ++c) {
         const uint32_t *sd = (const uint32_t *)&D.tabs[F.dc_tab[c]];
         const uint32_t *sa = (const uint32_t *)&D.tabs[F.ac_tab[c]];
-        uint32_t *dd = (uint32_t *)&L.dc[c], *da = (uint32_t *)&L.ac[c];
+        uint32_t *dd = (uint32_t *)&L.T[c], *da = (uint32_t *)&L.T[kMaxComp + c];
         for (int i = threadIdx.x; i < HW; i += nt) {
             dd[i] = sd[i];
             da[i] = sa[i];
@@ -83,6 +90,18 @@ __device__ __forceinline__ uint32_t frame_nsub(const Frame &F, uint32_t nb) {
 
 __device__ __forceinline__ uint32_t stream_words(const Frame &F, uint32_t nb) {
     return (nb / 8 + kStreamPad) / 4;
+}
+
+// Stage stream words [w0, w0 + n) of a frame into LDS in stream order (first byte in the top
+// bits); words past the frame's stream read as zero.
+__device__ __forceinline__ void stage_window(const Dev &D, const Frame &F, uint32_t nb, uint32_t w0, uint32_t n,
+                                             uint32_t *win) {
+    const uint32_t *src = (const uint32_t *)(D.stream + F.bits_off);
+    const uint32_t nw = stream_words(F, nb);
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t j = w0 + i;
+        win[i] = j < nw ? __builtin_bswap32(src[j]) : 0u;
+    }
 }
 
 // 256-thread block exclusive scan of a u32 (4 waves of 64).
@@ -174,71 +193,163 @@ __global__ void __launch_bounds__(256) jpeg_unstuff_write(Dev D) {
 }
 
 // ------------------------------------------------------------------------------------ sync
-__global__ void __launch_bounds__(128) jpeg_sync_warm(Dev D) {
+// Launch shapes: warm and fix run 256 threads = kSpb subsequences x np phase slots (the tail
+// threads idle); window = the bits those walks can reach.
+constexpr int kWarmMax = 16384;                     // cap of Frame::warm (bits)
+constexpr int kSyncThreads = 256;
+constexpr int kWinWords = (kWarmMax + kSyncThreads * kSubBits) / 32 + 2 * kMargin;
+
+__global__ void __launch_bounds__(kSyncThreads) jpeg_sync_warm(Dev D) {
     __shared__ LdsTabs L;
+    __shared__ uint32_t win[kWinWords];
     const int f = blockIdx.y;
     const Frame &F = D.frames[f];
-    stage_tabs(D, F, L);
-    __syncthreads();
     const uint32_t nb = D.nbits[f];
     const uint32_t nsub = frame_nsub(F, nb);
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t t = idx / (uint32_t)D.nps, j = idx % (uint32_t)D.nps;
-    if (t >= nsub || (int)j >= F.bpm) return;
-    const uint32_t *words = (const uint32_t *)(D.stream + F.bits_off);
-    const uint32_t nw = stream_words(F, nb);
-    const Huff *dcT = L.dc, *acT = L.ac;
-    const uint32_t p0 = t * kSubBits;
+    const int np = D.np, spb = kSyncThreads / np;
+    const uint32_t t0 = blockIdx.x * spb;
+    if (t0 >= nsub) return;                          // whole block past the frame's stream
     const uint32_t W = F.warm;
+    const uint32_t b0 = t0 * kSubBits > W ? t0 * kSubBits - W : 0;      // first bit any walk reads
+    const uint32_t w0 = b0 >> 5;
+    const uint32_t b1 = (t0 + spb) * kSubBits;
+    const uint32_t nwin = (b1 >> 5) - w0 + kMargin;
+    stage_tabs(D, F, L);
+    stage_window(D, F, nb, w0, nwin, win);
+    __syncthreads();
+    const uint32_t t = t0 + threadIdx.x / np, j = threadIdx.x % np;
+    if ((int)(threadIdx.x / np) >= spb || t >= nsub) return;
+    if ((int)j >= F.bpm) {                           // phase slot this frame's MCU lacks
+        D.cand[(size_t)(F.sub0 + t) * D.nps + j] = kNoCand;
+        return;
+    }
+    const uint32_t p0 = t * kSubBits;
     SinkNone sn;
-    const uint64_t s0 = p0 <= W ? walk(words, nw, pack_state(0, 0, 0), p0, dcT, acT, L.mcu_comp, F.bpm, sn)
-                                : walk(words, nw, pack_state(p0 - W, (int)j, 0), p0, dcT, acT, L.mcu_comp, F.bpm, sn);
+    const uint64_t s0 = p0 <= W ? walk(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, sn)
+                                : walk(win, w0, nwin, pack_state(p0 - W, (int)j, 0), p0, L.T, L.mcu_comp, F.bpm, sn);
     const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
     SinkCount sc;
-    const uint64_t x = walk(words, nw, s0, end, dcT, acT, L.mcu_comp, F.bpm, sc);
+    const uint64_t x = walk(win, w0, nwin, s0, end, L.T, L.mcu_comp, F.bpm, sc);
     const size_t q = (size_t)(F.sub0 + t) * D.nps + j;
     D.cand[q] = s0;
     D.cexit[q] = x;
     D.cstats[q] = sc.stats();
 }
 
-// Candidate map of subsequence t: for each candidate i of t-1, the first candidate of t whose
-// start equals i's exit (15 = none), 4 bits per entry.
+// Extra candidates: for subsequence t >= 1 and warm slot i of t-1 whose exit starts none of
+// t's warm candidates, t decoded from that exit (slot np + i); else the slot is empty.
+__global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix(Dev D) {
+    __shared__ LdsTabs L;
+    __shared__ uint32_t win[(kSyncThreads * kSubBits) / 32 + 2 * kMargin];
+    __shared__ int any;
+    const int f = blockIdx.y;
+    const Frame &F = D.frames[f];
+    const uint32_t nb = D.nbits[f];
+    const uint32_t nsub = frame_nsub(F, nb);
+    const int np = D.np, nps = D.nps, spb = kSyncThreads / np;
+    const uint32_t t0 = blockIdx.x * spb;
+    if (t0 >= nsub) return;
+    const uint32_t t = t0 + threadIdx.x / np, i = threadIdx.x % np;
+    bool need = false;
+    uint64_t e = kNoCand;
+    const bool slot = (int)(threadIdx.x / np) < spb && t < nsub;
+    const bool mine = slot && (int)i < F.bpm;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    if (mine && t >= 1) {
+        const size_t qp = (size_t)(F.sub0 + t - 1) * nps + i, qt = (size_t)(F.sub0 + t) * nps;
+        e = D.cexit[qp];
+        need = true;
+        for (int j = 0; j < F.bpm; ++j) need &= D.cand[qt + j] != e;
+        if (need) any = 1;
+    }
+    if (slot) D.cand[(size_t)(F.sub0 + t) * nps + np + i] = kNoCand;
+    __syncthreads();
+    if (!any) return;                                // uniform: no walk in this block
+    const uint32_t w0 = (t0 * kSubBits) >> 5;
+    const uint32_t nwin = (uint32_t)(spb * kSubBits) / 32 + kMargin;
+    stage_tabs(D, F, L);
+    stage_window(D, F, nb, w0, nwin, win);
+    __syncthreads();
+    if (!need) return;
+    const uint32_t p0 = t * kSubBits;
+    const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
+    SinkCount sc;
+    const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
+    const size_t q = (size_t)(F.sub0 + t) * nps + np + i;
+    D.cand[q] = e;
+    D.cexit[q] = x;
+    D.cstats[q] = sc.stats();
+}
+
+// Candidate map of subsequence t: for each slot i of t-1, the first slot of t whose start
+// equals i's exit (15 = none), 4 bits per entry (nps <= 12).
 constexpr uint64_t kNone = 15;
 __device__ __forceinline__ uint64_t map_get(uint64_t m, int i) { return (m >> (4 * i)) & 15; }
 // (second after first): entry i -> second[first[i]]
-__device__ __forceinline__ uint64_t map_then(uint64_t first, uint64_t second, int np) {
+__device__ __forceinline__ uint64_t map_then(uint64_t first, uint64_t second, int nps) {
     uint64_t r = 0;
-    for (int i = 0; i < np; ++i) {
+    for (int i = 0; i < nps; ++i) {
         const uint64_t a = map_get(first, i);
         r |= (a == kNone ? kNone : map_get(second, (int)a)) << (4 * i);
     }
     return r;
 }
-__device__ __forceinline__ uint64_t map_const(uint64_t v, int np) {
+__device__ __forceinline__ uint64_t map_const(uint64_t v, int nps) {
     uint64_t r = 0;
-    for (int i = 0; i < np; ++i) r |= v << (4 * i);
+    for (int i = 0; i < nps; ++i) r |= v << (4 * i);
     return r;
 }
+// first slot of t (candidates ct[0..nps)) starting at e
+__device__ __forceinline__ uint64_t find_slot(const uint64_t *ct, int nps, uint64_t e) {
+    uint64_t jj = kNone;
+    if (e == kNoCand) return jj;
+    for (int j = nps - 1; j >= 0; --j) if (ct[j] == e) jj = (uint64_t)j;
+    return jj;
+}
 
-__global__ void __launch_bounds__(256) jpeg_sync_resolve(Dev D) {
+constexpr int kResolveThreads = 512;
+
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    // kResolveThreads-thread exclusive scan (waves of 64)
+    constexpr int NW = kResolveThreads / 64;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int i = 0; i < NW; ++i) {
+        base += i < wv ? wsum[i] : 0;
+        tot += wsum[i];
+    }
+    *total = tot;
+    __syncthreads();
+    return base + x - v;
+}
+
+__global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
     __shared__ LdsTabs L;
-    __shared__ uint64_t maps[256];
-    __shared__ uint32_t wsum[4];
+    __shared__ uint64_t maps[kResolveThreads];
+    __shared__ uint32_t wsum[kResolveThreads / 64];
+    __shared__ uint32_t win[kSubBits / 32 + 2 * kMargin];
     __shared__ int s_fail;
     __shared__ uint64_t s_exit;
     __shared__ SubStats s_acc;
+    constexpr int NT = kResolveThreads;
     const int f = blockIdx.x;
     const Frame &F = D.frames[f];
     stage_tabs(D, F, L);
     const uint32_t nb = D.nbits[f];
     const uint32_t nsub = frame_nsub(F, nb);
-    const int np = F.bpm, nps = D.nps;
+    const int nps = D.nps;
     const size_t S0 = F.sub0;
-    const uint32_t *words = (const uint32_t *)(D.stream + F.bits_off);
-    const uint32_t nw = stream_words(F, nb);
-    if (threadIdx.x == 0) {
-        // subsequence 0 decodes from the exact start: every candidate is the same
+    if (threadIdx.x == 0 && nsub > 0) {
+        // subsequence 0 decodes from the exact start: every warm candidate is the same
         D.start[S0] = D.cand[S0 * nps];
         SubStats z = {0, {0, 0, 0}};
         D.scan[S0] = z;
@@ -246,55 +357,48 @@ __global__ void __launch_bounds__(256) jpeg_sync_resolve(Dev D) {
         s_exit = D.cexit[S0 * nps];
     }
     __syncthreads();
-    const Huff *dcT = L.dc, *acT = L.ac;
     uint32_t base = 1;
     uint32_t guard = nsub + 8;
     while (base < nsub && guard--) {
         const uint32_t t = base + threadIdx.x;
         const bool in = t < nsub;
-        // map of t: from the known exit (t == base) or from t-1's candidates
-        uint64_t m = map_const(kNone, np);
+        // map of t: from the known exit (t == base) or from t-1's slots
+        uint64_t m = map_const(kNone, nps);
         if (in) {
             const uint64_t *ct = D.cand + (S0 + t) * nps;
             if (threadIdx.x == 0) {
-                const uint64_t e = s_exit;
-                uint64_t jj = kNone;
-                for (int j = np - 1; j >= 0; --j) if (ct[j] == e) jj = (uint64_t)j;
-                m = map_const(jj, np);
+                m = map_const(find_slot(ct, nps, s_exit), nps);
             } else {
                 const uint64_t *xp = D.cexit + (S0 + t - 1) * nps;
+                const uint64_t *cp = D.cand + (S0 + t - 1) * nps;
                 m = 0;
-                for (int i = 0; i < np; ++i) {
-                    const uint64_t e = xp[i];
-                    uint64_t jj = kNone;
-                    for (int j = np - 1; j >= 0; --j) if (ct[j] == e) jj = (uint64_t)j;
-                    m |= jj << (4 * i);
-                }
+                for (int i = 0; i < nps; ++i)
+                    m |= (cp[i] == kNoCand ? kNone : find_slot(ct, nps, xp[i])) << (4 * i);
             }
         }
         maps[threadIdx.x] = m;
-        if (threadIdx.x == 0) s_fail = 256;
+        if (threadIdx.x == 0) s_fail = NT;
         __syncthreads();
         // inclusive scan by composition: maps[t] = M_t after ... after M_base
-        for (int o = 1; o < 256; o <<= 1) {
+        for (int o = 1; o < NT; o <<= 1) {
             uint64_t prev = 0;
             if ((int)threadIdx.x >= o) prev = maps[threadIdx.x - o];
             __syncthreads();
-            if ((int)threadIdx.x >= o) maps[threadIdx.x] = map_then(prev, maps[threadIdx.x], np);
+            if ((int)threadIdx.x >= o) maps[threadIdx.x] = map_then(prev, maps[threadIdx.x], nps);
             __syncthreads();
         }
-        // chosen candidate of t (the composed map is constant: its first map is)
+        // chosen slot of t (the composed map is constant: its first map is)
         const uint32_t J = (uint32_t)map_get(maps[threadIdx.x], 0);
         if (in && J == kNone) atomicMin(&s_fail, (int)threadIdx.x);
         __syncthreads();
-        const int nres = min(s_fail, (int)min(256u, nsub - base));   // resolved in this chunk
+        const int nres = min(s_fail, (int)min((uint32_t)NT, nsub - base));   // resolved in this chunk
         SubStats st = {0, {0, 0, 0}};
         if ((int)threadIdx.x < nres) st = D.cstats[(S0 + t) * nps + J];
         // exclusive prefix of the statistics over the resolved run
         uint32_t tb;
-        const uint32_t pb = block_exscan256((uint32_t)st.blocks, wsum, &tb);
+        const uint32_t pb = block_exscan((uint32_t)st.blocks, wsum, &tb);
         uint32_t pd[kMaxComp], td[kMaxComp];
-        for (int c = 0; c < kMaxComp; ++c) pd[c] = block_exscan256((uint32_t)st.dc[c], wsum, &td[c]);
+        for (int c = 0; c < kMaxComp; ++c) pd[c] = block_exscan((uint32_t)st.dc[c], wsum, &td[c]);
         if ((int)threadIdx.x < nres) {
             D.start[S0 + t] = D.cand[(S0 + t) * nps + J];
             SubStats sc;
@@ -310,13 +414,16 @@ __global__ void __launch_bounds__(256) jpeg_sync_resolve(Dev D) {
         }
         base += nres;
         __syncthreads();
-        if (nres < 256 && base < nsub) {
+        if (nres < NT && base < nsub) {
             // every candidate of `base` missed: decode it from the true start (one thread)
+            const uint32_t w0 = (base * kSubBits) >> 5, nwin = kSubBits / 32 + kMargin;
+            stage_window(D, F, nb, w0, nwin, win);
+            __syncthreads();
             if (threadIdx.x == 0) {
                 const uint64_t e = s_exit;
                 const uint32_t end = (base + 1) * kSubBits < nb ? (base + 1) * kSubBits : nb;
                 SinkCount sc;
-                const uint64_t x = walk(words, nw, e, end, dcT, acT, L.mcu_comp, F.bpm, sc);
+                const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
                 D.start[S0 + base] = e;
                 D.scan[S0 + base] = s_acc;
                 s_acc.blocks += sc.blocks;
@@ -339,34 +446,41 @@ __global__ void __launch_bounds__(256) jpeg_sync_resolve(Dev D) {
 }
 
 // ----------------------------------------------------------------------------------- write
-__global__ void __launch_bounds__(128) jpeg_write(Dev D) {
+constexpr int kWriteThreads = 128;
+__global__ void __launch_bounds__(kWriteThreads) jpeg_write(Dev D) {
     __shared__ LdsTabs L;
+    __shared__ Frame Fs;
+    __shared__ uint32_t win[(kWriteThreads * kSubBits) / 32 + 2 * kMargin];
     const int f = blockIdx.y;
     const Frame &F = D.frames[f];
-    stage_tabs(D, F, L);
-    __syncthreads();
     const uint32_t nb = D.nbits[f];
     const uint32_t nsub = frame_nsub(F, nb);
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nsub || D.flags[f] != PANO_OK) return;
-    const uint32_t *words = (const uint32_t *)(D.stream + F.bits_off);
-    const uint32_t nw = stream_words(F, nb);
-    const Huff *dcT = L.dc, *acT = L.ac;
+    const uint32_t t0 = blockIdx.x * kWriteThreads;
+    if (t0 >= nsub || D.flags[f] != PANO_OK) return;
+    const uint32_t w0 = (t0 * kSubBits) >> 5;
+    const uint32_t nwin = (uint32_t)(kWriteThreads * kSubBits) / 32 + kMargin;
+    stage_tabs(D, F, L);
+    stage_window(D, F, nb, w0, nwin, win);
+    for (int i = threadIdx.x; i < (int)(sizeof(Frame) / 4); i += kWriteThreads)
+        ((uint32_t *)&Fs)[i] = ((const uint32_t *)&F)[i];
+    __syncthreads();
+    const uint32_t t = t0 + threadIdx.x;
+    if (t >= nsub) return;
     const uint64_t s0 = D.start[F.sub0 + t];
     const SubStats sc = D.scan[F.sub0 + t];
     SinkWrite w;
     w.coef = D.coef;
-    w.F = &F;
+    w.F = &Fs;
     w.nat = L.nat;
     const int k0 = state_k(s0);
     w.blk = sc.blocks - (k0 > 0 ? 1 : 0);
     w.p0 = sc.dc[0];
     w.p1 = sc.dc[1];
     w.p2 = sc.dc[2];
-    w.live = k0 > 0 && w.blk >= 0 && w.blk < F.total_blocks;
-    w.addr = w.live ? block_addr(F, w.blk) : 0;
+    w.live = k0 > 0 && w.blk >= 0 && w.blk < Fs.total_blocks;
+    w.addr = w.live ? block_addr(Fs, w.blk) : 0;
     const uint32_t end = (t + 1) * kSubBits < nb ? (t + 1) * kSubBits : nb;
-    walk(words, nw, s0, end, dcT, acT, L.mcu_comp, F.bpm, w);
+    walk(win, w0, nwin, s0, end, L.T, L.mcu_comp, Fs.bpm, w);
 }
 
 // ------------------------------------------------------------------------------------ IDCT
@@ -466,7 +580,8 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
                     if (tab_keys[k] == key) { ti = (int)k; break; }
                 if (ti < 0) {
                     Huff T;
-                    if (!make_huff(bits, vals, &T)) return pano_fail(ctx, PANO_E_ARG, "bad Huffman table");
+                    const int hr = make_huff(bits, vals, &T);
+                    if (hr) return pano_fail(ctx, hr, "frame " + std::to_string(f) + ": unsupported Huffman table");
                     ti = (int)tabs.size();
                     tabs.push_back(T);
                     tab_keys.push_back(key);
@@ -481,7 +596,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     // ---- layout: upload (frames, tables, quant, chunk map, entropy bytes) and device arenas
     size_t src_total = 0, stream_total = 0, coef_total = 0, samp_total = 0;
     uint32_t chunks = 0, subs = 0, nsub_max = 0, max_blocks = 0;
-    int nps = 1;
+    int np = 1;
     for (int f = 0; f < n; ++f) {
         Frame &F = fr[f];
         F.src_off = src_total;
@@ -497,7 +612,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
         F.nsub = (uint32_t)(((uint64_t)F.src_len * 8 + kSubBits - 1) / kSubBits);
         subs += F.nsub;
         nsub_max = std::max(nsub_max, F.nsub);
-        nps = std::max(nps, F.bpm);
+        np = std::max(np, F.bpm);
         for (int c = 0; c < F.ncomp; ++c) {
             const size_t nbk = (size_t)F.comp_bw[c] * F.comp_bh[c];
             F.coef_off[c] = coef_total;
@@ -514,6 +629,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     const size_t o_chunks = up;  up = align_up(up + 4 * chunk_frame.size(), 256);
     const size_t o_src = up;     up = align_up(up + src_total, 256);
     const size_t up_bytes = up;
+    const int nps = 2 * np;
     size_t dv = align_up(up_bytes, 256);
     const size_t o_stream = dv;  dv = align_up(dv + stream_total, 256);
     const size_t o_coef = dv;    dv = align_up(dv + 2 * coef_total, 256);
@@ -530,20 +646,21 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
 
     int rc = pano_grow(ctx, &ctx->jscratch, &ctx->jscratch_bytes, dev_bytes);
     if (rc) return rc;
-    // pinned staging: wait until the previous upload out of it has completed
-    if (!ctx->jev) PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->jev, hipEventDisableTiming));
-    if (ctx->jpin_bytes < up_bytes) {
-        PANO_HIP(ctx, hipEventSynchronize(ctx->jev));
-        if (ctx->jpin) (void)hipHostFree(ctx->jpin);
-        ctx->jpin = nullptr;
-        ctx->jpin_bytes = 0;
+    // pinned staging, two buffers in turn: wait until the upload out of this one (two calls
+    // ago) has completed, fill it, upload
+    const int slot = ctx->jslot;
+    ctx->jslot ^= 1;
+    if (!ctx->jev[slot]) PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->jev[slot], hipEventDisableTiming));
+    else PANO_HIP(ctx, hipEventSynchronize(ctx->jev[slot]));
+    if (ctx->jpin_bytes[slot] < up_bytes) {
+        if (ctx->jpin[slot]) (void)hipHostFree(ctx->jpin[slot]);
+        ctx->jpin[slot] = nullptr;
+        ctx->jpin_bytes[slot] = 0;
         const size_t sz = up_bytes + up_bytes / 4 + 65536;
-        PANO_HIP(ctx, hipHostMalloc(&ctx->jpin, sz, hipHostMallocDefault));
-        ctx->jpin_bytes = sz;
-    } else {
-        PANO_HIP(ctx, hipEventSynchronize(ctx->jev));
+        PANO_HIP(ctx, hipHostMalloc(&ctx->jpin[slot], sz, hipHostMallocDefault));
+        ctx->jpin_bytes[slot] = sz;
     }
-    uint8_t *pin = (uint8_t *)ctx->jpin;
+    uint8_t *pin = (uint8_t *)ctx->jpin[slot];
     memcpy(pin + o_frames, fr.data(), sizeof(Frame) * n);
     if (!tabs.empty()) memcpy(pin + o_tabs, tabs.data(), sizeof(Huff) * tabs.size());
     memcpy(pin + o_quant, quant.data(), 2 * quant.size());
@@ -554,7 +671,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     }
     uint8_t *dev = (uint8_t *)ctx->jscratch;
     PANO_HIP(ctx, hipMemcpyAsync(dev, pin, up_bytes, hipMemcpyHostToDevice, ctx->stream));
-    PANO_HIP(ctx, hipEventRecord(ctx->jev, ctx->stream));
+    PANO_HIP(ctx, hipEventRecord(ctx->jev[slot], ctx->stream));
 
     Dev D;
     D.frames = (const Frame *)(dev + o_frames);
@@ -575,6 +692,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     D.start = (uint64_t *)(dev + o_start);
     D.scan = (SubStats *)(dev + o_scan);
     D.n = n;
+    D.np = np;
     D.nps = nps;
 
     PanoProf prof_(ctx, PK_JPEG);
@@ -584,11 +702,13 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     jpeg_unstuff_count<<<chunks, 256, 0, ctx->stream>>>(D);
     jpeg_unstuff_write<<<chunks, 256, 0, ctx->stream>>>(D);
     {
-        const unsigned gx = (unsigned)((nsub_max * (uint32_t)nps + 127) / 128);
-        jpeg_sync_warm<<<dim3(gx, n), 128, 0, ctx->stream>>>(D);
+        const uint32_t spb = kSyncThreads / np;
+        const unsigned gx = (unsigned)((nsub_max + spb - 1) / spb);
+        jpeg_sync_warm<<<dim3(gx, n), kSyncThreads, 0, ctx->stream>>>(D);
+        jpeg_sync_fix<<<dim3(gx, n), kSyncThreads, 0, ctx->stream>>>(D);
     }
-    jpeg_sync_resolve<<<n, 256, 0, ctx->stream>>>(D);
-    jpeg_write<<<dim3((nsub_max + 127) / 128, n), 128, 0, ctx->stream>>>(D);
+    jpeg_sync_resolve<<<n, kResolveThreads, 0, ctx->stream>>>(D);
+    jpeg_write<<<dim3((nsub_max + kWriteThreads - 1) / kWriteThreads, n), kWriteThreads, 0, ctx->stream>>>(D);
     jpeg_idct<<<dim3((max_blocks + 31) / 32, n * kMaxComp), 256, 0, ctx->stream>>>(D);
     jpeg_color<<<dim3((unsigned)(((size_t)h * w + 255) / 256), n), 256, 0, ctx->stream>>>(D, bgr, h, w);
     PANO_LAUNCH_CHECK(ctx, "jpeg decode");

@@ -27,16 +27,19 @@ namespace pj {
 
 constexpr int kMaxComp = 3;     // gray or YCbCr
 constexpr int kMaxBpm = 10;     // blocks per MCU (JPEG limit)
-constexpr int kSubBits = 1024;  // bits per subsequence of the self-synchronising decode
+constexpr int kSubBits = 512;   // bits per subsequence of the self-synchronising decode
 constexpr int kChunk = 4096;    // stuffed bytes per unstuff chunk
 constexpr int kStreamPad = 64;  // zero bytes after each unstuffed stream
+constexpr int kHuffSub = 16;    // second-level lookup tables per Huffman table
 
-// One Huffman table in decode form (jdhuff.c jpeg_make_d_derived_tbl restated).
+// One Huffman table in decode form (jdhuff.c jpeg_make_d_derived_tbl restated as a two-level
+// lookup): the first 9 bits of the stream index lut; codes of up to 9 bits resolve there,
+// longer ones through a 128-entry second-level table indexed by the next 7 bits.  Entries:
+// (code length << 8) | symbol; lut entries with bit 15 set hold a second-level offset; 0 = no
+// such code (only reached off-sync).  One or two LDS reads per symbol, no search loop.
 struct Huff {
-    uint16_t lut[512];    // 9-bit peek -> (code length << 8) | symbol; 0 = code longer than 9
-    int32_t maxcode[18];  // per length 1..16: largest code of that length, -1 none
-    int32_t valoff[18];   // symbol index = valoff[l] + code
-    uint8_t vals[256];
+    uint16_t lut[512];
+    uint16_t sub[kHuffSub * 128];
 };
 
 // Everything a kernel needs about one frame (built on the host by jpeg_plan).
@@ -62,24 +65,28 @@ struct Frame {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Bit reader over an unstuffed stream (big-endian bytes read as 32-bit words).
+// Bit reader over a window of the unstuffed stream held as 32-bit words in stream order
+// (word i = bytes 4i..4i+3, first byte in the top bits): w[j] is stream word woff + j.  Words
+// outside [woff, woff + nw) read as zeros (libjpeg pads with zeros after the last marker,
+// jdhuff.c jpeg_fill_bit_buffer; the kernels stage every window a walk can reach).
 struct Bits {
     const uint32_t *w;
-    uint32_t nw;       // words readable; beyond them the stream reads as zeros (libjpeg pads
-                       // with zeros after the last marker, jdhuff.c jpeg_fill_bit_buffer)
-    uint32_t wi;       // next word to load
+    uint32_t woff, nw;
+    uint32_t wi;       // next word to load (stream index)
     int cnt;           // valid bits in buf
     uint64_t buf;      // left-aligned: the next bit is bit 63
 
     __host__ __device__ __forceinline__ uint32_t load(uint32_t i) const {
-        return i < nw ? __builtin_bswap32(w[i]) : 0u;
+        const uint32_t j = i - woff;
+        return j < nw ? w[j] : 0u;
     }
     __host__ __device__ __forceinline__ void fill() {   // requires cnt <= 32
         buf |= (uint64_t)load(wi++) << (32 - cnt);
         cnt += 32;
     }
-    __host__ __device__ __forceinline__ void init(const uint32_t *words, uint32_t nwords, uint32_t pos) {
-        w = words; nw = nwords; wi = pos >> 5; buf = 0; cnt = 0;
+    __host__ __device__ __forceinline__ void init(const uint32_t *words, uint32_t word_off, uint32_t nwords,
+                                                  uint32_t pos) {
+        w = words; woff = word_off; nw = nwords; wi = pos >> 5; buf = 0; cnt = 0;
         fill(); fill();
         const int s = (int)(pos & 31);
         buf <<= s; cnt -= s;
@@ -94,24 +101,15 @@ struct Bits {
     }
 };
 
-// Decode one Huffman symbol (jdhuff.c jpeg_huff_decode).  An invalid code consumes 16 bits
-// and returns -1 (libjpeg warns and yields symbol 0); that only happens off-sync.
+// Decode one Huffman symbol (jdhuff.c jpeg_huff_decode).  A code the table lacks (only off
+// sync) consumes 16 bits and yields symbol 0.
 __host__ __device__ __forceinline__ int huff_decode(const Huff *T, Bits &br) {
     const uint32_t p = (uint32_t)(br.buf >> 48);
-    const uint32_t e = T->lut[p >> 7];
-    if (e) {
-        br.skip((int)(e >> 8));
-        return (int)(e & 0xFF);
-    }
-    for (int l = 10; l <= 16; ++l) {
-        const int32_t code = (int32_t)(p >> (16 - l));
-        if (code <= T->maxcode[l]) {
-            br.skip(l);
-            return T->vals[(T->valoff[l] + code) & 0xFF];
-        }
-    }
-    br.skip(16);
-    return -1;
+    uint32_t e = T->lut[p >> 7];
+    if (e & 0x8000) e = T->sub[(e & 0x7FFF) + (p & 127)];
+    const int len = (int)(e >> 8);
+    br.skip(len ? len : 16);
+    return (int)(e & 0xFF);
 }
 
 // HUFF_EXTEND (jdhuff.h)
@@ -185,45 +183,38 @@ __host__ __device__ __forceinline__ int natural_order(int k) {
 
 // Walk the codewords that start in [start, end): from state `start` decode until the bit
 // position reaches `end`; returns the state at the first boundary >= end.  The sink sees
-// every DC difference (dc returns false to stop early) and AC coefficient.  dcT / acT: the
-// DC / AC tables of components 0..2.
+// every DC difference (dc returns false to stop early) and AC coefficient.  T: the DC tables
+// of components 0..2 followed by their AC tables (T[c], T[3 + c]).
 template <class Sink>
-__host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_t nwords, uint64_t start,
-                                                  uint32_t end, const Huff *dcT, const Huff *acT,
+__host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_t woff, uint32_t nwords,
+                                                  uint64_t start, uint32_t end, const Huff *T,
                                                   const int8_t *mcu_comp, int bpm, Sink &sink) {
     Bits br;
-    br.init(words, nwords, state_pos(start));
+    br.init(words, woff, nwords, state_pos(start));
     int b = state_b(start), k = state_k(start);
+    int c = mcu_comp[b];
     uint32_t guard = end - state_pos(start) + 64;   // every codeword consumes >= 1 bit
     while (br.pos() < end && guard--) {
         br.ensure32();
-        const int c = mcu_comp[b];
+        const int sym = huff_decode(T + (k == 0 ? c : 3 + c), br);
+        // DC: the symbol is the difference's bit count; AC: run << 4 | bit count
+        const int r = k == 0 ? 0 : sym >> 4;
+        const int s = k == 0 ? (sym > 16 ? 16 : sym) : (sym & 15);
+        const int v = s ? huff_extend(br.get(s), s) : 0;
         if (k == 0) {
-            int s = huff_decode(dcT + c, br);
-            int diff = 0;
-            if (s > 0) {
-                if (s > 16) s = 16;
-                diff = huff_extend(br.get(s), s);
-            }
-            if (!sink.dc(c, diff)) break;
+            if (!sink.dc(c, v)) break;
             k = 1;
+        } else if (s) {
+            k += r;
+            sink.ac(k, v);
+            ++k;
         } else {
-            int rs = huff_decode(acT + c, br);
-            if (rs < 0) rs = 0;
-            const int r = rs >> 4, s = rs & 15;
-            if (s) {
-                k += r;
-                sink.ac(k, huff_extend(br.get(s), s));
-                ++k;
-            } else if (r == 15) {
-                k += 16;
-            } else {
-                k = 64;
-            }
+            k = r == 15 ? k + 16 : 64;     // ZRL or EOB
         }
         if (k >= 64) {
             k = 0;
-            if (++b == bpm) b = 0;
+            b = b + 1 == bpm ? 0 : b + 1;
+            c = mcu_comp[b];
             sink.end_block();
         }
     }
@@ -374,6 +365,208 @@ __host__ __device__ __forceinline__ void ycc_to_bgr(int y, int cb, int cr, uint8
 }
 
 // ---------------------------------------------------------------------------------------------
+// Encoder (cv2.imwrite / PIL save, quality 95: libjpeg-turbo's defaults).
+// RGB -> YCbCr, jccolor.c rgb_ycc_convert (SCALEBITS 16, FIX(x) = (int)(x * 65536 + 0.5)).
+__host__ __device__ __forceinline__ void rgb_to_ycc(int r, int g, int b, int &y, int &cb, int &cr) {
+    const int F0299 = 19595, F0587 = 38470, F0114 = 7471, F016874 = 11059, F033126 = 21709,
+              F05 = 32768, F041869 = 27439, F008131 = 5329;
+    const int half = 1 << 15, off = 128 << 16;
+    y = (F0299 * r + F0587 * g + F0114 * b + half) >> 16;
+    cb = (-F016874 * r - F033126 * g + F05 * b + off + half - 1) >> 16;
+    cr = (F05 * r - F041869 * g - F008131 * b + off + half - 1) >> 16;
+}
+
+// jfdctint.c jpeg_fdct_islow on one 8-point line (pass 1 when pass == 1: rows, descale
+// CONST_BITS - PASS1_BITS; pass 2: columns, descale by PASS1_BITS / CONST_BITS + PASS1_BITS).
+// d: 8 inputs (stride 1), written back in place; values are 16-bit DCTELEMs.
+__host__ __device__ __forceinline__ void fdct8(int32_t *d, int pass) {
+    const int64_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373,
+                  F1175 = 9633, F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819,
+                  F2562 = 20995, F3072 = 25172;
+    const int64_t tmp0 = d[0] + d[7], tmp7 = d[0] - d[7], tmp1 = d[1] + d[6], tmp6 = d[1] - d[6];
+    const int64_t tmp2 = d[2] + d[5], tmp5 = d[2] - d[5], tmp3 = d[3] + d[4], tmp4 = d[3] - d[4];
+    const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    const int sh = pass == 1 ? 11 : 15;           // CONST_BITS -/+ PASS1_BITS
+    if (pass == 1) {
+        d[0] = (int16_t)((tmp10 + tmp11) * 4);
+        d[4] = (int16_t)((tmp10 - tmp11) * 4);
+    } else {
+        d[0] = (int16_t)descale(tmp10 + tmp11, 2);
+        d[4] = (int16_t)descale(tmp10 - tmp11, 2);
+    }
+    int64_t z1 = (tmp12 + tmp13) * F0541;
+    d[2] = (int16_t)descale(z1 + tmp13 * F0765, sh);
+    d[6] = (int16_t)descale(z1 + tmp12 * (-F1847), sh);
+    z1 = tmp4 + tmp7;
+    int64_t z2 = tmp5 + tmp6, z3 = tmp4 + tmp6, z4 = tmp5 + tmp7;
+    const int64_t z5 = (z3 + z4) * F1175;
+    const int64_t t4 = tmp4 * F0298, t5 = tmp5 * F2053, t6 = tmp6 * F3072, t7 = tmp7 * F1501;
+    z1 *= -F0899; z2 *= -F2562; z3 *= -F1961; z4 *= -F0390;
+    z3 += z5; z4 += z5;
+    d[7] = (int16_t)descale(t4 + z1 + z3, sh);
+    d[5] = (int16_t)descale(t5 + z2 + z4, sh);
+    d[3] = (int16_t)descale(t6 + z2 + z3, sh);
+    d[1] = (int16_t)descale(t7 + z1 + z4, sh);
+}
+
+// jcdctmgr.c: quantisation by reciprocal multiplication (compute_reciprocal + quantize, 16-bit
+// DCTELEM), identical to libjpeg-turbo's C and SIMD paths.  q8 = quantval << 3.
+struct QRecip {
+    uint16_t recip, corr;
+    int16_t shift;           // total right shift of the product
+};
+__host__ __device__ __forceinline__ QRecip q_recip(uint32_t q8) {
+    QRecip r;
+    if (q8 == 1) { r.recip = 1; r.corr = 0; r.shift = 0; return r; }
+    int b = 0;
+    while ((1u << (b + 1)) <= q8) ++b;             // floor(log2(q8))
+    int rr = 16 + b;
+    uint32_t fq = (uint32_t)((1ull << rr) / q8), fr = (uint32_t)((1ull << rr) % q8);
+    uint32_t c = q8 / 2;
+    if (fr == 0) { fq >>= 1; --rr; }
+    else if (fr <= q8 / 2u) ++c;
+    else ++fq;
+    r.recip = (uint16_t)fq;
+    r.corr = (uint16_t)c;
+    r.shift = (int16_t)rr;
+    return r;
+}
+__host__ __device__ __forceinline__ int quantize(int v, QRecip q) {
+    const uint32_t a = (uint32_t)(v < 0 ? -v : v);
+    const uint32_t p = ((a + q.corr) & 0xFFFF) * (uint32_t)q.recip;   // UDCTELEM2 product
+    const int r = (int)(p >> q.shift);
+    return v < 0 ? -r : r;
+}
+
+__host__ __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+
+// Encoder geometry: 3 components, 4:2:0 (libjpeg's default for YCbCr), MCU = Y0 Y1 Y2 Y3 Cb Cr.
+struct EncGeom {
+    int32_t h, w, mcus_x, mcus_y;
+    int32_t ybw, ybh;            // luma blocks holding image data: ceil(w / 8), ceil(h / 8)
+    int64_t pitch;               // image row pitch in bytes (BGR rows)
+};
+__host__ __device__ __forceinline__ EncGeom enc_geom(int h, int w, int64_t pitch) {
+    EncGeom G;
+    G.h = h; G.w = w; G.pitch = pitch;
+    G.mcus_x = (w + 15) / 16; G.mcus_y = (h + 15) / 16;
+    G.ybw = (w + 7) / 8; G.ybh = (h + 7) / 8;
+    return G;
+}
+
+// Level-shifted samples of one block (MCU order index blk) in natural order: the
+// pre-processing chain of jcprepct.c / jcsample.c -- colour conversion, right-edge and
+// bottom-edge replication, h2v2 downsampling with the 1,2,1,2 bias -- for a real block.
+__host__ __device__ __forceinline__ void enc_samples(const uint8_t *img, const EncGeom &G, int blk, int32_t *s) {
+    const int m = blk / 6, b = blk - 6 * (blk / 6);
+    const int mx = m % G.mcus_x, my = m / G.mcus_x;
+    if (b < 4) {
+        const int bx = 2 * mx + (b & 1), by = 2 * my + (b >> 1);
+        for (int r = 0; r < 8; ++r) {
+            const int y = imin(by * 8 + r, G.h - 1);
+            const uint8_t *row = img + (int64_t)y * G.pitch;
+            for (int c = 0; c < 8; ++c) {
+                const uint8_t *p = row + 3 * imin(bx * 8 + c, G.w - 1);
+                int Y, cb, cr;
+                rgb_to_ycc(p[2], p[1], p[0], Y, cb, cr);
+                s[r * 8 + c] = Y - 128;
+            }
+        }
+        return;
+    }
+    const int hc = (G.h + 1) / 2;          // chroma rows holding data
+    for (int r = 0; r < 8; ++r) {
+        const int cy = imin(my * 8 + r, hc - 1);
+        const uint8_t *r0 = img + (int64_t)(2 * cy) * G.pitch;
+        const uint8_t *r1 = img + (int64_t)imin(2 * cy + 1, G.h - 1) * G.pitch;
+        for (int c = 0; c < 8; ++c) {
+            const int cx = mx * 8 + c;
+            const int x0 = 3 * imin(2 * cx, G.w - 1), x1 = 3 * imin(2 * cx + 1, G.w - 1);
+            int Y, cb[4], cr[4];
+            rgb_to_ycc(r0[x0 + 2], r0[x0 + 1], r0[x0], Y, cb[0], cr[0]);
+            rgb_to_ycc(r0[x1 + 2], r0[x1 + 1], r0[x1], Y, cb[1], cr[1]);
+            rgb_to_ycc(r1[x0 + 2], r1[x0 + 1], r1[x0], Y, cb[2], cr[2]);
+            rgb_to_ycc(r1[x1 + 2], r1[x1 + 1], r1[x1], Y, cb[3], cr[3]);
+            const int bias = (cx & 1) ? 2 : 1;
+            const int v = b == 4 ? (cb[0] + cb[1] + cb[2] + cb[3] + bias) >> 2 : (cr[0] + cr[1] + cr[2] + cr[3] + bias) >> 2;
+            s[r * 8 + c] = v - 128;
+        }
+    }
+}
+
+// Forward DCT (rows, then columns) and quantisation of 64 level-shifted samples -> coef
+// (natural order).  q: reciprocals of the component's table.
+__host__ __device__ __forceinline__ void enc_transform(int32_t *s, const QRecip *q, int16_t *coef) {
+    for (int r = 0; r < 8; ++r) fdct8(s + r * 8, 1);
+    for (int c = 0; c < 8; ++c) {
+        int32_t col[8];
+        for (int r = 0; r < 8; ++r) col[r] = s[r * 8 + c];
+        fdct8(col, 2);
+        for (int r = 0; r < 8; ++r) s[r * 8 + c] = col[r];
+    }
+    for (int i = 0; i < 64; ++i) coef[i] = (int16_t)quantize(s[i], q[i]);
+}
+
+// jccoefct.c compress_data dummy blocks: a luma block outside the image's block grid has
+// zero AC and the DC of the block it copies -- the left neighbour (right edge) or the MCU's
+// block 1 (bottom edge, which may itself copy block 0).  Returns the MCU-order index of the
+// real block whose DC it takes, or -1 for a real block.
+__host__ __device__ __forceinline__ int enc_dummy_source(const EncGeom &G, int blk) {
+    const int m = blk / 6, b = blk - 6 * (blk / 6);
+    if (b >= 4) return -1;
+    const int mx = m % G.mcus_x, my = m / G.mcus_x;
+    const int bx = 2 * mx + (b & 1), by = 2 * my + (b >> 1);
+    if (bx < G.ybw && by < G.ybh) return -1;
+    if (by >= G.ybh) return 6 * m + ((2 * mx + 1) < G.ybw ? 1 : 0);
+    return blk - 1;
+}
+
+// MCU-order index of the previous block of the same component (DC predictor), -1 at the start.
+__host__ __device__ __forceinline__ int enc_prev_same(int blk) {
+    const int m = blk / 6, b = blk - 6 * (blk / 6);
+    if (b >= 1 && b <= 3) return blk - 1;
+    if (m == 0) return -1;
+    return b == 0 ? blk - 3 : blk - 6;
+}
+
+// Huffman encode tables (jchuff.c jpeg_make_c_derived_tbl): code and length per symbol.
+struct HuffEnc {
+    uint16_t code[256];
+    uint8_t len[256];
+};
+
+// Bit count of |v| (jchuff.c: nbits of the magnitude).
+__host__ __device__ __forceinline__ int nbits_of(int v) {
+    uint32_t a = (uint32_t)(v < 0 ? -v : v);
+    int n = 0;
+    while (a) { ++n; a >>= 1; }
+    return n;
+}
+
+// One block's Huffman bits (jchuff.c encode_one_block): calls put(code, len) in stream order.
+// blk: quantised coefficients in natural order; nat: zig-zag -> natural.
+template <class Put>
+__host__ __device__ __forceinline__ void encode_block(const int16_t *blk, int dc_diff, const HuffEnc *dct,
+                                                      const HuffEnc *act, const uint8_t *nat, Put &put) {
+    int t2 = dc_diff < 0 ? dc_diff - 1 : dc_diff;
+    int nb = nbits_of(dc_diff);
+    put(dct->code[nb], dct->len[nb]);
+    if (nb) put((uint32_t)t2 & ((1u << nb) - 1), nb);
+    int r = 0;
+    for (int k = 1; k < 64; ++k) {
+        const int v = blk[nat[k]];
+        if (v == 0) { ++r; continue; }
+        while (r > 15) { put(act->code[0xF0], act->len[0xF0]); r -= 16; }
+        nb = nbits_of(v);
+        const int sym = (r << 4) + nb;
+        put(act->code[sym], act->len[sym]);
+        put((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1), nb);
+        r = 0;
+    }
+    if (r > 0) put(act->code[0], act->len[0]);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Host side: marker parsing (jdmarker.c restated for the markers a baseline file carries) and
 // the decode-form tables.
 struct Parsed {
@@ -393,10 +586,17 @@ struct Parsed {
 void std_huff(int cls, int id, uint8_t *bits17, uint8_t *vals256);
 // Returns 0 or a PANO_E_* code; *err gets a message.
 int parse(const uint8_t *buf, size_t len, Parsed *out, std::string *err);
-// Builds the decode form of a (bits, vals) table; false if the code lengths are invalid.
-bool make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *out);
+// Builds the decode form of a (bits, vals) table: PANO_OK, PANO_E_ARG (invalid code lengths)
+// or PANO_E_UNSUPPORTED (long codes spread over more than kHuffSub 9-bit prefixes).
+int make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *out);
 // Frame geometry (MCU layout, component planes, upsampling mode) of a parsed file; the
 // arena offsets and table indices are filled in by the caller.
 int plan_frame(const Parsed &P, Frame *F, std::string *err);
+// Encoder side: jcparam.c jpeg_set_quality tables (natural order) and the Annex K encode
+// tables; the file header libjpeg-turbo writes for a 3-component 4:2:0 baseline image
+// (SOI, JFIF APP0 1.01, DQT x2, SOF0, DHT x4, SOS), as PIL's save(quality=q) does.
+void quant_tables(int quality, uint16_t *lum64, uint16_t *chr64);
+void std_huff_enc(int cls, int id, HuffEnc *out);
+std::vector<uint8_t> encode_header(int h, int w, const uint16_t *lum64, const uint16_t *chr64);
 
 }  // namespace pj

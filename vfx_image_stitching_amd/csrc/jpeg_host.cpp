@@ -2,6 +2,7 @@
 // libjpeg's jdmarker.c a sequential file needs), Huffman decode tables (jdhuff.c
 // jpeg_make_d_derived_tbl restated) and the Annex K.3 standard tables.  Everything that
 // touches pixels runs on the GPU (jpeg.hip); this file only reads headers.
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/pano.h"
@@ -63,13 +64,78 @@ void std_huff(int cls, int id, uint8_t *bits17, uint8_t *vals256) {
     }
 }
 
-bool make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *T) {
-    // jdhuff.c jpeg_make_d_derived_tbl: code lengths -> canonical codes, per-length maxcode and
-    // value offsets, then the 9-bit lookahead table.
+void std_huff_enc(int cls, int id, HuffEnc *E) {
+    // jchuff.c jpeg_make_c_derived_tbl over the Annex K table: canonical codes by length
+    uint8_t bits[17], vals[256];
+    std_huff(cls, id, bits, vals);
+    memset(E, 0, sizeof(*E));
+    int code = 0, p = 0;
+    for (int l = 1; l <= 16; ++l) {
+        for (int i = 0; i < bits[l]; ++i, ++p) {
+            E->code[vals[p]] = (uint16_t)code++;
+            E->len[vals[p]] = (uint8_t)l;
+        }
+        code <<= 1;
+    }
+}
+
+void quant_tables(int quality, uint16_t *lum, uint16_t *chr) {
+    // jcparam.c: Annex K.1 tables (natural order) scaled by jpeg_quality_scaling, clamped to
+    // [1, 255] (force_baseline), as jpeg_set_quality(cinfo, quality, TRUE)
+    static const uint16_t kLum[64] = {
+        16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55,
+        14, 13, 16, 24, 40, 57, 69, 56, 14, 17, 22, 29, 51, 87, 80, 62,
+        18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+        49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+    static const uint16_t kChr[64] = {
+        17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+        24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+        99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+        99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+    if (quality <= 0) quality = 1;
+    if (quality > 100) quality = 100;
+    const long scale = quality < 50 ? 5000 / quality : 200 - quality * 2;
+    for (int i = 0; i < 64; ++i) {
+        long a = ((long)kLum[i] * scale + 50) / 100, b = ((long)kChr[i] * scale + 50) / 100;
+        lum[i] = (uint16_t)(a < 1 ? 1 : (a > 255 ? 255 : a));
+        chr[i] = (uint16_t)(b < 1 ? 1 : (b > 255 ? 255 : b));
+    }
+}
+
+std::vector<uint8_t> encode_header(int h, int w, const uint16_t *lum, const uint16_t *chr) {
+    // jcmarker.c write_file_header / write_frame_header / write_scan_header for a baseline
+    // 3-component 4:2:0 image with the default JFIF header and the Annex K Huffman tables
+    std::vector<uint8_t> o = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00, 0x01, 0x01,
+                              0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00};
+    for (int t = 0; t < 2; ++t) {
+        const uint16_t *q = t ? chr : lum;
+        o.insert(o.end(), {0xFF, 0xDB, 0x00, 0x43, (uint8_t)t});
+        for (int k = 0; k < 64; ++k) o.push_back((uint8_t)q[natural_order(k)]);
+    }
+    o.insert(o.end(), {0xFF, 0xC0, 0x00, 0x11, 0x08, (uint8_t)(h >> 8), (uint8_t)h, (uint8_t)(w >> 8), (uint8_t)w,
+                       0x03, 0x01, 0x22, 0x00, 0x02, 0x11, 0x01, 0x03, 0x11, 0x01});
+    for (int id = 0; id < 2; ++id)
+        for (int cls = 0; cls < 2; ++cls) {
+            uint8_t bits[17], vals[256];
+            std_huff(cls, id, bits, vals);
+            int total = 0;
+            for (int l = 1; l <= 16; ++l) total += bits[l];
+            const int len = 2 + 1 + 16 + total;
+            o.insert(o.end(), {0xFF, 0xC4, (uint8_t)(len >> 8), (uint8_t)len, (uint8_t)(cls << 4 | id)});
+            o.insert(o.end(), bits + 1, bits + 17);
+            o.insert(o.end(), vals, vals + total);
+        }
+    o.insert(o.end(), {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x00, 0x02, 0x11, 0x03, 0x11, 0x00, 0x3F, 0x00});
+    return o;
+}
+
+int make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *T) {
+    // jdhuff.c jpeg_make_d_derived_tbl: code lengths -> canonical codes; then the two-level
+    // lookup of jpeg_core.h (9 bits, then 7 more for the longer codes).
     int size[257], code[257];
     int p = 0;
     for (int l = 1; l <= 16; ++l) {
-        if (p + bits17[l] > 256) return false;
+        if (p + bits17[l] > 256) return PANO_E_ARG;
         for (int i = 0; i < bits17[l]; ++i) size[p++] = l;
     }
     size[p] = 0;
@@ -78,30 +144,33 @@ bool make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *T) {
     p = 0;
     while (size[p]) {
         while (size[p] == si) code[p++] = c++;
-        if (c >= (1 << si)) return false;     // JERR_BAD_HUFF_TABLE
+        if (c >= (1 << si)) return PANO_E_ARG;     // JERR_BAD_HUFF_TABLE
         c <<= 1;
         ++si;
     }
     memset(T, 0, sizeof(*T));
-    p = 0;
-    for (int l = 1; l <= 16; ++l) {
-        if (bits17[l]) {
-            T->valoff[l] = p - code[p];
-            p += bits17[l];
-            T->maxcode[l] = code[p - 1];
-        } else {
-            T->maxcode[l] = -1;
-        }
-    }
-    T->maxcode[17] = 0x7FFFFFFF;
-    memcpy(T->vals, vals, (size_t)total);
+    int nsub = 0;
     for (int i = 0; i < total; ++i) {
         const int l = size[i];
-        if (l > 9) continue;
-        const int lo = code[i] << (9 - l), hi = (code[i] + 1) << (9 - l);
-        for (int e = lo; e < hi; ++e) T->lut[e] = (uint16_t)(l << 8 | vals[i]);
+        const uint16_t e = (uint16_t)(l << 8 | vals[i]);
+        if (l <= 9) {
+            const int lo = code[i] << (9 - l), hi = (code[i] + 1) << (9 - l);
+            for (int q = lo; q < hi; ++q) T->lut[q] = e;
+            continue;
+        }
+        const int pre = code[i] >> (l - 9);             // first 9 bits of the code
+        if (!(T->lut[pre] & 0x8000)) {
+            if (T->lut[pre] != 0) return PANO_E_ARG;    // a shorter code is its prefix
+            if (nsub == kHuffSub) return PANO_E_UNSUPPORTED;
+            T->lut[pre] = (uint16_t)(0x8000 | nsub * 128);
+            ++nsub;
+        }
+        uint16_t *sub = T->sub + (T->lut[pre] & 0x7FFF);
+        const int rest = code[i] & ((1 << (l - 9)) - 1);    // the code's bits after the first 9
+        const int lo = rest << (16 - l), hi = (rest + 1) << (16 - l);
+        for (int q = lo; q < hi; ++q) sub[q] = e;
     }
-    return true;
+    return PANO_OK;
 }
 
 int parse(const uint8_t *buf, size_t len, Parsed *P, std::string *err) {
@@ -282,15 +351,17 @@ int plan_frame(const Parsed &P, Frame *F, std::string *err) {
         if (F->upsample && F->comp_dw[1] <= 2) return fail(err, PANO_E_UNSUPPORTED, "JPEG narrower than 5 pixels");
     }
     F->total_blocks = F->mcus_x * F->mcus_y * F->bpm;
-    // Warm-up window of the start search (jpeg.hip jpeg_sync_warm): ~8 MCUs' worth of bits,
-    // in [4096, 32768].  A decode started at a wrong bit position re-synchronises only when it
-    // also lands in the right block of the MCU, so the distance scales with the MCU size
-    // (measured on the reference's frames: 0.1 % of subsequences need the fallback).
+    // Warm-up window of the start search (jpeg.hip jpeg_sync_warm): ~6 MCUs' worth of bits
+    // (PANO_JPEG_WARM_MCUS), in [2048, 16384].  A decode started at a wrong bit position
+    // re-synchronises only when it also lands in the right block of the MCU, so the distance
+    // scales with the bits per MCU.
     {
+        const char *env = getenv("PANO_JPEG_WARM_MCUS");
+        const uint64_t m = env && atoi(env) > 0 ? (uint64_t)atoi(env) : 6;
         const uint64_t mcus = (uint64_t)F->mcus_x * F->mcus_y;
-        const uint64_t w8 = 8 * (uint64_t)P.ecs_len * 8 / (mcus ? mcus : 1);
-        const uint64_t wr = (w8 + kSubBits - 1) / kSubBits * kSubBits;
-        F->warm = (uint32_t)(wr < 4096 ? 4096 : (wr > 32768 ? 32768 : wr));
+        const uint64_t wb = m * (uint64_t)P.ecs_len * 8 / (mcus ? mcus : 1);
+        const uint64_t wr = (wb + kSubBits - 1) / kSubBits * kSubBits;
+        F->warm = (uint32_t)(wr < 2048 ? 2048 : (wr > 16384 ? 16384 : wr));
     }
     if (P.restart > 0 && P.restart < F->mcus_x * F->mcus_y)
         return fail(err, PANO_E_UNSUPPORTED, "JPEG with restart intervals");

@@ -122,8 +122,10 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->jscratch) (void)hipFree(ctx->jscratch);
-    if (ctx->jpin) (void)hipHostFree(ctx->jpin);
-    if (ctx->jev) (void)hipEventDestroy(ctx->jev);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->jpin[i]) (void)hipHostFree(ctx->jpin[i]);
+        if (ctx->jev[i]) (void)hipEventDestroy(ctx->jev[i]);
+    }
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
     delete ctx;
     return PANO_OK;
@@ -419,6 +421,16 @@ int pano_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const siz
     if (ctx->capturing)
         return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_jpeg_decode reads host files: not capturable");
     return launch_jpeg_decode(ctx, n, bufs, lens, bgr, h, w, status);
+}
+
+int pano_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t pitch, int quality,
+                     uint8_t *h_out, size_t cap, size_t *out_len) {
+    if (!ctx) return PANO_E_ARG;
+    if (!bgr || h <= 0 || w <= 0 || h > 65535 || w > 65535 || pitch < 3 * (int64_t)w || quality < 1 || quality > 100)
+        return pano_fail(ctx, PANO_E_ARG, "pano_jpeg_encode: bad arguments");
+    if (ctx->capturing)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_jpeg_encode writes host memory: not capturable");
+    return launch_jpeg_encode(ctx, bgr, h, w, pitch, quality, h_out, cap, out_len);
 }
 
 int pano_prof_enable(pano_ctx *ctx, int kernel_class) {

@@ -101,11 +101,13 @@ struct pano_ctx {
     void *hscratch = nullptr; size_t hscratch_bytes = 0;
     // ---- blend scratch
     void *bscratch = nullptr; size_t bscratch_bytes = 0;
-    // ---- JPEG decode (jpeg.hip): device scratch, pinned upload staging and the event that
-    // says when the last upload out of the staging buffer has completed
+    // ---- JPEG decode (jpeg.hip): device scratch, two pinned upload staging buffers used in
+    // turn, and per buffer the event that says when the upload out of it has completed (the
+    // host fills one while the other's upload may still be queued)
     void *jscratch = nullptr; size_t jscratch_bytes = 0;
-    void *jpin = nullptr; size_t jpin_bytes = 0;
-    hipEvent_t jev = nullptr;
+    void *jpin[2] = {nullptr, nullptr}; size_t jpin_bytes[2] = {0, 0};
+    hipEvent_t jev[2] = {nullptr, nullptr};
+    int jslot = 0;
     // ---- side stream: the small-octave blur tail runs there, overlapped with the extrema
     // scan of the large octaves (fork / join by events; see launch_sift_pyramid)
     hipStream_t side = nullptr;
@@ -250,6 +252,9 @@ int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, i
 // Baseline JPEG files in host memory -> u8 BGR [n][h][w][3] on the device (jpeg.hip).
 int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const size_t *lens, uint8_t *bgr,
                        int h, int w, int32_t *status);
+// u8 BGR rows on the device -> a baseline JPEG file in host memory (jpeg_enc.hip).
+int launch_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t pitch, int quality,
+                       uint8_t *h_out, size_t cap, size_t *out_len);
 
 // ---- device helpers
 // XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"):

@@ -1,4 +1,5 @@
-"""JPEG decode on the GPU: the reference's ``cv2.imread``.
+"""JPEG decode and encode on the GPU: the reference's ``cv2.imread``
+and ``cv2.imwrite``.
 
 The reference reads every frame with ``cv2.imread(full_p)`` (image_stitching_sift.py:282,
 image_stitching_harris.py:394), i.e. libjpeg-turbo's default decode to BGR uint8.
@@ -6,6 +7,10 @@ image_stitching_harris.py:394), i.e. libjpeg-turbo's default decode to BGR uint8
 bit-identical to libjpeg-turbo (and to PIL, which the harness uses on the host):
 
     frames = decode_batch([open(p, 'rb').read() for p in paths])   # torch u8 [n, h, w, 3] BGR
+
+``encode(img)`` is the reference's ``cv2.imwrite(path, panorama)`` (image_stitching_sift.py:386,
+OpenCV's default quality 95): the file bytes, byte-identical to libjpeg-turbo's encoder (PIL's
+``save(quality=q)``), computed on the GPU from the device image (a crop view is fine).
 
 Only headers are parsed on the host; the entropy-coded bytes go to the GPU in one copy and
 the Huffman decode (self-synchronising, no restart markers needed), the islow IDCT, the fancy
@@ -71,3 +76,29 @@ def imread(path: str, device: int | None = None):
     device tensor (the reference's array, resident where the stitch needs it)."""
     with open(path, "rb") as f:
         return decode_batch([f.read()], device=device)[0]
+
+
+def encode(img, quality: int = 95) -> bytes:
+    """JPEG file bytes of a u8 [h, w, 3] BGR device tensor (row-contiguous pixels; any row
+    stride, e.g. the panorama view of the canvas), encoded on the GPU."""
+    import torch
+    if not img.is_cuda or img.dtype != torch.uint8 or img.dim() != 3 or img.shape[2] != 3:
+        raise PanoError(_lib.PANO_E_ARG, "encode: expected a uint8 [h, w, 3] device tensor")
+    if img.stride(2) != 1 or img.stride(1) != 3:
+        raise PanoError(_lib.PANO_E_ARG, "encode: pixels of a row must be contiguous")
+    h, w = int(img.shape[0]), int(img.shape[1])
+    ctx = context(img.device.index)
+    cap = ctypes.c_size_t(0)
+    size = 1024 + h * w * 4
+    out = np.empty(size, np.uint8)
+    rc = ctx.lib.pano_jpeg_encode(ctx.h, ctypes.c_void_p(img.data_ptr()), h, w, img.stride(0), int(quality),
+                                  out.ctypes.data_as(ctypes.c_void_p), size, ctypes.byref(cap))
+    ctx.check(rc)
+    return out[:cap.value].tobytes()
+
+
+def imwrite(path: str, img, quality: int = 95) -> bool:
+    """cv2.imwrite(path, img) for a device image, encoded on the GPU."""
+    with open(path, "wb") as f:
+        f.write(encode(img, quality))
+    return True
