@@ -86,12 +86,11 @@ int main(int argc, char **argv) {
     for (uint32_t t = 0; t < nsub; ++t)
         for (int j = 0; j < NP; ++j) {
             const uint32_t p0 = t * (uint32_t)L;
-            SinkNone sn;
             const size_t q = (size_t)t * NS + j;
-            cand[q] = p0 <= W ? walk(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, sn)
-                              : walk(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, sn);
+            cand[q] = p0 <= W ? walk_sync<false>(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, nullptr)
+                              : walk_sync<false>(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, nullptr);
             SinkCount sc;
-            ex[q] = walk(words, 0, nw, cand[q], end_of(t), T, F.mcu_comp, F.bpm, sc);
+            ex[q] = walk_sync<true>(words, 0, nw, cand[q], end_of(t), T, F.mcu_comp, F.bpm, &sc);
             cstats[q] = sc.stats();
             ++decoded;
         }
@@ -107,7 +106,7 @@ int main(int argc, char **argv) {
             const size_t q = (size_t)t * NS + NP + i;
             SinkCount sc;
             cand[q] = e;
-            ex[q] = walk(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, sc);
+            ex[q] = walk_sync<true>(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, &sc);
             cstats[q] = sc.stats();
             ++fix_slots;
         }
@@ -125,7 +124,7 @@ int main(int argc, char **argv) {
             ++fails;
             SinkCount sc;
             start[t] = prev_exit;
-            prev_exit = walk(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, sc);
+            prev_exit = walk_sync<true>(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, &sc);
             stats[t] = sc.stats();
         } else {
             start[t] = cand[(size_t)t * NS + jj];
@@ -153,10 +152,12 @@ int main(int argc, char **argv) {
         SinkWrite w;
         w.coef = coef.data(); w.F = &F; w.nat = nat;
         const int k0 = state_k(start[t]);
-        w.blk = scan[t].blocks - (k0 > 0 ? 1 : 0);
+        const int32_t b0 = scan[t].blocks - (k0 > 0 ? 1 : 0);
+        w.seek(b0 > 0 ? b0 : 0);
+        w.blk = b0;
         w.p0 = scan[t].dc[0]; w.p1 = scan[t].dc[1]; w.p2 = scan[t].dc[2];
-        w.live = k0 > 0 && w.blk >= 0 && w.blk < F.total_blocks;
-        w.addr = w.live ? block_addr(F, w.blk) : 0;
+        w.live = k0 > 0 && b0 >= 0 && b0 < F.total_blocks;
+        w.addr = w.live ? w.address() : 0;
         walk(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, w);
     }
     // IDCT

@@ -224,12 +224,11 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_warm(Dev D) {
         return;
     }
     const uint32_t p0 = t * kSubBits;
-    SinkNone sn;
-    const uint64_t s0 = p0 <= W ? walk(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, sn)
-                                : walk(win, w0, nwin, pack_state(p0 - W, (int)j, 0), p0, L.T, L.mcu_comp, F.bpm, sn);
+    const uint64_t s0 = p0 <= W ? walk_sync<false>(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, nullptr)
+                                : walk_sync<false>(win, w0, nwin, pack_state(p0 - W, (int)j, 0), p0, L.T, L.mcu_comp, F.bpm, nullptr);
     const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
     SinkCount sc;
-    const uint64_t x = walk(win, w0, nwin, s0, end, L.T, L.mcu_comp, F.bpm, sc);
+    const uint64_t x = walk_sync<true>(win, w0, nwin, s0, end, L.T, L.mcu_comp, F.bpm, &sc);
     const size_t q = (size_t)(F.sub0 + t) * D.nps + j;
     D.cand[q] = s0;
     D.cexit[q] = x;
@@ -275,7 +274,7 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix(Dev D) {
     const uint32_t p0 = t * kSubBits;
     const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
     SinkCount sc;
-    const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
+    const uint64_t x = walk_sync<true>(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, &sc);
     const size_t q = (size_t)(F.sub0 + t) * nps + np + i;
     D.cand[q] = e;
     D.cexit[q] = x;
@@ -423,7 +422,7 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
                 const uint64_t e = s_exit;
                 const uint32_t end = (base + 1) * kSubBits < nb ? (base + 1) * kSubBits : nb;
                 SinkCount sc;
-                const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
+                const uint64_t x = walk_sync<true>(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, &sc);
                 D.start[S0 + base] = e;
                 D.scan[S0 + base] = s_acc;
                 s_acc.blocks += sc.blocks;
@@ -473,12 +472,14 @@ __global__ void __launch_bounds__(kWriteThreads) jpeg_write(Dev D) {
     w.F = &Fs;
     w.nat = L.nat;
     const int k0 = state_k(s0);
-    w.blk = sc.blocks - (k0 > 0 ? 1 : 0);
+    const int32_t b0 = sc.blocks - (k0 > 0 ? 1 : 0);
+    w.seek(b0 > 0 ? b0 : 0);
+    w.blk = b0;
     w.p0 = sc.dc[0];
     w.p1 = sc.dc[1];
     w.p2 = sc.dc[2];
-    w.live = k0 > 0 && w.blk >= 0 && w.blk < Fs.total_blocks;
-    w.addr = w.live ? block_addr(Fs, w.blk) : 0;
+    w.live = k0 > 0 && b0 >= 0 && b0 < Fs.total_blocks;
+    w.addr = w.live ? w.address() : 0;
     const uint32_t end = (t + 1) * kSubBits < nb ? (t + 1) * kSubBits : nb;
     walk(win, w0, nwin, s0, end, L.T, L.mcu_comp, Fs.bpm, w);
 }

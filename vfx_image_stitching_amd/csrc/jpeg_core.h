@@ -221,6 +221,68 @@ __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_
     return pack_state(br.pos(), b, k);
 }
 
+// Branch-free walk for the synchronisation passes (no coefficient output).  Lanes of a wave sit
+// at different decoder states (DC or AC next, code lengths, block ends); here every codeword
+// takes one instruction path -- the next stream word, the second-level table entry and the
+// MCU-layout entry are always read and chosen by selects -- so divergent lanes do not
+// serialise.  Same states and statistics as walk() with SinkNone / SinkCount.
+template <bool COUNT>
+__host__ __device__ __forceinline__ uint64_t walk_sync(const uint32_t *words, uint32_t woff, uint32_t nwords,
+                                                       uint64_t start, uint32_t end, const Huff *T,
+                                                       const int8_t *mcu_comp, int bpm, SinkCount *sc) {
+    Bits br;
+    br.init(words, woff, nwords, state_pos(start));
+    int b = state_b(start), k = state_k(start);
+    int c = mcu_comp[b];
+    uint32_t guard = end - state_pos(start) + 64;
+    int32_t nblk = 0, d0 = 0, d1 = 0, d2 = 0;
+    while (br.pos() < end && guard--) {
+        // refill: cnt >= 32 after it
+        const uint32_t nxt = br.load(br.wi);
+        const bool need = br.cnt < 32;
+        br.buf |= need ? (uint64_t)nxt << ((32 - br.cnt) & 63) : 0ull;
+        br.wi += need ? 1u : 0u;
+        br.cnt += need ? 32 : 0;
+        // symbol: two-level lookup, both levels read
+        const bool isdc = k == 0;
+        const Huff *Tt = T + (isdc ? c : 3 + c);
+        const uint32_t p = (uint32_t)(br.buf >> 48);
+        const uint32_t e1 = Tt->lut[p >> 7];
+        const uint32_t e2 = Tt->sub[((e1 & 0x7FFF) + (p & 127)) & (kHuffSub * 128 - 1)];
+        const uint32_t e = (e1 & 0x8000) ? e2 : e1;
+        const int len = (int)(e >> 8) ? (int)(e >> 8) : 16;
+        const int sym = (int)(e & 0xFF);
+        br.buf <<= len;
+        br.cnt -= len;
+        const int r = isdc ? 0 : sym >> 4;
+        const int s = isdc ? (sym > 16 ? 16 : sym) : (sym & 15);
+        const int raw = s ? (int)(br.buf >> ((64 - s) & 63)) : 0;
+        br.buf <<= s;
+        br.cnt -= s;
+        if (COUNT) {
+            const int v = s ? huff_extend(raw, s) : 0;
+            const int dv = isdc ? v : 0;
+            nblk += isdc ? 1 : 0;
+            d0 += c == 0 ? dv : 0;
+            d1 += c == 1 ? dv : 0;
+            d2 += c == 2 ? dv : 0;
+        }
+        const int kn = isdc ? 1 : (s ? k + r + 1 : (r == 15 ? k + 16 : 64));
+        const bool eob = kn >= 64;
+        const int bn = eob ? (b + 1 == bpm ? 0 : b + 1) : b;
+        k = eob ? 0 : kn;
+        b = bn;
+        c = mcu_comp[bn];
+    }
+    if (COUNT) {
+        sc->blocks += nblk;
+        sc->d0 += d0;
+        sc->d1 += d1;
+        sc->d2 += d2;
+    }
+    return pack_state(br.pos(), b, k);
+}
+
 // Block index (MCU order) -> coefficient block address (int16 elements).
 __host__ __device__ __forceinline__ uint64_t block_addr(const Frame &F, int32_t blk) {
     const int32_t m = blk / F.bpm, bb = blk - m * F.bpm;
@@ -231,21 +293,36 @@ __host__ __device__ __forceinline__ uint64_t block_addr(const Frame &F, int32_t 
     return F.coef_off[c] + ((uint64_t)by * F.comp_bw[c] + bx) * 64;
 }
 
-// Writes coefficients of the blocks a subsequence decodes (natural order, DC predicted).
+// Writes coefficients of the blocks a subsequence decodes (natural order, DC predicted).  The
+// block position advances incrementally (block of the MCU, MCU column, MCU row): no division
+// per block.
 struct SinkWrite {
     int16_t *coef;
     const Frame *F;
     const uint8_t *nat;           // natural_order(k) for k < 80 (a table in LDS / host memory)
     int32_t blk;                  // current block index (MCU order)
+    int32_t bb, mx, my;           // its block of the MCU, MCU column and row
     int32_t p0, p1, p2;           // DC predictors of components 0..2
     uint64_t addr;                // current block's address
     bool live;
+    __host__ __device__ __forceinline__ void seek(int32_t b) {     // position of block b
+        blk = b;
+        const int32_t m = b / F->bpm;
+        bb = b - m * F->bpm;
+        mx = m % F->mcus_x;
+        my = m / F->mcus_x;
+    }
+    __host__ __device__ __forceinline__ uint64_t address() const {
+        const int c = F->mcu_comp[bb];
+        return F->coef_off[c] + ((uint64_t)(my * F->comp_v[c] + F->mcu_by[bb]) * F->comp_bw[c] +
+                                 mx * F->comp_h[c] + F->mcu_bx[bb]) * 64;
+    }
     __host__ __device__ __forceinline__ bool dc(int c, int diff) {
         if (blk >= F->total_blocks) return false;
         p0 += c == 0 ? diff : 0;
         p1 += c == 1 ? diff : 0;
         p2 += c == 2 ? diff : 0;
-        addr = block_addr(*F, blk);
+        addr = address();
         live = true;
         coef[addr] = (int16_t)(c == 0 ? p0 : (c == 1 ? p1 : p2));
         return true;
@@ -253,7 +330,14 @@ struct SinkWrite {
     __host__ __device__ __forceinline__ void ac(int k, int v) {
         if (live) coef[addr + nat[k < 80 ? k : 79]] = (int16_t)v;
     }
-    __host__ __device__ __forceinline__ void end_block() { ++blk; live = false; }
+    __host__ __device__ __forceinline__ void end_block() {
+        ++blk;
+        live = false;
+        if (++bb == F->bpm) {
+            bb = 0;
+            if (++mx == F->mcus_x) { mx = 0; ++my; }
+        }
+    }
 };
 
 // ---------------------------------------------------------------------------------------------
