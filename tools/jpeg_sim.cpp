@@ -45,7 +45,7 @@ int main(int argc, char **argv) {
             const int id = cls ? P.comp_ac[c] : P.comp_dc[c];
             if (P.h_ok[cls][id]) { memcpy(bits, P.hbits[cls][id], 17); memcpy(vals, P.hvals[cls][id], 256); }
             else std_huff(cls, id, bits, vals);
-            const int hr = make_huff(bits, vals, &T[cls * 3 + c]);
+            const int hr = make_huff(cls, bits, vals, &T[cls * 3 + c]);
             if (hr) { printf("{\"status\": %d, \"error\": \"huffman table\"}\n", hr); return 1; }
         }
 
@@ -87,10 +87,11 @@ int main(int argc, char **argv) {
         for (int j = 0; j < NP; ++j) {
             const uint32_t p0 = t * (uint32_t)L;
             const size_t q = (size_t)t * NS + j;
-            cand[q] = p0 <= W ? walk_sync<false>(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, nullptr)
-                              : walk_sync<false>(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, nullptr);
+            SinkNone sn;
+            cand[q] = p0 <= W ? walk(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, sn)
+                              : walk(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, sn);
             SinkCount sc;
-            ex[q] = walk_sync<true>(words, 0, nw, cand[q], end_of(t), T, F.mcu_comp, F.bpm, &sc);
+            ex[q] = walk(words, 0, nw, cand[q], end_of(t), T, F.mcu_comp, F.bpm, sc);
             cstats[q] = sc.stats();
             ++decoded;
         }
@@ -106,7 +107,7 @@ int main(int argc, char **argv) {
             const size_t q = (size_t)t * NS + NP + i;
             SinkCount sc;
             cand[q] = e;
-            ex[q] = walk_sync<true>(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, &sc);
+            ex[q] = walk(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, sc);
             cstats[q] = sc.stats();
             ++fix_slots;
         }
@@ -124,7 +125,7 @@ int main(int argc, char **argv) {
             ++fails;
             SinkCount sc;
             start[t] = prev_exit;
-            prev_exit = walk_sync<true>(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, &sc);
+            prev_exit = walk(words, 0, nw, start[t], end_of(t), T, F.mcu_comp, F.bpm, sc);
             stats[t] = sc.stats();
         } else {
             start[t] = cand[(size_t)t * NS + jj];

@@ -57,7 +57,7 @@ struct Dev {
 };
 
 constexpr uint64_t kNoCand = ~0ull;
-constexpr int kMargin = 8;      // words staged past a window's last bit (Bits prefetch + one code)
+constexpr int kMargin = 8;      // words staged past a window's last bit (the 32-bit peek of its last code)
 
 // ---------------------------------------------------------------------------------------- LDS
 // A frame's decode tables in LDS: DC / AC per component + the MCU layout.
@@ -224,11 +224,12 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_warm(Dev D) {
         return;
     }
     const uint32_t p0 = t * kSubBits;
-    const uint64_t s0 = p0 <= W ? walk_sync<false>(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, nullptr)
-                                : walk_sync<false>(win, w0, nwin, pack_state(p0 - W, (int)j, 0), p0, L.T, L.mcu_comp, F.bpm, nullptr);
+    SinkNone sn;
+    const uint64_t s0 = p0 <= W ? walk(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, sn)
+                                : walk(win, w0, nwin, pack_state(p0 - W, (int)j, 0), p0, L.T, L.mcu_comp, F.bpm, sn);
     const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
     SinkCount sc;
-    const uint64_t x = walk_sync<true>(win, w0, nwin, s0, end, L.T, L.mcu_comp, F.bpm, &sc);
+    const uint64_t x = walk(win, w0, nwin, s0, end, L.T, L.mcu_comp, F.bpm, sc);
     const size_t q = (size_t)(F.sub0 + t) * D.nps + j;
     D.cand[q] = s0;
     D.cexit[q] = x;
@@ -274,7 +275,7 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix(Dev D) {
     const uint32_t p0 = t * kSubBits;
     const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
     SinkCount sc;
-    const uint64_t x = walk_sync<true>(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, &sc);
+    const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
     const size_t q = (size_t)(F.sub0 + t) * nps + np + i;
     D.cand[q] = e;
     D.cexit[q] = x;
@@ -422,7 +423,7 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
                 const uint64_t e = s_exit;
                 const uint32_t end = (base + 1) * kSubBits < nb ? (base + 1) * kSubBits : nb;
                 SinkCount sc;
-                const uint64_t x = walk_sync<true>(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, &sc);
+                const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
                 D.start[S0 + base] = e;
                 D.scan[S0 + base] = s_acc;
                 s_acc.blocks += sc.blocks;
@@ -581,7 +582,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
                     if (tab_keys[k] == key) { ti = (int)k; break; }
                 if (ti < 0) {
                     Huff T;
-                    const int hr = make_huff(bits, vals, &T);
+                    const int hr = make_huff(cls, bits, vals, &T);
                     if (hr) return pano_fail(ctx, hr, "frame " + std::to_string(f) + ": unsupported Huffman table");
                     ti = (int)tabs.size();
                     tabs.push_back(T);

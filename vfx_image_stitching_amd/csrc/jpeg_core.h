@@ -34,9 +34,13 @@ constexpr int kHuffSub = 16;    // second-level lookup tables per Huffman table
 
 // One Huffman table in decode form (jdhuff.c jpeg_make_d_derived_tbl restated as a two-level
 // lookup): the first 9 bits of the stream index lut; codes of up to 9 bits resolve there,
-// longer ones through a 128-entry second-level table indexed by the next 7 bits.  Entries:
-// (code length << 8) | symbol; lut entries with bit 15 set hold a second-level offset; 0 = no
-// such code (only reached off-sync).  One or two LDS reads per symbol, no search loop.
+// longer ones through a 128-entry second-level table indexed by the next 7 bits.  An entry
+// describes the whole codeword: code length - 1 (bits 0-3), the count s of magnitude bits that
+// follow (bits 4-8) and the zig-zag advance - 1 (bits 9-14: 0 for a DC code, the zero run r
+// for an AC coefficient, 15 for ZRL, 63 for EOB) -- so a walker moves by length + s bits and
+// k + advance positions without decoding the symbol.  lut entries with bit 15 set hold a
+// second-level offset; codes the table lacks (reached only off sync) read as a 1-bit code.
+// One or two LDS reads per codeword, no search loop.
 struct Huff {
     uint16_t lut[512];
     uint16_t sub[kHuffSub * 128];
@@ -65,51 +69,25 @@ struct Frame {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Bit reader over a window of the unstuffed stream held as 32-bit words in stream order
-// (word i = bytes 4i..4i+3, first byte in the top bits): w[j] is stream word woff + j.  Words
-// outside [woff, woff + nw) read as zeros (libjpeg pads with zeros after the last marker,
-// jdhuff.c jpeg_fill_bit_buffer; the kernels stage every window a walk can reach).
-struct Bits {
-    const uint32_t *w;
-    uint32_t woff, nw;
-    uint32_t wi;       // next word to load (stream index)
-    int cnt;           // valid bits in buf
-    uint64_t buf;      // left-aligned: the next bit is bit 63
+// The stream is read through a window held as 32-bit words in stream order (word i = bytes
+// 4i..4i+3, first byte in the top bits): w[j] is stream word woff + j.  Words outside
+// [woff, woff + nw) read as zeros (libjpeg pads with zeros after the last marker,
+// jdhuff.c jpeg_fill_bit_buffer; the kernels stage every window a walk can reach in LDS).
+// The 32 stream bits starting at bit `pos` (a codeword plus its magnitude bits fit in 32).
+__host__ __device__ __forceinline__ uint32_t window32(const uint32_t *w, uint32_t woff, uint32_t nw, uint32_t pos) {
+    // clamped indices read unconditionally, then selected: no masked (divergent) loads
+    const uint32_t i = (pos >> 5) - woff, j = i + 1, last = nw - 1;
+    const uint32_t a = w[i < nw ? i : last], b = w[j < nw ? j : last];
+    const uint32_t av = i < nw ? a : 0u, bv = j < nw ? b : 0u;
+    return (uint32_t)(((((uint64_t)av << 32) | bv) << (pos & 31)) >> 32);
+}
 
-    __host__ __device__ __forceinline__ uint32_t load(uint32_t i) const {
-        const uint32_t j = i - woff;
-        return j < nw ? w[j] : 0u;
-    }
-    __host__ __device__ __forceinline__ void fill() {   // requires cnt <= 32
-        buf |= (uint64_t)load(wi++) << (32 - cnt);
-        cnt += 32;
-    }
-    __host__ __device__ __forceinline__ void init(const uint32_t *words, uint32_t word_off, uint32_t nwords,
-                                                  uint32_t pos) {
-        w = words; woff = word_off; nw = nwords; wi = pos >> 5; buf = 0; cnt = 0;
-        fill(); fill();
-        const int s = (int)(pos & 31);
-        buf <<= s; cnt -= s;
-    }
-    __host__ __device__ __forceinline__ void ensure32() { if (cnt < 32) fill(); }
-    __host__ __device__ __forceinline__ uint32_t pos() const { return wi * 32u - (uint32_t)cnt; }
-    __host__ __device__ __forceinline__ void skip(int n) { buf <<= n; cnt -= n; }
-    __host__ __device__ __forceinline__ int get(int n) {   // 1 <= n <= 16
-        const int v = (int)(buf >> (64 - n));
-        skip(n);
-        return v;
-    }
-};
-
-// Decode one Huffman symbol (jdhuff.c jpeg_huff_decode).  A code the table lacks (only off
-// sync) consumes 16 bits and yields symbol 0.
-__host__ __device__ __forceinline__ int huff_decode(const Huff *T, Bits &br) {
-    const uint32_t p = (uint32_t)(br.buf >> 48);
-    uint32_t e = T->lut[p >> 7];
-    if (e & 0x8000) e = T->sub[(e & 0x7FFF) + (p & 127)];
-    const int len = (int)(e >> 8);
-    br.skip(len ? len : 16);
-    return (int)(e & 0xFF);
+// Codeword entry of the table for the bits x (jdhuff.c jpeg_huff_decode): both levels read,
+// the second chosen by a select.
+__host__ __device__ __forceinline__ uint32_t huff_entry(const Huff *T, uint32_t x) {
+    const uint32_t e1 = T->lut[x >> 23];
+    const uint32_t e2 = T->sub[((e1 & 0x7FFF) + ((x >> 16) & 127)) & (kHuffSub * 128 - 1)];
+    return (e1 & 0x8000) ? e2 : e1;
 }
 
 // HUFF_EXTEND (jdhuff.h)
@@ -136,11 +114,13 @@ struct SubStats {
 
 // Sinks for walk(): what to do with each decoded value.
 struct SinkNone {
+    static constexpr bool kValues = false;
     __host__ __device__ __forceinline__ bool dc(int, int) { return true; }
     __host__ __device__ __forceinline__ void ac(int, int) {}
     __host__ __device__ __forceinline__ void end_block() {}
 };
 struct SinkCount {
+    static constexpr bool kValues = true;
     // per-component sums kept in three scalars (a dynamically indexed array would live in
     // scratch memory on the GPU)
     int32_t blocks = 0, d0 = 0, d1 = 0, d2 = 0;
@@ -184,103 +164,42 @@ __host__ __device__ __forceinline__ int natural_order(int k) {
 // Walk the codewords that start in [start, end): from state `start` decode until the bit
 // position reaches `end`; returns the state at the first boundary >= end.  The sink sees
 // every DC difference (dc returns false to stop early) and AC coefficient.  T: the DC tables
-// of components 0..2 followed by their AC tables (T[c], T[3 + c]).
+// of components 0..2 followed by their AC tables (T[c], T[3 + c]).  Every codeword takes one
+// instruction path (selects, not branches) up to the sink calls, so the lanes of a wave, each
+// at its own decoder state, do not serialise on divergent paths.
 template <class Sink>
 __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_t woff, uint32_t nwords,
                                                   uint64_t start, uint32_t end, const Huff *T,
                                                   const int8_t *mcu_comp, int bpm, Sink &sink) {
-    Bits br;
-    br.init(words, woff, nwords, state_pos(start));
+    uint32_t pos = state_pos(start);
     int b = state_b(start), k = state_k(start);
     int c = mcu_comp[b];
-    uint32_t guard = end - state_pos(start) + 64;   // every codeword consumes >= 1 bit
-    while (br.pos() < end && guard--) {
-        br.ensure32();
-        const int sym = huff_decode(T + (k == 0 ? c : 3 + c), br);
-        // DC: the symbol is the difference's bit count; AC: run << 4 | bit count
-        const int r = k == 0 ? 0 : sym >> 4;
-        const int s = k == 0 ? (sym > 16 ? 16 : sym) : (sym & 15);
-        const int v = s ? huff_extend(br.get(s), s) : 0;
-        if (k == 0) {
-            if (!sink.dc(c, v)) break;
-            k = 1;
-        } else if (s) {
-            k += r;
-            sink.ac(k, v);
-            ++k;
-        } else {
-            k = r == 15 ? k + 16 : 64;     // ZRL or EOB
-        }
-        if (k >= 64) {
-            k = 0;
-            b = b + 1 == bpm ? 0 : b + 1;
-            c = mcu_comp[b];
-            sink.end_block();
-        }
-    }
-    return pack_state(br.pos(), b, k);
-}
-
-// Branch-free walk for the synchronisation passes (no coefficient output).  Lanes of a wave sit
-// at different decoder states (DC or AC next, code lengths, block ends); here every codeword
-// takes one instruction path -- the next stream word, the second-level table entry and the
-// MCU-layout entry are always read and chosen by selects -- so divergent lanes do not
-// serialise.  Same states and statistics as walk() with SinkNone / SinkCount.
-template <bool COUNT>
-__host__ __device__ __forceinline__ uint64_t walk_sync(const uint32_t *words, uint32_t woff, uint32_t nwords,
-                                                       uint64_t start, uint32_t end, const Huff *T,
-                                                       const int8_t *mcu_comp, int bpm, SinkCount *sc) {
-    Bits br;
-    br.init(words, woff, nwords, state_pos(start));
-    int b = state_b(start), k = state_k(start);
-    int c = mcu_comp[b];
-    uint32_t guard = end - state_pos(start) + 64;
-    int32_t nblk = 0, d0 = 0, d1 = 0, d2 = 0;
-    while (br.pos() < end && guard--) {
-        // refill: cnt >= 32 after it
-        const uint32_t nxt = br.load(br.wi);
-        const bool need = br.cnt < 32;
-        br.buf |= need ? (uint64_t)nxt << ((32 - br.cnt) & 63) : 0ull;
-        br.wi += need ? 1u : 0u;
-        br.cnt += need ? 32 : 0;
-        // symbol: two-level lookup, both levels read
+    uint32_t guard = end - pos + 64;   // every codeword consumes >= 1 bit
+    while (pos < end && guard--) {
+        const uint32_t x = window32(words, woff, nwords, pos);
         const bool isdc = k == 0;
-        const Huff *Tt = T + (isdc ? c : 3 + c);
-        const uint32_t p = (uint32_t)(br.buf >> 48);
-        const uint32_t e1 = Tt->lut[p >> 7];
-        const uint32_t e2 = Tt->sub[((e1 & 0x7FFF) + (p & 127)) & (kHuffSub * 128 - 1)];
-        const uint32_t e = (e1 & 0x8000) ? e2 : e1;
-        const int len = (int)(e >> 8) ? (int)(e >> 8) : 16;
-        const int sym = (int)(e & 0xFF);
-        br.buf <<= len;
-        br.cnt -= len;
-        const int r = isdc ? 0 : sym >> 4;
-        const int s = isdc ? (sym > 16 ? 16 : sym) : (sym & 15);
-        const int raw = s ? (int)(br.buf >> ((64 - s) & 63)) : 0;
-        br.buf <<= s;
-        br.cnt -= s;
-        if (COUNT) {
-            const int v = s ? huff_extend(raw, s) : 0;
-            const int dv = isdc ? v : 0;
-            nblk += isdc ? 1 : 0;
-            d0 += c == 0 ? dv : 0;
-            d1 += c == 1 ? dv : 0;
-            d2 += c == 2 ? dv : 0;
+        const uint32_t e = huff_entry(T + (isdc ? c : 3 + c), x);
+        const int cl = (int)(e & 15) + 1;
+        const int s = (int)((e >> 4) & 31);
+        const int adv = (int)((e >> 9) & 63) + 1;
+        pos += (uint32_t)(cl + s);
+        if (Sink::kValues) {
+            const uint32_t raw = s ? (x << cl) >> (32 - s) : 0u;
+            const int v = s ? huff_extend((int)raw, s) : 0;
+            if (isdc) {
+                if (!sink.dc(c, v)) break;
+            } else if (s) {
+                sink.ac(k + adv - 1, v);
+            }
         }
-        const int kn = isdc ? 1 : (s ? k + r + 1 : (r == 15 ? k + 16 : 64));
+        const int kn = k + adv;
         const bool eob = kn >= 64;
-        const int bn = eob ? (b + 1 == bpm ? 0 : b + 1) : b;
+        b = eob ? (b + 1 == bpm ? 0 : b + 1) : b;
         k = eob ? 0 : kn;
-        b = bn;
-        c = mcu_comp[bn];
+        c = mcu_comp[b];
+        if (Sink::kValues && eob) sink.end_block();
     }
-    if (COUNT) {
-        sc->blocks += nblk;
-        sc->d0 += d0;
-        sc->d1 += d1;
-        sc->d2 += d2;
-    }
-    return pack_state(br.pos(), b, k);
+    return pack_state(pos, b, k);
 }
 
 // Block index (MCU order) -> coefficient block address (int16 elements).
@@ -297,6 +216,7 @@ __host__ __device__ __forceinline__ uint64_t block_addr(const Frame &F, int32_t 
 // block position advances incrementally (block of the MCU, MCU column, MCU row): no division
 // per block.
 struct SinkWrite {
+    static constexpr bool kValues = true;
     int16_t *coef;
     const Frame *F;
     const uint8_t *nat;           // natural_order(k) for k < 80 (a table in LDS / host memory)
@@ -670,9 +590,10 @@ struct Parsed {
 void std_huff(int cls, int id, uint8_t *bits17, uint8_t *vals256);
 // Returns 0 or a PANO_E_* code; *err gets a message.
 int parse(const uint8_t *buf, size_t len, Parsed *out, std::string *err);
-// Builds the decode form of a (bits, vals) table: PANO_OK, PANO_E_ARG (invalid code lengths)
-// or PANO_E_UNSUPPORTED (long codes spread over more than kHuffSub 9-bit prefixes).
-int make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *out);
+// Builds the decode form of a (bits, vals) table of class cls (0 DC, 1 AC): PANO_OK, PANO_E_ARG
+// (invalid code lengths) or PANO_E_UNSUPPORTED (long codes spread over more than kHuffSub 9-bit
+// prefixes).
+int make_huff(int cls, const uint8_t *bits17, const uint8_t *vals, Huff *out);
 // Frame geometry (MCU layout, component planes, upsampling mode) of a parsed file; the
 // arena offsets and table indices are filled in by the caller.
 int plan_frame(const Parsed &P, Frame *F, std::string *err);

@@ -129,7 +129,7 @@ std::vector<uint8_t> encode_header(int h, int w, const uint16_t *lum, const uint
     return o;
 }
 
-int make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *T) {
+int make_huff(int cls, const uint8_t *bits17, const uint8_t *vals, Huff *T) {
     // jdhuff.c jpeg_make_d_derived_tbl: code lengths -> canonical codes; then the two-level
     // lookup of jpeg_core.h (9 bits, then 7 more for the longer codes).
     int size[257], code[257];
@@ -152,7 +152,12 @@ int make_huff(const uint8_t *bits17, const uint8_t *vals, Huff *T) {
     int nsub = 0;
     for (int i = 0; i < total; ++i) {
         const int l = size[i];
-        const uint16_t e = (uint16_t)(l << 8 | vals[i]);
+        // length - 1 | magnitude bits << 4 | (zig-zag advance - 1) << 9 (jpeg_core.h Huff):
+        // DC advance 1; AC s > 0: run + 1; ZRL 16; EOB (s = 0, any other run) to the end
+        const int sym = vals[i];
+        const int sbits = cls ? (sym & 15) : (sym > 16 ? 16 : sym);
+        const int advm1 = !cls ? 0 : (sbits ? sym >> 4 : ((sym >> 4) == 15 ? 15 : 63));
+        const uint16_t e = (uint16_t)((l - 1) | sbits << 4 | advm1 << 9);
         if (l <= 9) {
             const int lo = code[i] << (9 - l), hi = (code[i] + 1) << (9 - l);
             for (int q = lo; q < hi; ++q) T->lut[q] = e;
