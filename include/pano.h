@@ -348,6 +348,12 @@ int pano_gray_bbox(pano_ctx *ctx, const uint8_t *d_img, int H, int W, int black_
 int pano_jpeg_info(const uint8_t *h_buf, size_t len, int *h, int *w, int *ncomp);
 int pano_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *h_bufs, const size_t *lens,
                      uint8_t *d_bgr, int h, int w, int32_t *d_status);
+/* Synchronisation statistics of the last pano_jpeg_decode (synchronises the stream): per frame
+ * h_stats[4 f + 0] = subsequences the scan was cut into, [4 f + 1] = extra candidates decoded
+ * from a predecessor's exit, [4 f + 2] = subsequences decoded serially from their true start
+ * (none of their candidates reached), [4 f + 3] = 0.  Diagnostics: the output never depends
+ * on them. */
+int pano_jpeg_stats(pano_ctx *ctx, int32_t *h_stats, int n);
 /* cv2.imwrite(path, panorama) (image_stitching_sift.py:386; OpenCV's default quality 95): the
  * u8 BGR image at d_bgr (h rows of w pixels, row pitch `pitch` bytes -- a crop view of a
  * canvas works as is) encoded on the GPU as a baseline JFIF file, YCbCr 4:2:0, byte-identical

@@ -24,5 +24,7 @@ for _ in range(N):
     t_call += time.perf_counter() - a
 torch.cuda.synchronize()
 el = (time.perf_counter() - t0) / N
+st_ = jpeg.last_stats(len(bufs))
+print("sync stats (nsub, fix candidates, serial):", st_[:, :3].sum(0).tolist(), "max serial/frame", int(st_[:, 2].max()))
 print(f"{name}: {len(bufs)} files, {sum(map(len, bufs))} bytes: {el * 1e3:.3f} ms per batch decode "
       f"(host call {t_call / N * 1e3:.3f} ms); status {st.cpu().tolist()}")

@@ -137,6 +137,7 @@ SIGNATURES = {
     "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),
     "pano_jpeg_info": (_I, [_P, ctypes.c_size_t, _PI32, _PI32, _PI32]),
     "pano_jpeg_decode": (_I, [_P, _I, _P, _P, _P, _I, _I, _P]),
+    "pano_jpeg_stats": (_I, [_P, _PI32, _I]),
     "pano_jpeg_encode": (_I, [_P, _P, _I, _I, ctypes.c_int64, _I, _P, ctypes.c_size_t,
                               ctypes.POINTER(ctypes.c_size_t)]),
     "pano_prof_enable": (_I, [_P, _I]),

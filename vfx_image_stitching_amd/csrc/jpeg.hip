@@ -47,6 +47,7 @@ struct Dev {
     uint32_t *chunk_cnt;
     uint32_t *nbits;
     int32_t *flags;
+    int32_t *stats;             // [n][4]: subsequences, fix candidates, serial decodes, 0
     int32_t *status;            // caller's, may be null
     uint64_t *cand;             // [S][nps]: warm slots [0, np), fix slots [np, 2 np)
     uint64_t *cexit;            // [S][nps]
@@ -261,7 +262,10 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix(Dev D) {
         e = D.cexit[qp];
         need = true;
         for (int j = 0; j < F.bpm; ++j) need &= D.cand[qt + j] != e;
-        if (need) any = 1;
+        if (need) {
+            any = 1;
+            atomicAdd(&D.stats[4 * f + 1], 1);
+        }
     }
     if (slot) D.cand[(size_t)(F.sub0 + t) * nps + np + i] = kNoCand;
     __syncthreads();
@@ -416,6 +420,7 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
         __syncthreads();
         if (nres < NT && base < nsub) {
             // every candidate of `base` missed: decode it from the true start (one thread)
+            if (threadIdx.x == 0) D.stats[4 * f + 2] += 1;
             const uint32_t w0 = (base * kSubBits) >> 5, nwin = kSubBits / 32 + kMargin;
             stage_window(D, F, nb, w0, nwin, win);
             __syncthreads();
@@ -441,6 +446,7 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
         if (D.flags[f] & 1) st = PANO_E_UNSUPPORTED;            // a marker inside the scan
         else if (s_acc.blocks < F.total_blocks || nsub == 0) st = PANO_E_ARG;   // truncated
         D.flags[f] = st;
+        D.stats[4 * f] = (int32_t)nsub;
         if (D.status) D.status[f] = st;
     }
 }
@@ -546,6 +552,13 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 }  // namespace
 
+int jpeg_last_stats(pano_ctx *ctx, int32_t *h, int n) {
+    if (!ctx->jstats || n > ctx->jstats_n) return pano_fail(ctx, PANO_E_ARG, "no JPEG decode with that many frames");
+    PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PANO_HIP(ctx, hipMemcpy(h, ctx->jstats, 16 * (size_t)n, hipMemcpyDeviceToHost));
+    return PANO_OK;
+}
+
 int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const size_t *lens, uint8_t *bgr,
                        int h, int w, int32_t *status) {
     // ---- host: parse, plan, tables
@@ -639,6 +652,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     const size_t o_ccnt = dv;    dv = align_up(dv + 4 * (size_t)chunks, 256);
     const size_t o_nbits = dv;   dv = align_up(dv + 4 * (size_t)n, 256);
     const size_t o_flags = dv;   dv = align_up(dv + 4 * (size_t)n, 256);
+    const size_t o_stats = dv;   dv = align_up(dv + 16 * (size_t)n, 256);
     const size_t o_cand = dv;    dv = align_up(dv + 8 * (size_t)subs * nps, 256);
     const size_t o_cexit = dv;   dv = align_up(dv + 8 * (size_t)subs * nps, 256);
     const size_t o_cstats = dv;  dv = align_up(dv + sizeof(SubStats) * (size_t)subs * nps, 256);
@@ -687,6 +701,9 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     D.chunk_cnt = (uint32_t *)(dev + o_ccnt);
     D.nbits = (uint32_t *)(dev + o_nbits);
     D.flags = (int32_t *)(dev + o_flags);
+    D.stats = (int32_t *)(dev + o_stats);
+    ctx->jstats = D.stats;
+    ctx->jstats_n = n;
     D.status = status;
     D.cand = (uint64_t *)(dev + o_cand);
     D.cexit = (uint64_t *)(dev + o_cexit);
@@ -700,6 +717,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     PanoProf prof_(ctx, PK_JPEG);
     rc = launch_fill(ctx, dev + o_coef, 0, 2 * coef_total);
     if (!rc) rc = launch_fill(ctx, dev + o_flags, 0, 4 * (size_t)n);
+    if (!rc) rc = launch_fill(ctx, dev + o_stats, 0, 16 * (size_t)n);
     if (rc) return rc;
     jpeg_unstuff_count<<<chunks, 256, 0, ctx->stream>>>(D);
     jpeg_unstuff_write<<<chunks, 256, 0, ctx->stream>>>(D);

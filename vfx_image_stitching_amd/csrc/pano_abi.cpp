@@ -423,6 +423,11 @@ int pano_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const siz
     return launch_jpeg_decode(ctx, n, bufs, lens, bgr, h, w, status);
 }
 
+int pano_jpeg_stats(pano_ctx *ctx, int32_t *h_stats, int n) {
+    if (!ctx || !h_stats || n <= 0) return PANO_E_ARG;
+    return jpeg_last_stats(ctx, h_stats, n);
+}
+
 int pano_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t pitch, int quality,
                      uint8_t *h_out, size_t cap, size_t *out_len) {
     if (!ctx) return PANO_E_ARG;

@@ -108,6 +108,7 @@ struct pano_ctx {
     void *jpin[2] = {nullptr, nullptr}; size_t jpin_bytes[2] = {0, 0};
     hipEvent_t jev[2] = {nullptr, nullptr};
     int jslot = 0;
+    int32_t *jstats = nullptr; int jstats_n = 0;   // last decode's per-frame sync statistics
     // ---- side stream: the small-octave blur tail runs there, overlapped with the extrema
     // scan of the large octaves (fork / join by events; see launch_sift_pyramid)
     hipStream_t side = nullptr;
@@ -252,6 +253,7 @@ int launch_gray_bbox(pano_ctx *ctx, const uint8_t *img, int H, int W, int thr, i
 // Baseline JPEG files in host memory -> u8 BGR [n][h][w][3] on the device (jpeg.hip).
 int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const size_t *lens, uint8_t *bgr,
                        int h, int w, int32_t *status);
+int jpeg_last_stats(pano_ctx *ctx, int32_t *h, int n);
 // u8 BGR rows on the device -> a baseline JPEG file in host memory (jpeg_enc.hip).
 int launch_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t pitch, int quality,
                        uint8_t *h_out, size_t cap, size_t *out_len);

@@ -71,6 +71,15 @@ def decode_batch(bufs, out=None, status: bool = False, device: int | None = None
     return out
 
 
+def last_stats(n: int, device: int | None = None) -> np.ndarray:
+    """Per-frame synchronisation statistics of the last decode on this device: int32 [n, 4] =
+    (subsequences, extra candidates, serial decodes, 0) -- pano_jpeg_stats."""
+    ctx = context(device)
+    out = np.zeros((n, 4), np.int32)
+    ctx.check(ctx.lib.pano_jpeg_stats(ctx.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n))
+    return out
+
+
 def imread(path: str, device: int | None = None):
     """cv2.imread(path) for a baseline JPEG, decoded on the GPU: a torch u8 [h, w, 3] BGR
     device tensor (the reference's array, resident where the stitch needs it)."""
