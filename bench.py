@@ -446,22 +446,34 @@ def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx):
 
 
 def jpeg_inclusive(st, name, dev, focals, margin, steps, graph, mpx):
-    """File-to-panorama rate: per step the frames' JPEG files (host bytes, the
+    """File-to-file rate: per step the frames' JPEG files (host bytes, the
     reference's cv2.imread input, image_stitching_sift.py:282) are decoded on the GPU straight
     into the resident frame buffer (pano_jpeg_decode: headers parsed on the host, entropy bytes
-    uploaded once), the stitch runs, and the crop's canvas rows come back to pinned host memory.
-    The decode alone and PIL's host decode of the same files (what the harness otherwise runs,
-    one core) are timed beside it; the GPU decode must equal the resident PIL-decoded frames."""
+    uploaded once), the stitch runs, and the cropped panorama is encoded on the GPU into its
+    JPEG file bytes (pano_jpeg_encode, cv2.imwrite at quality 95, :386).  The decode and the
+    encode are also timed alone, with PIL's host decode / encode of the same data (what the
+    harness otherwise runs, one core) beside them; the GPU decode must equal the resident
+    PIL-decoded frames and the GPU file must equal PIL's q95 file byte for byte."""
+    import io
+
     import torch
+    from PIL import Image
+
     from vfx_image_stitching_amd import data, jpeg
     names, bufs = data.load_set_jpegs(name)
     if len(bufs) != dev.shape[0]:
         return None
     ref = dev.clone()
     out, st_ = jpeg.decode_batch(bufs, out=dev, status=True)
-    exact = bool(torch.equal(dev, ref)) and not bool(st_.any())
+    dec_exact = bool(torch.equal(dev, ref)) and not bool(st_.any())
+    sync = jpeg.last_stats(len(bufs))
     res = st.run(dev, focals, margin=margin, graph=graph)
-    host_out = torch.empty(res.canvas.numel(), dtype=torch.uint8).pin_memory()
+    pano = res.panorama
+    file_gpu = jpeg.encode(pano)
+    pano_h = np.ascontiguousarray(pano.cpu().numpy())
+    b = io.BytesIO()
+    Image.fromarray(np.ascontiguousarray(pano_h[..., ::-1])).save(b, "JPEG", quality=95)
+    enc_exact = file_gpu == b.getvalue()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -469,28 +481,35 @@ def jpeg_inclusive(st, name, dev, focals, margin, steps, graph, mpx):
     torch.cuda.synchronize()
     dec_ms = (time.perf_counter() - t0) / steps * 1e3
     t0 = time.perf_counter()
-    for _ in range(max(1, steps // 4)):
-        for b in bufs:
-            data.decode_jpeg(b)
-    pil_ms = (time.perf_counter() - t0) / max(1, steps // 4) * 1e3
-    cur = torch.cuda.current_stream()
+    for _ in range(steps):
+        jpeg.encode(pano)
+    enc_ms = (time.perf_counter() - t0) / steps * 1e3
+    reps = max(1, steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for bb in bufs:
+            data.decode_jpeg(bb)
+    pil_dec_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        Image.fromarray(np.ascontiguousarray(pano_h[..., ::-1])).save(io.BytesIO(), "JPEG", quality=95)
+    pil_enc_ms = (time.perf_counter() - t0) / reps * 1e3
     t0 = time.perf_counter()
     for _ in range(steps):
         jpeg.decode_batch(bufs, out=dev, status=True)
         r = st.run(dev, focals, margin=margin, graph=graph)
-        base = r.canvas.reshape(-1)
-        row = r.canvas.stride(0)
-        first = (r.panorama.storage_offset() - r.canvas.storage_offset()) // row
-        flat = base[first * row:(first + r.panorama.shape[0]) * row]
-        host_out[:flat.numel()].copy_(flat, non_blocking=True)
-        cur.synchronize()
+        jpeg.encode(r.panorama)
     el = (time.perf_counter() - t0) / steps
     return {"value": round(mpx / el, 3), "unit": "Mpx/s", "ms_per_step": round(el * 1e3, 4),
-            "includes": "GPU decode of the frames' JPEG files (host bytes) + stitch + pinned D2H of "
-                        "the crop's canvas rows, per step",
-            "decode_ms": round(dec_ms, 4), "decode_bit_exact_vs_pil": exact,
-            "jpeg_bytes": int(sum(len(b) for b in bufs)),
-            "pil_host_decode_ms": round(pil_ms, 3), "pil_host_decode_cores": 1}
+            "includes": "GPU decode of the frames' JPEG files (host bytes) + stitch + GPU encode of the "
+                        "cropped panorama into its q95 JPEG file (host bytes), per step",
+            "decode_ms": round(dec_ms, 4), "encode_ms": round(enc_ms, 4),
+            "decode_bit_exact_vs_pil": dec_exact, "encode_bytes_equal_pil_q95": enc_exact,
+            "jpeg_bytes_in": int(sum(len(x) for x in bufs)), "jpeg_bytes_out": len(file_gpu),
+            "decode_sync": {"subsequences": int(sync[:, 0].sum()), "fix_candidates": int(sync[:, 1].sum()),
+                            "serial_decodes": int(sync[:, 2].sum())},
+            "pil_host_decode_ms": round(pil_dec_ms, 3), "pil_host_encode_ms": round(pil_enc_ms, 3),
+            "pil_cores": 1}
 
 
 def check_parity(st, dev, focals, margin, workload, method, graph):

@@ -87,9 +87,17 @@ def test_run_panorama_non_interactive(gpu, tmp_path, gold_json):
         (tmp_path / n).write_bytes(z[f"jpg_{n}"].tobytes())
         lines += [f"C:\\Users\\x\\out\\{n}", "428 571", "", f"{f}", ""]
     (tmp_path / "pano.txt").write_text("\n".join(lines))
-    pano, res = ish.run_panorama(str(tmp_path), margin=30)
+    pano, res = ish.run_panorama(str(tmp_path), margin=30)     # GPU JPEG decode + encode
     assert digest(pano) == gold_json("harris_out.json")["pano_digest"]
-    assert (tmp_path / "panoroma_harris.jpg").exists()
+    written = (tmp_path / "panoroma_harris.jpg").read_bytes()
+    # the GPU encoder's file is PIL's (libjpeg-turbo's) q95 file of the same array, byte for byte
+    import io
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(np.ascontiguousarray(pano[..., ::-1])).save(b, "JPEG", quality=95)
+    assert written == b.getvalue()
+    pano_h, _ = ish.run_panorama(str(tmp_path), margin=30, decode="host", encode="host", out_name="h.jpg")
+    assert np.array_equal(pano_h, pano) and (tmp_path / "h.jpg").read_bytes() == written
 
 
 # ------------------------------------------------------------------ published-result PSNR

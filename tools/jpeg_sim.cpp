@@ -83,17 +83,22 @@ int main(int argc, char **argv) {
     std::vector<SubStats> cstats((size_t)nsub * NS);
     auto end_of = [&](uint32_t t) { uint32_t e = (t + 1) * (uint32_t)L; return e < nbits ? e : nbits; };
     long decoded = 0;
-    for (uint32_t t = 0; t < nsub; ++t)
+    const uint32_t G = getenv("JPEG_SIM_CHAIN") ? (uint32_t)atoi(getenv("JPEG_SIM_CHAIN")) : 4;
+    for (uint32_t ta = 0; ta < nsub; ta += G)          // chains of G subsequences
         for (int j = 0; j < NP; ++j) {
-            const uint32_t p0 = t * (uint32_t)L;
-            const size_t q = (size_t)t * NS + j;
+            const uint32_t p0 = ta * (uint32_t)L;
             SinkNone sn;
-            cand[q] = p0 <= W ? walk(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, sn)
-                              : walk(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, sn);
-            SinkCount sc;
-            ex[q] = walk(words, 0, nw, cand[q], end_of(t), T, F.mcu_comp, F.bpm, sc);
-            cstats[q] = sc.stats();
-            ++decoded;
+            uint64_t stt = p0 <= W ? walk(words, 0, nw, pack_state(0, 0, 0), p0, T, F.mcu_comp, F.bpm, sn)
+                                   : walk(words, 0, nw, pack_state(p0 - W, j, 0), p0, T, F.mcu_comp, F.bpm, sn);
+            for (uint32_t t = ta; t < ta + G && t < nsub; ++t) {
+                const size_t q = (size_t)t * NS + j;
+                SinkCount sc;
+                cand[q] = stt;
+                ex[q] = walk(words, 0, nw, stt, end_of(t), T, F.mcu_comp, F.bpm, sc);
+                cstats[q] = sc.stats();
+                stt = ex[q];
+                ++decoded;
+            }
         }
     // jpeg_sync_fix: where a warm exit of t-1 matches no warm candidate of t, decode t from that
     // exit as an extra candidate (slot bpm + i)

@@ -7,10 +7,11 @@
 //        entropy-coded segments (a chunked stream compaction);
 //   jpeg_sync_warm   the Huffman stream has no restart markers, so it is cut into subsequences
 //        of kSubBits bits and the decoder state at each subsequence start is found by
-//        self-synchronisation: one thread per (subsequence, MCU-phase hypothesis) decodes a
-//        warm-up window before its subsequence from a guessed state, which converges on the
-//        true codeword boundaries; then it decodes its subsequence with counting (exit state,
-//        blocks started, DC difference sums);
+//        self-synchronisation: one thread per (chain of kChain subsequences, MCU-phase
+//        hypothesis) decodes a warm-up window before its chain from a guessed state, which
+//        converges on the true codeword boundaries, then walks its subsequences with counting,
+//        recording at each one's start a candidate state and its exit state, blocks started
+//        and DC difference sums;
 //   jpeg_sync_fix    where an exit of subsequence t-1 matches none of t's candidates, t is
 //        decoded from that exit as an extra candidate (all such (t, exit) pairs in parallel);
 //   jpeg_sync_resolve  one workgroup per frame chains the candidates: the true start of
@@ -194,11 +195,17 @@ __global__ void __launch_bounds__(256) jpeg_unstuff_write(Dev D) {
 }
 
 // ------------------------------------------------------------------------------------ sync
-// Launch shapes: warm and fix run 256 threads = kSpb subsequences x np phase slots (the tail
-// threads idle); window = the bits those walks can reach.
+// Launch shapes: warm runs kSyncThreads threads = chains x np phase slots (the tail threads
+// idle), at most kChainsPerBlock chains; fix runs kSyncThreads = subsequences x np slots.  The
+// window is every bit those walks can reach.
 constexpr int kWarmMax = 16384;                     // cap of Frame::warm (bits)
 constexpr int kSyncThreads = 256;
-constexpr int kWinWords = (kWarmMax + kSyncThreads * kSubBits) / 32 + 2 * kMargin;
+constexpr int kChain = 4;                           // subsequences per warm chain
+constexpr int kChainsPerBlock = 42;
+constexpr int kWinWords = (kWarmMax + kChainsPerBlock * kChain * kSubBits) / 32 + 2 * kMargin;
+__host__ __device__ __forceinline__ int chains_per_block(int np) {
+    return kSyncThreads / np < kChainsPerBlock ? kSyncThreads / np : kChainsPerBlock;
+}
 
 __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_warm(Dev D) {
     __shared__ LdsTabs L;
@@ -207,34 +214,38 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_warm(Dev D) {
     const Frame &F = D.frames[f];
     const uint32_t nb = D.nbits[f];
     const uint32_t nsub = frame_nsub(F, nb);
-    const int np = D.np, spb = kSyncThreads / np;
-    const uint32_t t0 = blockIdx.x * spb;
+    const int np = D.np, cpb = chains_per_block(np);
+    const uint32_t t0 = blockIdx.x * cpb * kChain;   // first subsequence of the block
     if (t0 >= nsub) return;                          // whole block past the frame's stream
     const uint32_t W = F.warm;
     const uint32_t b0 = t0 * kSubBits > W ? t0 * kSubBits - W : 0;      // first bit any walk reads
     const uint32_t w0 = b0 >> 5;
-    const uint32_t b1 = (t0 + spb) * kSubBits;
+    const uint32_t b1 = (t0 + cpb * kChain) * kSubBits;
     const uint32_t nwin = (b1 >> 5) - w0 + kMargin;
     stage_tabs(D, F, L);
     stage_window(D, F, nb, w0, nwin, win);
     __syncthreads();
-    const uint32_t t = t0 + threadIdx.x / np, j = threadIdx.x % np;
-    if ((int)(threadIdx.x / np) >= spb || t >= nsub) return;
-    if ((int)j >= F.bpm) {                           // phase slot this frame's MCU lacks
-        D.cand[(size_t)(F.sub0 + t) * D.nps + j] = kNoCand;
+    const int ch = threadIdx.x / np, j = threadIdx.x % np;
+    const uint32_t ta = t0 + ch * kChain;            // the chain's first subsequence
+    if (ch >= cpb || ta >= nsub) return;
+    if (j >= F.bpm) {                                // phase slot this frame's MCU lacks
+        for (uint32_t t = ta; t < ta + kChain && t < nsub; ++t) D.cand[(size_t)(F.sub0 + t) * D.nps + j] = kNoCand;
         return;
     }
-    const uint32_t p0 = t * kSubBits;
+    const uint32_t p0 = ta * kSubBits;
     SinkNone sn;
-    const uint64_t s0 = p0 <= W ? walk(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, sn)
-                                : walk(win, w0, nwin, pack_state(p0 - W, (int)j, 0), p0, L.T, L.mcu_comp, F.bpm, sn);
-    const uint32_t end = p0 + kSubBits < nb ? p0 + kSubBits : nb;
-    SinkCount sc;
-    const uint64_t x = walk(win, w0, nwin, s0, end, L.T, L.mcu_comp, F.bpm, sc);
-    const size_t q = (size_t)(F.sub0 + t) * D.nps + j;
-    D.cand[q] = s0;
-    D.cexit[q] = x;
-    D.cstats[q] = sc.stats();
+    uint64_t st = p0 <= W ? walk(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, sn)
+                          : walk(win, w0, nwin, pack_state(p0 - W, j, 0), p0, L.T, L.mcu_comp, F.bpm, sn);
+    for (uint32_t t = ta; t < ta + kChain && t < nsub; ++t) {
+        const uint32_t end = (t + 1) * kSubBits < nb ? (t + 1) * kSubBits : nb;
+        SinkCount sc;
+        const uint64_t x = walk(win, w0, nwin, st, end, L.T, L.mcu_comp, F.bpm, sc);
+        const size_t q = (size_t)(F.sub0 + t) * D.nps + j;
+        D.cand[q] = st;
+        D.cexit[q] = x;
+        D.cstats[q] = sc.stats();
+        st = x;
+    }
 }
 
 // Extra candidates: for subsequence t >= 1 and warm slot i of t-1 whose exit starts none of
@@ -250,7 +261,7 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix(Dev D) {
     const int np = D.np, nps = D.nps, spb = kSyncThreads / np;
     const uint32_t t0 = blockIdx.x * spb;
     if (t0 >= nsub) return;
-    const uint32_t t = t0 + threadIdx.x / np, i = threadIdx.x % np;
+    const uint32_t t = t0 + threadIdx.x / np, i = threadIdx.x % np;   // subsequence, predecessor slot
     bool need = false;
     uint64_t e = kNoCand;
     const bool slot = (int)(threadIdx.x / np) < spb && t < nsub;
@@ -313,6 +324,7 @@ __device__ __forceinline__ uint64_t find_slot(const uint64_t *ct, int nps, uint6
 }
 
 constexpr int kResolveThreads = 512;
+constexpr int kFixRun = 16;      // subsequences one serial fallback may decode in a row
 
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uint32_t *total) {
     // kResolveThreads-thread exclusive scan (waves of 64)
@@ -340,8 +352,9 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
     __shared__ LdsTabs L;
     __shared__ uint64_t maps[kResolveThreads];
     __shared__ uint32_t wsum[kResolveThreads / 64];
-    __shared__ uint32_t win[kSubBits / 32 + 2 * kMargin];
+    __shared__ uint32_t win[kFixRun * kSubBits / 32 + 2 * kMargin];
     __shared__ int s_fail;
+    __shared__ uint32_t s_next;
     __shared__ uint64_t s_exit;
     __shared__ SubStats s_acc;
     constexpr int NT = kResolveThreads;
@@ -419,25 +432,35 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
         base += nres;
         __syncthreads();
         if (nres < NT && base < nsub) {
-            // every candidate of `base` missed: decode it from the true start (one thread)
-            if (threadIdx.x == 0) D.stats[4 * f + 2] += 1;
-            const uint32_t w0 = (base * kSubBits) >> 5, nwin = kSubBits / 32 + kMargin;
+            // every candidate of `base` missed: decode it from the true start (one thread), and
+            // its successors while their candidates miss too (a run of such subsequences is
+            // typical: the warm chains of one region failed together)
+            const uint32_t w0 = (base * kSubBits) >> 5, nwin = (kFixRun * kSubBits) / 32 + kMargin;
             stage_window(D, F, nb, w0, nwin, win);
             __syncthreads();
             if (threadIdx.x == 0) {
-                const uint64_t e = s_exit;
-                const uint32_t end = (base + 1) * kSubBits < nb ? (base + 1) * kSubBits : nb;
-                SinkCount sc;
-                const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
-                D.start[S0 + base] = e;
-                D.scan[S0 + base] = s_acc;
-                s_acc.blocks += sc.blocks;
-                s_acc.dc[0] += sc.d0;
-                s_acc.dc[1] += sc.d1;
-                s_acc.dc[2] += sc.d2;
-                s_exit = x;
+                uint64_t e = s_exit;
+                uint32_t t = base;
+                for (int r = 0; r < kFixRun && t < nsub; ++r) {
+                    const uint32_t end = (t + 1) * kSubBits < nb ? (t + 1) * kSubBits : nb;
+                    SinkCount sc;
+                    const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
+                    D.start[S0 + t] = e;
+                    D.scan[S0 + t] = s_acc;
+                    s_acc.blocks += sc.blocks;
+                    s_acc.dc[0] += sc.d0;
+                    s_acc.dc[1] += sc.d1;
+                    s_acc.dc[2] += sc.d2;
+                    D.stats[4 * f + 2] += 1;
+                    e = x;
+                    ++t;
+                    if (t >= nsub || find_slot(D.cand + (S0 + t) * nps, nps, x) != kNone) break;
+                }
+                s_exit = e;
+                s_next = t;
             }
-            base += 1;
+            __syncthreads();
+            base = s_next;
             __syncthreads();
         }
     }
@@ -722,10 +745,10 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     jpeg_unstuff_count<<<chunks, 256, 0, ctx->stream>>>(D);
     jpeg_unstuff_write<<<chunks, 256, 0, ctx->stream>>>(D);
     {
+        const uint32_t per = (uint32_t)(chains_per_block(np) * kChain);
+        jpeg_sync_warm<<<dim3((nsub_max + per - 1) / per, n), kSyncThreads, 0, ctx->stream>>>(D);
         const uint32_t spb = kSyncThreads / np;
-        const unsigned gx = (unsigned)((nsub_max + spb - 1) / spb);
-        jpeg_sync_warm<<<dim3(gx, n), kSyncThreads, 0, ctx->stream>>>(D);
-        jpeg_sync_fix<<<dim3(gx, n), kSyncThreads, 0, ctx->stream>>>(D);
+        jpeg_sync_fix<<<dim3((nsub_max + spb - 1) / spb, n), kSyncThreads, 0, ctx->stream>>>(D);
     }
     jpeg_sync_resolve<<<n, kResolveThreads, 0, ctx->stream>>>(D);
     jpeg_write<<<dim3((nsub_max + kWriteThreads - 1) / kWriteThreads, n), kWriteThreads, 0, ctx->stream>>>(D);

@@ -149,10 +149,37 @@ def imwrite_jpeg(path, img_bgr, quality=95):
     Image.fromarray(np.ascontiguousarray(img_bgr[..., ::-1])).save(path, quality=quality)
 
 
+def _read_frames(paths, decode, st):
+    """The cv2.imread loop (run_panorama :280-287): "gpu" decodes the set's JPEG files in one
+    pano_jpeg_decode batch straight into device memory; "host" is PIL; "auto" takes the GPU
+    when every file is a baseline JPEG of one size (the reference's sets are) and PIL
+    otherwise (progressive files, other formats, mixed sizes)."""
+    from . import jpeg
+    if any(not os.path.exists(p) for p in paths):
+        raise FileNotFoundError("a frame listed in pano.txt is missing")
+    if decode != "host":
+        bufs = [open(p, "rb").read() for p in paths]
+        try:
+            shapes = {jpeg.info(b)[:2] for b in bufs}
+        except Exception:
+            if decode == "gpu":
+                raise
+            shapes = None
+        if shapes is not None and len(shapes) == 1:
+            return jpeg.decode_batch(bufs, device=st.device.index)
+        if decode == "gpu":
+            raise ValueError("GPU decode needs JPEG frames of one size")
+    return st.upload([imread_bgr(p) for p in paths])
+
+
 def run_panorama(folder_path=".", pano_file=None, margin=15, method="sift", out_name=None,
-                 write=True):
-    """Non-interactive run_panorama: the three input() prompts become arguments."""
+                 write=True, decode="auto", encode="gpu"):
+    """Non-interactive run_panorama: the three input() prompts become arguments.  The frames
+    are read with the GPU JPEG decoder (decode, see _read_frames) and the panorama is written
+    with the GPU JPEG encoder at cv2.imwrite's default quality 95 (encode="gpu"; "host" = PIL;
+    both give the same bytes)."""
     import time
+    from . import jpeg
     from .pipeline import Stitcher
     if not (folder_path.endswith("/") or folder_path.endswith("\\")):
         folder_path += "/"
@@ -161,14 +188,15 @@ def run_panorama(folder_path=".", pano_file=None, margin=15, method="sift", out_
     if not img_paths:
         raise ValueError("no valid entries in pano.txt")
     t0 = time.time()
-    frames = [imread_bgr(p) for p in resolve_paths(folder_path, img_paths)]
-    if any(f is None for f in frames):
-        raise FileNotFoundError("a frame listed in pano.txt is missing")
     st = Stitcher(method)
-    res = st.run(st.upload(frames), np.array(focals, np.float64), margin=margin)
+    frames_dev = _read_frames(resolve_paths(folder_path, img_paths), decode, st)
+    res = st.run(frames_dev, np.array(focals, np.float64), margin=margin)
     pano = res.panorama.cpu().numpy()
     if write:
         name = out_name or ("panoroma_sift.jpg" if method == "sift" else "panoroma_harris.jpg")
-        imwrite_jpeg(os.path.join(folder_path, name), pano)
+        if encode == "gpu":
+            jpeg.imwrite(os.path.join(folder_path, name), res.panorama)
+        else:
+            imwrite_jpeg(os.path.join(folder_path, name), pano)
     res.timings["wall_with_io"] = time.time() - t0
     return pano, res
