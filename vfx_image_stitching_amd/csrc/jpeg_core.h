@@ -458,44 +458,43 @@ __host__ __device__ __forceinline__ EncGeom enc_geom(int h, int w, int64_t pitch
     return G;
 }
 
-// Level-shifted samples of one block (MCU order index blk) in natural order: the
+// Level-shifted samples of row r of one block (MCU order index blk), 8 values: the
 // pre-processing chain of jcprepct.c / jcsample.c -- colour conversion, right-edge and
 // bottom-edge replication, h2v2 downsampling with the 1,2,1,2 bias -- for a real block.
-__host__ __device__ __forceinline__ void enc_samples(const uint8_t *img, const EncGeom &G, int blk, int32_t *s) {
+__host__ __device__ __forceinline__ void enc_sample_row(const uint8_t *img, const EncGeom &G, int blk, int r,
+                                                        int32_t *s8) {
     const int m = blk / 6, b = blk - 6 * (blk / 6);
     const int mx = m % G.mcus_x, my = m / G.mcus_x;
     if (b < 4) {
         const int bx = 2 * mx + (b & 1), by = 2 * my + (b >> 1);
-        for (int r = 0; r < 8; ++r) {
-            const int y = imin(by * 8 + r, G.h - 1);
-            const uint8_t *row = img + (int64_t)y * G.pitch;
-            for (int c = 0; c < 8; ++c) {
-                const uint8_t *p = row + 3 * imin(bx * 8 + c, G.w - 1);
-                int Y, cb, cr;
-                rgb_to_ycc(p[2], p[1], p[0], Y, cb, cr);
-                s[r * 8 + c] = Y - 128;
-            }
+        const uint8_t *row = img + (int64_t)imin(by * 8 + r, G.h - 1) * G.pitch;
+        for (int c = 0; c < 8; ++c) {
+            const uint8_t *p = row + 3 * imin(bx * 8 + c, G.w - 1);
+            int Y, cb, cr;
+            rgb_to_ycc(p[2], p[1], p[0], Y, cb, cr);
+            s8[c] = Y - 128;
         }
         return;
     }
     const int hc = (G.h + 1) / 2;          // chroma rows holding data
-    for (int r = 0; r < 8; ++r) {
-        const int cy = imin(my * 8 + r, hc - 1);
-        const uint8_t *r0 = img + (int64_t)(2 * cy) * G.pitch;
-        const uint8_t *r1 = img + (int64_t)imin(2 * cy + 1, G.h - 1) * G.pitch;
-        for (int c = 0; c < 8; ++c) {
-            const int cx = mx * 8 + c;
-            const int x0 = 3 * imin(2 * cx, G.w - 1), x1 = 3 * imin(2 * cx + 1, G.w - 1);
-            int Y, cb[4], cr[4];
-            rgb_to_ycc(r0[x0 + 2], r0[x0 + 1], r0[x0], Y, cb[0], cr[0]);
-            rgb_to_ycc(r0[x1 + 2], r0[x1 + 1], r0[x1], Y, cb[1], cr[1]);
-            rgb_to_ycc(r1[x0 + 2], r1[x0 + 1], r1[x0], Y, cb[2], cr[2]);
-            rgb_to_ycc(r1[x1 + 2], r1[x1 + 1], r1[x1], Y, cb[3], cr[3]);
-            const int bias = (cx & 1) ? 2 : 1;
-            const int v = b == 4 ? (cb[0] + cb[1] + cb[2] + cb[3] + bias) >> 2 : (cr[0] + cr[1] + cr[2] + cr[3] + bias) >> 2;
-            s[r * 8 + c] = v - 128;
-        }
+    const int cy = imin(my * 8 + r, hc - 1);
+    const uint8_t *r0 = img + (int64_t)(2 * cy) * G.pitch;
+    const uint8_t *r1 = img + (int64_t)imin(2 * cy + 1, G.h - 1) * G.pitch;
+    for (int c = 0; c < 8; ++c) {
+        const int cx = mx * 8 + c;
+        const int x0 = 3 * imin(2 * cx, G.w - 1), x1 = 3 * imin(2 * cx + 1, G.w - 1);
+        int Y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
+        rgb_to_ycc(r0[x0 + 2], r0[x0 + 1], r0[x0], Y, cb0, cr0);
+        rgb_to_ycc(r0[x1 + 2], r0[x1 + 1], r0[x1], Y, cb1, cr1);
+        rgb_to_ycc(r1[x0 + 2], r1[x0 + 1], r1[x0], Y, cb2, cr2);
+        rgb_to_ycc(r1[x1 + 2], r1[x1 + 1], r1[x1], Y, cb3, cr3);
+        const int bias = (cx & 1) ? 2 : 1;
+        const int v = b == 4 ? (cb0 + cb1 + cb2 + cb3 + bias) >> 2 : (cr0 + cr1 + cr2 + cr3 + bias) >> 2;
+        s8[c] = v - 128;
     }
+}
+__host__ __device__ __forceinline__ void enc_samples(const uint8_t *img, const EncGeom &G, int blk, int32_t *s) {
+    for (int r = 0; r < 8; ++r) enc_sample_row(img, G, blk, r, s + 8 * r);
 }
 
 // Forward DCT (rows, then columns) and quantisation of 64 level-shifted samples -> coef

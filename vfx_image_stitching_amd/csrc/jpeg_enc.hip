@@ -4,7 +4,7 @@
 // forward DCT, reciprocal quantisation, Annex K Huffman tables, JFIF header.
 //
 // Five launches:
-//   jpeg_enc_blocks   one thread per 8x8 block (MCU order): colour conversion, edge
+//   jpeg_enc_blocks   8 threads per 8x8 block (MCU order; row, then column): colour conversion, edge
 //                     replication and h2v2 downsampling of its samples, forward DCT,
 //                     quantisation (jpeg_core.h enc_samples / enc_transform); the luma blocks
 //                     outside the image's block grid take the DC of the block libjpeg copies;
@@ -84,27 +84,36 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *wsum) {
     return t;
 }
 
+// 32 blocks per workgroup, 8 threads per block: thread r samples and transforms row r, then
+// (after an LDS transpose) transforms and quantises column r.
 __global__ void __launch_bounds__(kEncThreads) jpeg_enc_blocks(EncDev D) {
-    const int b = blockIdx.x * kEncThreads + threadIdx.x;
-    if (b >= D.nblk) return;
-    const QRecip *q = D.tabs->q[(b % 6) < 4 ? 0 : 1];
-    int32_t s[64];
-    int16_t *dst = D.coef + (size_t)b * 64;
-    int src = enc_dummy_source(D.G, b);
-    if (src < 0) {
-        enc_samples(D.img, D.G, b, s);
-        int16_t c[64];
-        enc_transform(s, q, c);
-        for (int i = 0; i < 64; i += 8) *(uint4 *)(dst + i) = *(const uint4 *)(c + i);
-        return;
+    __shared__ int32_t ws[kEncThreads / 8][8][9];
+    __shared__ QRecip q[2][64];
+    for (int i = threadIdx.x; i < 128; i += kEncThreads) q[i >> 6][i & 63] = D.tabs->q[i >> 6][i & 63];
+    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
+    const int b = blockIdx.x * (kEncThreads / 8) + lb;
+    const bool live = b < D.nblk;
+    int src = live ? enc_dummy_source(D.G, b) : -1;
+    const bool dummy = src >= 0;
+    if (dummy && enc_dummy_source(D.G, src) >= 0) src = enc_dummy_source(D.G, src);
+    const int sb = dummy ? src : b;
+    int32_t row[8];
+    if (live) {
+        enc_sample_row(D.img, D.G, sb, r, row);
+        fdct8(row, 1);
+        for (int c = 0; c < 8; ++c) ws[lb][r][c] = row[c];
     }
-    // dummy luma block: zero AC, the DC of the real block libjpeg copies
-    for (int g = 0; g < 2 && enc_dummy_source(D.G, src) >= 0; ++g) src = enc_dummy_source(D.G, src);
-    enc_samples(D.img, D.G, src, s);
-    int16_t c[64];
-    enc_transform(s, q, c);
-    for (int i = 0; i < 64; i += 8) *(uint4 *)(dst + i) = make_uint4(0, 0, 0, 0);
-    dst[0] = c[0];
+    __syncthreads();
+    if (!live) return;
+    int32_t col[8];
+    for (int i = 0; i < 8; ++i) col[i] = ws[lb][i][r];
+    fdct8(col, 2);
+    const QRecip *qq = q[(b % 6) < 4 ? 0 : 1];
+    int16_t *dst = D.coef + (size_t)b * 64;
+    for (int i = 0; i < 8; ++i) {
+        const int v = quantize(col[i], qq[i * 8 + r]);
+        dst[i * 8 + r] = (int16_t)(dummy && (i | r) ? 0 : v);   // a dummy block keeps the DC only
+    }
 }
 
 struct CountPut {
@@ -328,7 +337,7 @@ int launch_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t 
         PanoProf prof_(ctx, PK_JPEG);
         rc = launch_fill(ctx, D.words, 0, 4 * ((max_bits + 31) / 32 + 2));
         if (rc) return rc;
-        jpeg_enc_blocks<<<(nblk + kEncThreads - 1) / kEncThreads, kEncThreads, 0, ctx->stream>>>(D);
+        jpeg_enc_blocks<<<(nblk + kEncThreads / 8 - 1) / (kEncThreads / 8), kEncThreads, 0, ctx->stream>>>(D);
         jpeg_enc_lengths<<<nchunk, kEncThreads, 0, ctx->stream>>>(D);
         jpeg_enc_emit<<<nchunk, kEncThreads, 0, ctx->stream>>>(D);
         jpeg_enc_ff_count<<<nbchunk, kEncThreads, 0, ctx->stream>>>(D);
