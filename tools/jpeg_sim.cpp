@@ -77,7 +77,7 @@ int main(int argc, char **argv) {
     // decode from a wrong bit position re-synchronises with the true decode only when it also
     // lands in the right block of the MCU; trying every phase makes one of them land early.
     const uint32_t W = getenv("JPEG_SIM_W") ? (uint32_t)atoi(getenv("JPEG_SIM_W")) : F.warm;
-    const int NP = F.bpm, NS = 2 * F.bpm;          // warm slots, + fix slots
+    const int NP = F.bpm, NS = 2 * F.bpm + 1;      // warm slots, fix slots, fix2 slot
     const uint64_t kNoCand = ~0ull;
     std::vector<uint64_t> cand((size_t)nsub * NS, kNoCand), ex((size_t)nsub * NS, kNoCand);
     std::vector<SubStats> cstats((size_t)nsub * NS);
@@ -115,6 +115,23 @@ int main(int argc, char **argv) {
             ex[q] = walk(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, sc);
             cstats[q] = sc.stats();
             ++fix_slots;
+        }
+    // jpeg_sync_fix2: the same from the fix slots' exits, into slot 2 np (first such one)
+    for (uint32_t t = nsub - 1; t >= 1; --t)          // reads t-1's fix slots only: any order
+        for (int i = 0; i < NP; ++i) {
+            const size_t qp = (size_t)(t - 1) * NS + NP + i;
+            if (cand[qp] == kNoCand) continue;
+            const uint64_t e = ex[qp];
+            bool hit = false;
+            for (int j = 0; j < 2 * NP; ++j) hit |= cand[(size_t)t * NS + j] == e;
+            if (hit) continue;
+            const size_t q = (size_t)t * NS + 2 * NP;
+            SinkCount sc;
+            cand[q] = e;
+            ex[q] = walk(words, 0, nw, e, end_of(t), T, F.mcu_comp, F.bpm, sc);
+            cstats[q] = sc.stats();
+            ++fix_slots;
+            break;
         }
     // jpeg_sync_resolve: J_t = the first candidate of t equal to the true exit of t-1 (t = 0
     // exact); none -> decode t from that exit (serial fallback)

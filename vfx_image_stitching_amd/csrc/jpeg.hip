@@ -14,6 +14,8 @@
 //        and DC difference sums;
 //   jpeg_sync_fix    where an exit of subsequence t-1 matches none of t's candidates, t is
 //        decoded from that exit as an extra candidate (all such (t, exit) pairs in parallel);
+//   jpeg_sync_fix2   the same once more from the extra candidates' exits (one more slot per
+//        subsequence): a region where every warm chain failed is bridged in two rounds;
 //   jpeg_sync_resolve  one workgroup per frame chains the candidates: the true start of
 //        subsequence t is the exit of t-1's chosen candidate, found by a composition scan of
 //        the per-subsequence candidate maps; a subsequence whose candidates all missed is
@@ -27,6 +29,7 @@
 // from LDS (two-level lookup, jpeg_core.h).  The host parses headers only (jpeg_host.cpp) and
 // uploads tables + entropy bytes once.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "jpeg_core.h"
@@ -50,12 +53,13 @@ struct Dev {
     int32_t *flags;
     int32_t *stats;             // [n][4]: subsequences, fix candidates, serial decodes, 0
     int32_t *status;            // caller's, may be null
-    uint64_t *cand;             // [S][nps]: warm slots [0, np), fix slots [np, 2 np)
+    uint64_t *cand;             // [S][nps]: warm slots [0, np), fix slots [np, 2 np), fix2 slot 2 np
     uint64_t *cexit;            // [S][nps]
     SubStats *cstats;           // [S][nps]
     uint64_t *start;            // [S]
     SubStats *scan;             // [S] exclusive prefix
-    int n, np, nps;             // candidate slots: np phases (max bpm), nps = 2 np
+    int n, np, nps;             // candidate slots: np phases (max bpm), nps = 2 np + 1
+    int chain;                  // subsequences per warm chain (<= kChain)
 };
 
 constexpr uint64_t kNoCand = ~0ull;
@@ -215,28 +219,29 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_warm(Dev D) {
     const uint32_t nb = D.nbits[f];
     const uint32_t nsub = frame_nsub(F, nb);
     const int np = D.np, cpb = chains_per_block(np);
-    const uint32_t t0 = blockIdx.x * cpb * kChain;   // first subsequence of the block
+    const int G = D.chain;
+    const uint32_t t0 = blockIdx.x * cpb * G;        // first subsequence of the block
     if (t0 >= nsub) return;                          // whole block past the frame's stream
     const uint32_t W = F.warm;
     const uint32_t b0 = t0 * kSubBits > W ? t0 * kSubBits - W : 0;      // first bit any walk reads
     const uint32_t w0 = b0 >> 5;
-    const uint32_t b1 = (t0 + cpb * kChain) * kSubBits;
+    const uint32_t b1 = (t0 + cpb * G) * kSubBits;
     const uint32_t nwin = (b1 >> 5) - w0 + kMargin;
     stage_tabs(D, F, L);
     stage_window(D, F, nb, w0, nwin, win);
     __syncthreads();
     const int ch = threadIdx.x / np, j = threadIdx.x % np;
-    const uint32_t ta = t0 + ch * kChain;            // the chain's first subsequence
+    const uint32_t ta = t0 + ch * G;                 // the chain's first subsequence
     if (ch >= cpb || ta >= nsub) return;
     if (j >= F.bpm) {                                // phase slot this frame's MCU lacks
-        for (uint32_t t = ta; t < ta + kChain && t < nsub; ++t) D.cand[(size_t)(F.sub0 + t) * D.nps + j] = kNoCand;
+        for (uint32_t t = ta; t < ta + G && t < nsub; ++t) D.cand[(size_t)(F.sub0 + t) * D.nps + j] = kNoCand;
         return;
     }
     const uint32_t p0 = ta * kSubBits;
     SinkNone sn;
     uint64_t st = p0 <= W ? walk(win, w0, nwin, pack_state(0, 0, 0), p0, L.T, L.mcu_comp, F.bpm, sn)
                           : walk(win, w0, nwin, pack_state(p0 - W, j, 0), p0, L.T, L.mcu_comp, F.bpm, sn);
-    for (uint32_t t = ta; t < ta + kChain && t < nsub; ++t) {
+    for (uint32_t t = ta; t < ta + G && t < nsub; ++t) {
         const uint32_t end = (t + 1) * kSubBits < nb ? (t + 1) * kSubBits : nb;
         SinkCount sc;
         const uint64_t x = walk(win, w0, nwin, st, end, L.T, L.mcu_comp, F.bpm, sc);
@@ -297,8 +302,63 @@ __global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix(Dev D) {
     D.cstats[q] = sc.stats();
 }
 
+// Second round: for subsequence t >= 1 and fix slot np + i of t-1 whose exit starts none of
+// t's candidates, t decoded from that exit into slot 2 np (the first such i; the others fall to
+// the serial fallback of the resolve).
+__global__ void __launch_bounds__(kSyncThreads) jpeg_sync_fix2(Dev D) {
+    __shared__ LdsTabs L;
+    __shared__ uint32_t win[(kSyncThreads * kSubBits) / 32 + 2 * kMargin];
+    __shared__ int pick[kSyncThreads];
+    __shared__ int any;
+    const int f = blockIdx.y;
+    const Frame &F = D.frames[f];
+    const uint32_t nb = D.nbits[f];
+    const uint32_t nsub = frame_nsub(F, nb);
+    const int np = D.np, nps = D.nps, spb = kSyncThreads / np;
+    const uint32_t t0 = blockIdx.x * spb;
+    if (t0 >= nsub) return;
+    const int tl = threadIdx.x / np, i = threadIdx.x % np;
+    const uint32_t t = t0 + tl;
+    const bool slot = tl < spb && t < nsub;
+    const bool mine = slot && i < F.bpm;
+    if (threadIdx.x == 0) any = 0;
+    pick[threadIdx.x] = np;
+    __syncthreads();
+    uint64_t e = kNoCand;
+    bool need = false;
+    if (mine && t >= 1) {
+        const size_t qp = (size_t)(F.sub0 + t - 1) * nps + np + i, qt = (size_t)(F.sub0 + t) * nps;
+        if (D.cand[qp] != kNoCand) {
+            e = D.cexit[qp];
+            need = true;
+            for (int j = 0; j < 2 * np; ++j) need &= D.cand[qt + j] != e;
+            if (need) atomicMin(&pick[tl], i);
+        }
+    }
+    __syncthreads();
+    if (slot && i == 0) D.cand[(size_t)(F.sub0 + t) * nps + 2 * np] = kNoCand;
+    need = need && pick[tl] == i;
+    if (need) any = 1;
+    __syncthreads();
+    if (!any) return;
+    const uint32_t w0 = (t0 * kSubBits) >> 5;
+    const uint32_t nwin = (uint32_t)(spb * kSubBits) / 32 + kMargin;
+    stage_tabs(D, F, L);
+    stage_window(D, F, nb, w0, nwin, win);
+    __syncthreads();
+    if (!need) return;
+    atomicAdd(&D.stats[4 * f + 1], 1);
+    const uint32_t end = (t + 1) * kSubBits < nb ? (t + 1) * kSubBits : nb;
+    SinkCount sc;
+    const uint64_t x = walk(win, w0, nwin, e, end, L.T, L.mcu_comp, F.bpm, sc);
+    const size_t q = (size_t)(F.sub0 + t) * nps + 2 * np;
+    D.cand[q] = e;
+    D.cexit[q] = x;
+    D.cstats[q] = sc.stats();
+}
+
 // Candidate map of subsequence t: for each slot i of t-1, the first slot of t whose start
-// equals i's exit (15 = none), 4 bits per entry (nps <= 12).
+// equals i's exit (15 = none), 4 bits per entry (nps <= 13).
 constexpr uint64_t kNone = 15;
 __device__ __forceinline__ uint64_t map_get(uint64_t m, int i) { return (m >> (4 * i)) & 15; }
 // (second after first): entry i -> second[first[i]]
@@ -667,7 +727,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     const size_t o_chunks = up;  up = align_up(up + 4 * chunk_frame.size(), 256);
     const size_t o_src = up;     up = align_up(up + src_total, 256);
     const size_t up_bytes = up;
-    const int nps = 2 * np;
+    const int nps = 2 * np + 1;
     size_t dv = align_up(up_bytes, 256);
     const size_t o_stream = dv;  dv = align_up(dv + stream_total, 256);
     const size_t o_coef = dv;    dv = align_up(dv + 2 * coef_total, 256);
@@ -736,6 +796,12 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     D.n = n;
     D.np = np;
     D.nps = nps;
+    {
+        // subsequences per warm chain (PANO_JPEG_CHAIN, 1..kChain; speed only)
+        const char *env = getenv("PANO_JPEG_CHAIN");
+        const int g = env ? atoi(env) : 2;
+        D.chain = g < 1 ? 1 : (g > kChain ? kChain : g);
+    }
 
     PanoProf prof_(ctx, PK_JPEG);
     rc = launch_fill(ctx, dev + o_coef, 0, 2 * coef_total);
@@ -745,10 +811,11 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     jpeg_unstuff_count<<<chunks, 256, 0, ctx->stream>>>(D);
     jpeg_unstuff_write<<<chunks, 256, 0, ctx->stream>>>(D);
     {
-        const uint32_t per = (uint32_t)(chains_per_block(np) * kChain);
+        const uint32_t per = (uint32_t)(chains_per_block(np) * D.chain);
         jpeg_sync_warm<<<dim3((nsub_max + per - 1) / per, n), kSyncThreads, 0, ctx->stream>>>(D);
         const uint32_t spb = kSyncThreads / np;
         jpeg_sync_fix<<<dim3((nsub_max + spb - 1) / spb, n), kSyncThreads, 0, ctx->stream>>>(D);
+        jpeg_sync_fix2<<<dim3((nsub_max + spb - 1) / spb, n), kSyncThreads, 0, ctx->stream>>>(D);
     }
     jpeg_sync_resolve<<<n, kResolveThreads, 0, ctx->stream>>>(D);
     jpeg_write<<<dim3((nsub_max + kWriteThreads - 1) / kWriteThreads, n), kWriteThreads, 0, ctx->stream>>>(D);
