@@ -83,7 +83,7 @@ int main(int argc, char **argv) {
     std::vector<SubStats> cstats((size_t)nsub * NS);
     auto end_of = [&](uint32_t t) { uint32_t e = (t + 1) * (uint32_t)L; return e < nbits ? e : nbits; };
     long decoded = 0;
-    const uint32_t G = getenv("JPEG_SIM_CHAIN") ? (uint32_t)atoi(getenv("JPEG_SIM_CHAIN")) : 4;
+    const uint32_t G = getenv("JPEG_SIM_CHAIN") ? (uint32_t)atoi(getenv("JPEG_SIM_CHAIN")) : 1;
     for (uint32_t ta = 0; ta < nsub; ta += G)          // chains of G subsequences
         for (int j = 0; j < NP; ++j) {
             const uint32_t p0 = ta * (uint32_t)L;

@@ -799,7 +799,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     {
         // subsequences per warm chain (PANO_JPEG_CHAIN, 1..kChain; speed only)
         const char *env = getenv("PANO_JPEG_CHAIN");
-        const int g = env ? atoi(env) : 2;
+        const int g = env ? atoi(env) : 1;
         D.chain = g < 1 ? 1 : (g > kChain ? kChain : g);
     }
 

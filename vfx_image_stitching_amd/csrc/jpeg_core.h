@@ -173,7 +173,10 @@ __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_
                                                   const int8_t *mcu_comp, int bpm, Sink &sink) {
     uint32_t pos = state_pos(start);
     int b = state_b(start), k = state_k(start);
-    int c = mcu_comp[b];
+    // the MCU layout as 2 bits per block in a register (no memory read per block)
+    uint32_t layout = 0;
+    for (int i = 0; i < bpm; ++i) layout |= (uint32_t)(mcu_comp[i] & 3) << (2 * i);
+    int c = (int)(layout >> (2 * b)) & 3;
     uint32_t guard = end - pos + 64;   // every codeword consumes >= 1 bit
     while (pos < end && guard--) {
         const uint32_t x = window32(words, woff, nwords, pos);
@@ -196,7 +199,7 @@ __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_
         const bool eob = kn >= 64;
         b = eob ? (b + 1 == bpm ? 0 : b + 1) : b;
         k = eob ? 0 : kn;
-        c = mcu_comp[b];
+        c = (int)(layout >> (2 * b)) & 3;
         if (Sink::kValues && eob) sink.end_block();
     }
     return pack_state(pos, b, k);
