@@ -177,15 +177,37 @@ __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_
     uint32_t layout = 0;
     for (int i = 0; i < bpm; ++i) layout |= (uint32_t)(mcu_comp[i] & 3) << (2 * i);
     int c = (int)(layout >> (2 * b)) & 3;
+    // bit buffer: buf holds stream bits [pos, pos + cnt) left-aligned, cnt >= 32 at the top of
+    // every iteration; nxt is the next stream word, loaded an iteration before it is needed, so
+    // the only reads on a codeword's critical path are its table entries
+    const uint32_t last = nwords - 1;
+    auto rd = [&](uint32_t wi) -> uint32_t {
+        const uint32_t j = wi - woff;
+        const uint32_t v = words[j < nwords ? j : last];
+        return j < nwords ? v : 0u;
+    };
+    uint32_t wi = pos >> 5;
+    uint64_t buf = (((uint64_t)rd(wi) << 32) | rd(wi + 1)) << (pos & 31);
+    int cnt = 64 - (int)(pos & 31);
+    wi += 2;
+    uint32_t nxt = rd(wi);
     uint32_t guard = end - pos + 64;   // every codeword consumes >= 1 bit
     while (pos < end && guard--) {
-        const uint32_t x = window32(words, woff, nwords, pos);
+        const bool need = cnt < 32;
+        buf |= need ? (uint64_t)nxt << ((32 - cnt) & 63) : 0ull;
+        cnt += need ? 32 : 0;
+        wi += need ? 1u : 0u;
+        nxt = rd(wi);
+        const uint32_t x = (uint32_t)(buf >> 32);
         const bool isdc = k == 0;
         const uint32_t e = huff_entry(T + (isdc ? c : 3 + c), x);
         const int cl = (int)(e & 15) + 1;
         const int s = (int)((e >> 4) & 31);
         const int adv = (int)((e >> 9) & 63) + 1;
-        pos += (uint32_t)(cl + s);
+        const int used = cl + s;
+        pos += (uint32_t)used;
+        buf = used < 64 ? buf << used : 0ull;
+        cnt -= used;
         if (Sink::kValues) {
             const uint32_t raw = s ? (x << cl) >> (32 - s) : 0u;
             const int v = s ? huff_extend((int)raw, s) : 0;
