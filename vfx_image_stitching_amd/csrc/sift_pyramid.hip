@@ -302,8 +302,8 @@ gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t 
 #define PANO_BLUR_ABL 0     // timing ablations of blur_fast only: bit 2 no stores, 4 no loads
 #endif
 // Row pass, RowVec_32f: output j takes taps t = 0..NT-1 in order, the first as a product.
-template <int NT, int SEG>
-__device__ __forceinline__ void row_seg(const float *__restrict__ p, const float *__restrict__ k,
+template <int NT, int SEG, typename PF = const float *>
+__device__ __forceinline__ void row_seg(PF __restrict__ p, const float *__restrict__ k,
                                         float (&acc)[SEG]) {
 #pragma unroll
     for (int i = 0; i < SEG + NT - 1; ++i) {
@@ -335,7 +335,8 @@ __device__ __forceinline__ void col_seg(const float *__restrict__ p, int stride,
 }
 
 // Runtime tap count fallback (sigma values other than the reference defaults).
-__device__ __forceinline__ float row_one(const float *__restrict__ p, const float *__restrict__ k, int n) {
+template <typename PF = const float *, typename KF = const float *>
+__device__ __forceinline__ float row_one(PF __restrict__ p, KF __restrict__ k, int n) {
     float acc = p[0] * k[0];
     for (int t = 1; t < n; ++t) acc = __builtin_fmaf(p[t], k[t], acc);
     return acc;
@@ -900,22 +901,53 @@ __device__ __forceinline__ int tail_src(int d, double inv) {   // OpenCV INTER_N
     return (int)floor(d * inv);
 }
 
-// One tail level, compile-time tap count (NT = 0: runtime count n).  in / outb are [64][kTP]
-// LDS planes; g / d the frame's Gaussian and DoG planes in HBM.  The small octaves are all
-// border: instead of reflecting every tap (a runtime modulo per tap and output), the level
-// is first copied into `pad` with its BORDER_REFLECT_101 columns ([H][W + 2R]), the row pass
-// runs branch-free over it into rows [R, R + H) of `rowt`, whose reflected halo rows are then
-// filled in, and the column pass runs branch-free too.  SG outputs per thread per pass
-// (register-blocked sliding window, taps in tap order: blur_level's arithmetic).
+// Tail LDS layout.  A level plane is stored with its BORDER_REFLECT_101 columns already in
+// place: row y at y * kPP, image column x at kOff + x, and the mirrored columns the NEXT
+// level's row pass reads (x in [-Rn, 0) and [W, W + Rn)) written by the thread that
+// computes column x's value (tail_mirrors).  Likewise the row pass writes each row-pass
+// output row also to the mirrored rows [-R, 0) and [H, H + R) of rowt (a reflected halo row
+// IS the row pass of an image row).  So a level is two phases and two barriers: the row pass
+// over the H image rows from the padded plane into rowt, and the column pass reading rowt
+// rows through the octave's table of reflected row offsets (rowix: a wave-uniform LDS read
+// per tap row), writing the next padded plane, its mirrors, the Gaussian level and the DoG.
 constexpr int kRMax = (PANO_MAX_TAPS - 1) / 2;
-constexpr int kPP = (kTailDim + 8 + 2 * kRMax) | 1;     // pad pitch (segment overrun included)
-constexpr int kRowtRows = kTailDim + 8 + 2 * kRMax;
+constexpr int kOff = kRMax;                               // padded column of image column 0
+constexpr int kPP = (kTailDim + 2 * kRMax) | 1;           // padded plane pitch (odd)
+constexpr int kRowIx = kTailDim + 2 * kRMax + 8;          // reflected row table (+ SG overrun)
 
-template <int NT>
-__device__ __forceinline__ void tail_level(const float *in, float *outb, float *pad, float *rowt, int H,
-                                           int W, const float *__restrict__ taps_g, int n_rt, float *g,
-                                           float *d, int tid) {
-    constexpr int SG = 8;
+// call f(m) for every m of [-Rn, 0) u [n, n + Rn) whose BORDER_REFLECT_101 source is x (the
+// reflection has period P = 2n - 2: sources x + kP and -x + kP)
+template <typename F>
+__device__ __forceinline__ void tail_mirrors(int x, int n, int Rn, F f) {
+    if (Rn <= 0) return;
+    if (n == 1) {
+        for (int m = 1; m <= Rn; ++m) { f(-m); f(m); }
+        return;
+    }
+    const int P = 2 * n - 2;
+    for (int m = x - P; m >= -Rn; m -= P) f(m);
+    for (int m = x + P; m < n + Rn; m += P) f(m);
+    if (x != 0 && x != n - 1) {                          // x = 0 / n - 1: the same positions
+        for (int m = -x; m >= -Rn; m -= P) f(m);
+        for (int m = P - x; m < n + Rn; m += P) f(m);
+    }
+}
+
+// One tail level: compile-time tap count NT with SG outputs per thread item (register-blocked
+// sliding windows, taps in tap order: blur_level's arithmetic), or NT = 0: runtime count n,
+// one output per item.  in / outp: padded planes (column 0 at kOff); rowt: [kTailDim][kTP];
+// rowix[kRMax + r] = kTP * reflect101(r, H) for r in [-kRMax, H + kRMax).
+// LDS / global address-space pointers: tail_level is a real call (inlining its ten
+// instances into blur_tail ran out of scalar registers), so its pointer arguments carry
+// their address space explicitly -- plain pointers would become flat accesses.
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) int lds_i32;
+typedef __attribute__((address_space(1))) float gbl_f32;
+
+template <int NT, int SG>
+__device__ __noinline__ void tail_level(const lds_f32 *in, lds_f32 *outp, lds_f32 *rowt, const lds_i32 *rowix,
+                                        int H, int W, int Rn, const lds_f32 *__restrict__ taps_g, int n_rt,
+                                        gbl_f32 *g, gbl_f32 *d, int tid) {
     const int n = NT > 0 ? NT : n_rt;
     const int R = (n - 1) / 2;
     float k[NT > 0 ? NT : 1];
@@ -923,86 +955,105 @@ __device__ __forceinline__ void tail_level(const float *in, float *outb, float *
 #pragma unroll
         for (int t = 0; t < NT; ++t) k[t] = taps_g[t];
     }
-    auto row = [&](const float *p, float (&acc)[SG]) {
+    // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
+    const int nseg = (W + SG - 1) / SG;
+    for (int it = tid; it < H * nseg; it += kTailThreads) {
+        const int y = it % H, x0 = (it / H) * SG;
+        const lds_f32 *p = in + y * kPP + kOff - R + x0;
+        float acc[SG];
         if constexpr (NT > 0) {
             row_seg<NT, SG>(p, k, acc);
         } else {
 #pragma unroll
             for (int j = 0; j < SG; ++j) acc[j] = row_one(p + j, taps_g, n);
         }
-    };
-    auto col = [&](const float *p, int stride, float (&acc)[SG]) {
-        if constexpr (NT > 0) {
-            col_seg<NT, SG>(p, stride, k, acc);
-        } else {
-#pragma unroll
-            for (int j = 0; j < SG; ++j) acc[j] = col_one(p + j * stride, stride, taps_g, n);
-        }
-    };
-    // reflected columns
-    const int PW = W + 2 * R;
-    constexpr int NWV = kTailThreads / 64;
-    const int lane = tid & 63, wv = tid >> 6;           // rows by wave, columns by lane
-    for (int y = wv; y < H; y += NWV)
-        for (int c = lane; c < PW; c += 64) pad[y * kPP + c] = in[y * kTP + reflect101(c - R, W)];
-    lds_barrier();
-    // row pass: item = (row y, segment of SG columns); lanes on consecutive rows
-    const int nseg = (W + SG - 1) / SG;
-    for (int it = tid; it < H * nseg; it += kTailThreads) {
-        const int y = it % H, x0 = (it / H) * SG;
-        float acc[SG];
-        row(pad + y * kPP + x0, acc);
 #pragma unroll
         for (int j = 0; j < SG; ++j)
-            if (x0 + j < W) rowt[(y + R) * kTP + x0 + j] = acc[j];
-    }
-    lds_barrier();
-    // reflected rows of the row-pass output
-    for (int q = wv; q < 2 * R; q += NWV) {
-        const int ry = q < R ? q - R : H + (q - R);
-        const int sy = reflect101(ry, H);
-        for (int x = lane; x < W; x += 64) rowt[(ry + R) * kTP + x] = rowt[(sy + R) * kTP + x];
+            if (x0 + j < W) rowt[y * kTP + x0 + j] = acc[j];
     }
     lds_barrier();
     // column pass: item = (column x, segment of SG rows); lanes on consecutive columns
     const int nrs = (H + SG - 1) / SG;
     for (int it = tid; it < W * nrs; it += kTailThreads) {
         const int x = it % W, y0 = (it / W) * SG;
+        // rows y0 - R ... through the octave's reflected row table (offsets into rowt)
+        const lds_i32 *rix = rowix + kRMax + y0;
         float acc[SG];
-        col(rowt + y0 * kTP + x, kTP, acc);
+        if constexpr (NT > 0) {
+            constexpr int RR = (NT - 1) / 2;
+            float v[SG + NT - 1];
+#pragma unroll
+            for (int i = 0; i < SG + NT - 1; ++i) v[i] = rowt[rix[i - RR] + x];
+#pragma unroll
+            for (int j = 0; j < SG; ++j) acc[j] = v[j + RR] * k[RR];
+#pragma unroll
+            for (int dd = 1; dd <= RR; ++dd)
+#pragma unroll
+                for (int j = 0; j < SG; ++j) acc[j] = __builtin_fmaf(v[j + RR + dd] + v[j + RR - dd], k[RR + dd], acc[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < SG; ++j) {
+                float a = rowt[rix[j] + x] * taps_g[R];
+                for (int dd = 1; dd <= R; ++dd)
+                    a = __builtin_fmaf(rowt[rix[j + dd] + x] + rowt[rix[j - dd] + x], taps_g[R + dd], a);
+                acc[j] = a;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < SG; ++j) {
             const int y = y0 + j;
             if (y >= H) break;
             const float o = acc[j];
-            outb[y * kTP + x] = o;
+            lds_f32 *orow = outp + y * kPP + kOff;
+            orow[x] = o;
+            tail_mirrors(x, W, Rn, [&](int m) { orow[m] = o; });
             if (g) g[y * W + x] = o;
-            d[y * W + x] = o - in[y * kTP + x];
+            d[y * W + x] = o - in[y * kPP + kOff + x];
         }
     }
 }
 
+#ifndef PANO_TAIL_GENERIC
+#define PANO_TAIL_GENERIC 0   // 1: every tail level through the runtime tap-count loops (small code)
+#endif
+#ifndef PANO_TAIL_TIMING
+#define PANO_TAIL_TIMING 0    // 1: frame 0's workgroup records s_memtime after every level (diagnostics)
+#endif
+#if PANO_TAIL_TIMING
+__device__ unsigned long long g_tail_clock[64];
+#define PANO_TAIL_STAMP(i) \
+    do { if (f == 0 && tid == 0 && (i) < 64) g_tail_clock[(i)] = (unsigned long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PANO_TAIL_STAMP(i) do {} while (0)
+#endif
+
 __global__ void __launch_bounds__(kTailThreads)
 blur_tail(TailArgs ta) {
     __shared__ float taps_s[PANO_MAX_LEVELS * PANO_MAX_TAPS];   // every level's taps, loaded once
-    __shared__ float lv[3][kTailDim * kTP];      // current / next level, octave seed
-    __shared__ float pad[kTailDim * kPP];         // level with reflected columns
-    __shared__ float rowt[kRowtRows * kTP];       // row-pass output with reflected rows
+    __shared__ float lv[3][kTailDim * kPP];      // padded planes: current / next level, octave seed
+    __shared__ float rowt[kTailDim * kTP];        // row-pass output
+    __shared__ int rowix[kRowIx];                 // reflected row offsets into rowt
     // the tail is a latency chain of 18 workgroups running beside the extrema scan, which
     // fills every CU: raise its waves' issue priority so the chain is not starved
     __builtin_amdgcn_s_setprio(3);
     const int f = blockIdx.x, tid = threadIdx.x;
+    PANO_TAIL_STAMP(0);
     // taps to LDS once: each level's loop then starts on LDS reads, not on a global load
     for (int i = tid; i < ta.n_lvl * PANO_MAX_TAPS; i += kTailThreads) taps_s[i] = ta.taps[i];
-    lds_barrier();
     int cur = 0, keep = -1;
+    int stamp = 1;
+    (void)stamp;
     for (int oi = 0; oi < ta.n_oct; ++oi) {
         const int H = ta.H[oi], W = ta.W[oi];
+        // planes up to 32 x 32: 2 outputs per thread item (a short serial chain per thread);
+        // larger: 8 (every item fits one pass of the 512 threads at 64 x 48)
+        const bool small = H <= 32 && W <= 32;
         // ---- level 0: nearest 1/2 of the previous octave's level n_lvl-3
         {
             const int sh = oi == 0 ? ta.ph : ta.H[oi - 1];
             const int sw = oi == 0 ? ta.pw : ta.W[oi - 1];
             const double ifx = 1.0 / ((double)W / sw), ify = 1.0 / ((double)H / sh);
+            const int R1 = (ta.ntap[1] - 1) / 2;
             int dst = 0;
             while (dst == keep) ++dst;
             float *o0 = lv[dst];
@@ -1011,30 +1062,52 @@ blur_tail(TailArgs ta) {
                 const int y = i / W, x = i - (i / W) * W;
                 const int sy = min(tail_src(y, ify), sh - 1), sx = min(tail_src(x, ifx), sw - 1);
                 const float v = oi == 0 ? ta.prev[(size_t)f * sh * sw + (size_t)sy * sw + sx]
-                                        : lv[keep][sy * kTP + sx];
-                o0[y * kTP + x] = v;
+                                        : lv[keep][sy * kPP + kOff + sx];
+                float *orow = o0 + y * kPP + kOff;
+                orow[x] = v;
+                tail_mirrors(x, W, R1, [&](int m) { orow[m] = v; });
                 if (g0) g0[i] = v;
             }
+            for (int r = tid; r < kRowIx; r += kTailThreads)   // rows past H + kRMax: SG overrun
+                rowix[r] = kTP * reflect101(min(r - kRMax, H + kRMax - 1), H);
             cur = dst;
             keep = -1;
             lds_barrier();
+            PANO_TAIL_STAMP(stamp);
+            ++stamp;
         }
         for (int l = 1; l < ta.n_lvl; ++l) {
             const int n = ta.ntap[l];
+            const int Rn = l + 1 < ta.n_lvl ? (ta.ntap[l + 1] - 1) / 2 : 0;   // next level's halo
             int out = 0;
             while (out == cur || out == keep) ++out;
             float *g = (ta.full || l < ta.n_lvl - 1) ? ta.G[oi][l] + (size_t)f * H * W : nullptr;
             float *d = ta.D[oi][l - 1] + (size_t)f * H * W;
             const float *tg = taps_s + l * PANO_MAX_TAPS;
+            const lds_f32 *Lin = (const lds_f32 *)lv[cur];
+            lds_f32 *Lout = (lds_f32 *)lv[out], *Lrowt = (lds_f32 *)rowt;
+            const lds_i32 *Lrix = (const lds_i32 *)rowix;
+            const lds_f32 *Ltg = (const lds_f32 *)tg;
+            gbl_f32 *Gg = (gbl_f32 *)g, *Gd = (gbl_f32 *)d;
+#define PANO_TAIL_LEVEL(NT)                                                                        \
+    (small ? tail_level<NT, 2>(Lin, Lout, Lrowt, Lrix, H, W, Rn, Ltg, n, Gg, Gd, tid)                  \
+           : tail_level<NT, 8>(Lin, Lout, Lrowt, Lrix, H, W, Rn, Ltg, n, Gg, Gd, tid))
+#if PANO_TAIL_GENERIC
+            tail_level<0, 1>(Lin, Lout, Lrowt, Lrix, H, W, Rn, Ltg, n, Gg, Gd, tid);
+#else
             switch (n) {   // the reference's kernel sizes; others take the runtime-count path
-                case 11: tail_level<11>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
-                case 13: tail_level<13>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
-                case 17: tail_level<17>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
-                case 21: tail_level<21>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
-                case 27: tail_level<27>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
-                default: tail_level<0>(lv[cur], lv[out], pad, rowt, H, W, tg, n, g, d, tid); break;
+                case 11: PANO_TAIL_LEVEL(11); break;
+                case 13: PANO_TAIL_LEVEL(13); break;
+                case 17: PANO_TAIL_LEVEL(17); break;
+                case 21: PANO_TAIL_LEVEL(21); break;
+                case 27: PANO_TAIL_LEVEL(27); break;
+                default: tail_level<0, 1>(Lin, Lout, Lrowt, Lrix, H, W, Rn, Ltg, n, Gg, Gd, tid); break;
             }
+#endif
+#undef PANO_TAIL_LEVEL
             lds_barrier();
+            PANO_TAIL_STAMP(stamp);
+            ++stamp;
             cur = out;
             if (l == ta.n_lvl - 3) keep = cur;
         }
@@ -1561,6 +1634,13 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     ctx->pyr_full = full;
     return PANO_OK;
 }
+
+#if PANO_TAIL_TIMING
+// diagnostics build only (not in pano.h): the stamps of the last blur_tail, after a sync
+extern "C" int pano_dbg_tail_clock(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail_clock), sizeof(g_tail_clock)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                         const pano_sift_params *p, bool defer_tail, bool full) {
