@@ -116,6 +116,11 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->lvl_side) (void)hipStreamSynchronize(ctx->lvl_side);
+    if (ctx->lvl_side) (void)hipStreamDestroy(ctx->lvl_side);
+    for (hipEvent_t e : ctx->ev_lvl)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->ev_lvl_join) (void)hipEventDestroy(ctx->ev_lvl_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
                     ctx->boxslots, ctx->hmscratch, ctx->dorder};

@@ -114,6 +114,11 @@ struct pano_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool tail_pending = false;           // blur_tail enqueued on `side`, not yet joined
+    // second side stream: levels nl-2.. of an octave (PANO_OCT_FORK) beside the next octave's
+    // first levels, which need only level nl-3; joined before anything reads them
+    hipStream_t lvl_side = nullptr;
+    hipEvent_t ev_lvl[PANO_MAX_OCTAVES] = {};
+    hipEvent_t ev_lvl_join = nullptr;
     int o_tail = 0;                      // first octave of the tail
     bool pyr_full = false;               // every Gaussian level materialised (see launch_sift_pyramid)
     // ---- hipGraph capture (pano_graph_begin / end)

@@ -1132,7 +1132,9 @@ __device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ coun
 }
 
 #ifndef PANO_DESC_OCC
-#define PANO_DESC_OCC 4               // waves per SIMD the register budget is sized for
+#define PANO_DESC_OCC 3               // waves per SIMD the register budget is sized for (measured:
+                                      // 3 -> 168 VGPRs, no spills, 250-257 us parrington; 4 -> 128
+                                      // VGPRs with spills, 260 us; 5 -> 264 us)
 #endif
 template <bool OUT_U8>
 __global__ void __launch_bounds__(64 * kDescWaves, PANO_DESC_OCC)

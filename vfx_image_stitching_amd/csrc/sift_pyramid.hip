@@ -1519,9 +1519,21 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         const char *e = getenv("PANO_BLUR_PAIR");
         return e ? atoi(e) : 0;
     }();
+    // Levels nl-2 and nl-1 of octave o (4 and 5 by default) on a second side stream, beside
+    // octave o+1's first levels, which read only level nl-3 of octave o: the octaves' chains
+    // of small latency-bound launches then overlap instead of running back to back.  From
+    // octave PANO_OCT_FORK on (-1: off); joined into the main stream after the octave loop.
+    // Measured on MI355X: bit-exact, but 1.34-1.55 ms per graph-replayed
+    // parrington stitch against 1.16 ms unforked (from octave 0, 1 or 2), so off by default.
+    static const int oct_fork = [] {
+        const char *e = getenv("PANO_OCT_FORK");
+        return e ? atoi(e) : -1;
+    }();
+    bool lvl_forked = false;
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
         ctx->stream = o >= o_side ? ctx->side : main_stream;     // side-stream octaves
+        const bool fork_lvl = oct_fork >= 0 && o >= oct_fork && o < o_side && nl >= 4 && !chain_ok(o);
         if (chain_ok(o)) {
             // chain A: levels 1-2 (octave 0 from gray: base, 1, 2); chain B: levels 3-5 from G2.
             // Written: G1-G3 and DoG 0-4 (every level in a full pyramid)
@@ -1571,6 +1583,19 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         const bool pairs_here = o >= 1 && nl == 6 && H >= 32 && W >= 32 &&
                                 (long)((W + 63) / 64) * ((H + 63) / 64) * n < pair_tiles;
         for (int l = 1; l < nl; ++l) {
+            if (fork_lvl && l == nl - 2) {
+                if (!ctx->lvl_side) {
+                    int lo_prio = 0, hi_prio = 0;
+                    PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+                    PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->lvl_side, hipStreamNonBlocking, lo_prio));
+                    PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_lvl_join, hipEventDisableTiming));
+                }
+                if (!ctx->ev_lvl[o]) PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_lvl[o], hipEventDisableTiming));
+                PANO_HIP(ctx, hipEventRecord(ctx->ev_lvl[o], main_stream));
+                PANO_HIP(ctx, hipStreamWaitEvent(ctx->lvl_side, ctx->ev_lvl[o], 0));
+                ctx->stream = ctx->lvl_side;
+                lvl_forked = true;
+            }
             float *out = G + ctx->gauss_off[o][l];
             float *dg = D + ctx->dog_off[o][l - 1];
             LoadArgs la{};
@@ -1624,6 +1649,10 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         }
     }
     ctx->stream = main_stream;
+    if (lvl_forked) {
+        PANO_HIP(ctx, hipEventRecord(ctx->ev_lvl_join, ctx->lvl_side));
+        PANO_HIP(ctx, hipStreamWaitEvent(main_stream, ctx->ev_lvl_join, 0));
+    }
     if (o_tail < no) {
         rc = launch_tail();
         if (rc) return rc;

@@ -473,7 +473,8 @@ class Stitcher:
             else:
                 self._fast_key = fk
                 cyl, colnz, head, off_bb, off_plan, canvas = self._planned(frames_dev, focals)
-            recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1).copy()
+            head = head.copy()          # ONE read of the pinned head; the next run() reuses it
+            recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1)
             hdr = head[off_plan:off_plan + 32].view(np.int32)
             t["features_match_ransac"] = tick() - t0
             self._check_records(recs)
@@ -482,10 +483,10 @@ class Stitcher:
             if hdr[0] == _lib.PANO_OK:
                 shifts, best_pairs = self._shifts(recs)
                 H, W = int(hdr[1]), int(hdr[2])
-                view = canvas.as_strided((H, W, 3), (W * 3, 3, 1))
                 slots = head[off_bb:off_bb + 16 * BBOX_SLOTS].view(np.int32).reshape(BBOX_SLOTS, 4)
-                bb = (slots[:, 0].min(), slots[:, 1].max(), slots[:, 2].min(), slots[:, 3].max())
-                return self._crop(view, bb, margin, shifts, best_pairs, recs, t, t0)
+                mn, mx = slots.min(axis=0), slots.max(axis=0)
+                bb = (int(mn[0]), int(mx[1]), int(mn[2]), int(mx[3]))
+                return self._crop_planned(canvas, H, W, bb, margin, shifts, best_pairs, recs, t, t0)
             # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
             return self._finish(cyl, colnz, recs, margin, graph, t, t0)
         cyl, colnz, recs_dev = self.records(frames_dev, focals, graph)
@@ -523,6 +524,22 @@ class Stitcher:
         canvas, bb_dev = self.composite(cyl, colnz, corr, pxy, bbox=True, graph=graph)
         bb = bb_dev.cpu().numpy()                                        # sync point 2
         return self._crop(canvas, bb, margin, shifts, best_pairs, recs, t, t0)
+
+    def _crop_planned(self, buf, H, W, bb, margin, shifts, best_pairs, recs, t, t0):
+        """_crop on the device-planned canvas (an H x W x 3 view of the capacity buffer), with
+        one strided view each for the canvas and the panorama."""
+        canvas = buf.as_strided((H, W, 3), (W * 3, 3, 1))
+        if bb[1] < 0:
+            y0, y1, x0, x1 = 0, H - 1, 0, W - 1
+            pano = canvas
+        else:
+            y0 = max(0, bb[0] + margin)
+            y1 = min(H - 1, bb[1] - margin)
+            x0, x1 = bb[2], bb[3]
+            pano = canvas if (y0 > y1 or x0 > x1) else buf.as_strided(
+                (y1 + 1 - y0, x1 + 1 - x0, 3), (W * 3, 3, 1), buf.storage_offset() + y0 * W * 3 + x0 * 3)
+        t["total"] = time.perf_counter() - t0
+        return StitchResult(pano, canvas, shifts, best_pairs, recs, (y0, y1, x0, x1), t)
 
     def _crop(self, canvas, bb, margin, shifts, best_pairs, recs, t, t0):
         """rectangle_crop (image_stitching_sift.py:208-247) from the fused bbox."""
