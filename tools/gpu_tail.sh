@@ -1,6 +1,6 @@
 #!/bin/bash
-# Tail check: pyramid/SIFT parity subset, per-level stamps of blur_tail, bench lines of the
-# side-stream octave split.
+# Tail check: GPU parity subset, per-level stamps of blur_tail (solo / beside the extrema
+# scan), then bench A/B of the working tree against tools/ab/libpano_HEAD.so.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out/tail
@@ -15,9 +15,13 @@ for solo in 1 0; do
   [ $rc -ne 0 ] && exit $rc
 done
 unset PANO_TAIL_SOLO
-for so in 0 1 2 0 1 2; do
-  PANO_SIDE_OCT=$so timeout -k 10 180 python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline > $O/bench_side$so.txt 2>&1
-  rc=$?; echo "side=$so rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $O/bench_side$so.txt | head -1) $(grep -o '"kernel_ms_per_step": [0-9.]*' $O/bench_side$so.txt | head -1)"
-  [ $rc -ne 0 ] && exit $rc
+for i in 1 2; do
+  for lib in vfx_image_stitching_amd/libpano.so tools/ab/libpano_HEAD.so; do
+    tag=$(basename $lib .so)_$i
+    PANO_LIB=$lib timeout -k 10 240 python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline > $O/bench_$tag.txt 2>&1
+    rc=$?
+    echo "$tag rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $O/bench_$tag.txt | head -1) $(grep -o '"blur_level": [0-9.]*' $O/bench_$tag.txt | head -1) $(grep -o '"extrema_localize": [0-9.]*' $O/bench_$tag.txt | head -1)"
+    [ $rc -ne 0 ] && exit $rc
+  done
 done
 exit 0

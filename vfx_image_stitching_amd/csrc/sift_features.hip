@@ -1645,8 +1645,11 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         return e && atoi(e) == 16 ? 16 : XSR;
     }();
     static const int xmin_h = [] {
-        const char *e = getenv("PANO_EXTREMA_STREAM_MIN_H");   // 0 disables the streaming kernel
-        return e ? atoi(e) : 192;
+        // 0 disables the streaming kernel.  Measured (same box): 96 -- parrington's octave 3
+        // joins the streaming launch instead of its own scan -- 164-167 us per extrema class
+        // against 175-178 us at 192; 48 within noise of 96
+        const char *e = getenv("PANO_EXTREMA_STREAM_MIN_H");
+        return e ? atoi(e) : 96;
     }();
     if (tiles > 0) {
         XArgs xa{};
