@@ -254,23 +254,63 @@ __global__ void composite_owner(const uint8_t *__restrict__ mode, const float2 *
 // each thread walks 8 rows; byte loads / stores are contiguous across the wave.  One bbox
 // atomic per workgroup.
 constexpr int kCompRows = 8;
+// The owner record of canvas column X (composite_owner's per-column work), for the
+// device-planned composite, which computes it in composite_pixels itself: the owner is
+// usually the last or second-to-last frame tried, and the recomputation per 32-row block
+// costs less than a launch.
+__device__ __forceinline__ ColInfo column_owner(const uint8_t *__restrict__ mode, const float2 *__restrict__ wgt,
+                                                int n, int w, const SeqArg &sa, int X) {
+    int o = -1;
+    for (int i = n - 1; i >= 0; --i) {
+        const int c = X - sa.fx[i];
+        if (c >= 0 && c < w && mode[(size_t)i * w + c]) { o = i; break; }
+    }
+    ColInfo ci{};
+    ci.i = o;
+    if (o >= 0) {
+        ci.c = X - sa.fx[o];
+        ci.fy = sa.fy[o];
+        ci.mode = mode[(size_t)o * w + ci.c];
+        ci.is_a = sa.is_a[o];
+        const float2 ab = wgt[(size_t)o * w + ci.c];
+        ci.w0 = ab.x;
+        ci.w1 = ab.y;
+        ci.cm = -1;
+        if (o > 0) {
+            const int cm = X - sa.fx[o - 1];
+            ci.cm = (cm >= 0 && cm < w) ? cm : -1;
+            ci.fym = sa.fy[o - 1];
+        }
+    }
+    return ci;
+}
+
 template <bool DEV>
 __global__ void __launch_bounds__(256)
 composite_pixels(const uint8_t *__restrict__ frames, int h, int w, const ColInfo *__restrict__ info,
                  uint8_t *__restrict__ canvas, int H, int W, int thr, int32_t *__restrict__ bbox,
-                 const DevPlan *__restrict__ dp) {
+                 const DevPlan *__restrict__ dp, const uint8_t *__restrict__ mode = nullptr,
+                 const float2 *__restrict__ wgt = nullptr) {
     __shared__ int r[4][256];
     const int tid = threadIdx.x;
-    if (DEV) {   // grid sized for the capacity; the planned canvas is [H][W] inside it
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (DEV) {
+        // grid sized for the capacity; the planned canvas is [H][W] inside it.  The linear
+        // block id is remapped onto the planned canvas's blocks, so the live blocks are the
+        // first ones dispatched (not interleaved with the empty capacity columns of each row)
         H = dp->status == PANO_OK ? dp->H : 0;
         W = dp->status == PANO_OK ? dp->W : 0;
-        if ((int)blockIdx.x * 64 >= W || (int)blockIdx.y * 4 * kCompRows >= H) return;
+        const int nbx = (W + 63) / 64, nby = (H + 4 * kCompRows - 1) / (4 * kCompRows);
+        const int b = blockIdx.x + gridDim.x * blockIdx.y;
+        if (b >= nbx * nby) return;
+        by = b / nbx;
+        bx = b - by * nbx;
     }
     int ymin = 0x7fffffff, ymax = -1, xmin = 0x7fffffff, xmax = -1;
-    const int X = blockIdx.x * 64 + (tid & 63);
-    const int y0 = (blockIdx.y * 4 + (tid >> 6)) * kCompRows;
+    const int X = bx * 64 + (tid & 63);
+    const int y0 = (by * 4 + (tid >> 6)) * kCompRows;
     if (X < W) {
-        const ColInfo ci = info[X];
+        const ColInfo ci = DEV ? column_owner(mode, wgt, dp->n, w, dp->sa, X) : info[X];
         // all rows' source bytes first (loads in flight together), then blend and store
         uint8_t F[kCompRows][3], M[kCompRows][3];
         const uint8_t *fp = frames + (((size_t)max(ci.i, 0) * h) * w + ci.c) * 3;
@@ -769,16 +809,12 @@ int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t
         composite_tables<true><<<n, 256, 0, ctx->stream>>>(colnz, w, none, dp, mode, wgt, bbox);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_tables");
-    {
-        PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_owner<true><<<(Wcap + 255) / 256, 256, 0, ctx->stream>>>(mode, wgt, n, w, Wcap, none, dp, info);
-    }
-    PANO_LAUNCH_CHECK(ctx, "composite_owner");
+    (void)info;                                  // the owner records: computed per column in composite_pixels
     {
         dim3 grid((Wcap + 63) / 64, (Hcap + 4 * kCompRows - 1) / (4 * kCompRows));
         PanoProf prof_(ctx, PK_COMPOSITE);
-        composite_pixels<true><<<grid, 256, 0, ctx->stream>>>(frames, h, w, info, canvas, Hcap, Wcap, thr,
-                                                              bbox, dp);
+        composite_pixels<true><<<grid, 256, 0, ctx->stream>>>(frames, h, w, nullptr, canvas, Hcap, Wcap, thr,
+                                                              bbox, dp, mode, wgt);
     }
     PANO_LAUNCH_CHECK(ctx, "composite_pixels");
     return PANO_OK;

@@ -365,12 +365,12 @@ dist_u8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
         int n_split) {
     __shared__ __attribute__((aligned(16))) unsigned short Bs2[2][BT * BKP];   // double buffer
     __shared__ Part red[2][QT];
-    const int p = blockIdx.z;
+    const int p = blockIdx.y;             // grid (split, pair, query tile): see launch_match_u8
     const int fa = pairs.a[p], fb = pairs.b[p];
     int NA = counts[fa], NB = counts[fb];
     NA = min(max(NA, 0), cap);
     NB = min(max(NB, 0), cap);
-    const int i0 = blockIdx.y * QT;
+    const int i0 = blockIdx.z * QT;
     const int n_jt = (NB + BT - 1) / BT;
     if (i0 >= NA || (int)blockIdx.x >= n_jt) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -564,7 +564,7 @@ __device__ __forceinline__ int mad_i24(int a, int b, int c) {
 __global__ void __launch_bounds__(256)
 row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
            const int32_t *__restrict__ counts, int cap, int32_t *__restrict__ cst) {
-    const int f = blockIdx.y, row = blockIdx.x * 64 + (threadIdx.x >> 2), part = threadIdx.x & 3;
+    const int f = blockIdx.x, row = blockIdx.y * 64 + (threadIdx.x >> 2), part = threadIdx.x & 3;   // (frame, block)
     const int n = min(max(counts[f], 0), cap);
     unsigned int sum = 0;
     if (row < n) {
@@ -600,12 +600,12 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
 #endif
     struct IPart { int best, idx, second; };
     __shared__ IPart red[2][QT];
-    const int p = blockIdx.z;
+    const int p = blockIdx.y;             // grid (split, pair, query tile): see launch_match_u8
     const int fa = pairs.a[p], fb = pairs.b[p];
     int NA = counts[fa], NB = counts[fb];
     NA = min(max(NA, 0), cap);
     NB = min(max(NB, 0), cap);
-    const int i0 = blockIdx.y * QT;
+    const int i0 = blockIdx.z * QT;
     const int n_jt = (NB + BT - 1) / BT;
     if (i0 >= NA || (int)blockIdx.x >= n_jt) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -762,8 +762,8 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
 __global__ void reduce_parts(const Part *__restrict__ parts, const int32_t *__restrict__ counts,
                              int cap, PairArg pairs, int n_jt, int32_t *__restrict__ best,
                              float *__restrict__ d1, float *__restrict__ d2) {
-    const int p = blockIdx.y;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = blockIdx.x;                         // grid (pair, row block)
+    const int i = blockIdx.y * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     int NA = counts[pairs.a[p]], NB = counts[pairs.b[p]];
     NA = min(max(NA, 0), cap);
@@ -878,7 +878,11 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
         Part *parts = (Part *)ctx->mscratch;
         int32_t *bp = best + (size_t)p0 * cap;
         float *p1 = d1 + (size_t)p0 * cap, *p2 = d2 ? d2 + (size_t)p0 * cap : nullptr;
-        dim3 grid(n_split, n_qt, np);
+        // (split, pair, query tile): the dispatcher walks x, then y fastest, so every pair's
+        // live query tiles (the low ones; the grid is sized by the capacity) go out before the
+        // empty tail -- with the tile index outermost each pair's empty tiles were dispatched
+        // ahead of the next pair's live ones (the same for row_consts and reduce_parts)
+        dim3 grid(n_split, np, n_qt);
         static const bool use_i8 = [] {
             const char *e = getenv("PANO_MATCH_I8");     // 1 (default): i8 MFMA; 0: bf16 MFMA
             return e ? atoi(e) != 0 : true;
@@ -893,7 +897,7 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
             int32_t *cst = (int32_t *)((char *)ctx->mscratch + part_bytes);
             {
                 PanoProf prof_(ctx, PK_NORMS);
-                row_consts<<<dim3((cap + 63) / 64, nf), 256, 0, ctx->stream>>>(desc, norms, counts, cap, cst);
+                row_consts<<<dim3(nf, (cap + 63) / 64), 256, 0, ctx->stream>>>(desc, norms, counts, cap, cst);
             }
             PANO_LAUNCH_CHECK(ctx, "row_consts");
             {
@@ -914,7 +918,7 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
             }
             PANO_LAUNCH_CHECK(ctx, "dist_u8");
         }
-        dim3 g2((cap + 255) / 256, np);
+        dim3 g2(np, (cap + 255) / 256);
         {
             PanoProf prof_(ctx, PK_REDUCE);
             reduce_parts<<<g2, 256, 0, ctx->stream>>>(parts, counts, cap, pa, n_split, bp, p1, p2);
@@ -951,7 +955,7 @@ int launch_match(pano_ctx *ctx, const float *desc, const int32_t *counts, int ca
         }
         const int n_t = (cap + MT - 1) / MT;
         const size_t norm_bytes = ((size_t)n_frames * n_t * MT * sizeof(float) + 255) & ~size_t(255);
-        dim3 g2((cap + 255) / 256, np);
+        dim3 g2(np, (cap + 255) / 256);                      // reduce_parts: (pair, row block)
         if (exact_int == 2) {
             // query tiles x candidate splits x pairs: enough workgroups to fill the GPU even
             // when each pair is small; large pairs walk their candidate tiles in-kernel

@@ -145,11 +145,13 @@ __global__ void __launch_bounds__(VB)
 pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount, int cap,
            double thr, int32_t *__restrict__ votes) {
     __shared__ double2 tile[VB];
+    // grid (split, pair, hypothesis chunk): the chunks are sized by the capacity, and with
+    // the chunk index outermost every live chunk 0 is dispatched before the empty ones
     const int p = blockIdx.y, tid = threadIdx.x;
     const int K = kcount[p];
-    const int m0 = blockIdx.x * VB;
+    const int m0 = blockIdx.z * VB;
     if (m0 >= K) return;                              // whole workgroup
-    const int jlo = (int)((long long)K * blockIdx.z / VJS), jhi = (int)((long long)K * (blockIdx.z + 1) / VJS);
+    const int jlo = (int)((long long)K * blockIdx.x / VJS), jhi = (int)((long long)K * (blockIdx.x + 1) / VJS);
     if (jlo >= jhi) return;
     const double2 *mv = moves + (size_t)p * cap;
     const int m = m0 + tid;
@@ -304,7 +306,7 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
         PANO_LAUNCH_CHECK(ctx, "pair_compact");
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
-            pair_votes<<<dim3((cap + VB - 1) / VB, np, VJS), VB, 0, ctx->stream>>>(moves + o, kcount + p0, cap,
+            pair_votes<<<dim3(VJS, np, (cap + VB - 1) / VB), VB, 0, ctx->stream>>>(moves + o, kcount + p0, cap,
                                                                                   thr, votes + o);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_votes");

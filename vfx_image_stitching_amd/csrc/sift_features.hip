@@ -503,11 +503,13 @@ __global__ void __launch_bounds__(256)
 localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
          const int32_t *__restrict__ raw_cnt, int raw_cap, Cand *__restrict__ cands,
          int32_t *__restrict__ cand_cnt, int cand_cap) {
-    const int f = blockIdx.y;
-    const int ci = blockIdx.x * 256 + threadIdx.x;
+    // grid (frame, block): the dispatcher walks x fastest, so every frame's live blocks (the
+    // low block indices; the grid is sized by the capacity) go out before the empty ones
+    const int f = blockIdx.x;
+    const int ci = blockIdx.y * 256 + threadIdx.x;
     int cnt = raw_cnt[f * kCntStride];
     cnt = cnt < raw_cap ? cnt : raw_cap;
-    if ((int)blockIdx.x * 256 >= cnt) return;   // uniform
+    if ((int)blockIdx.y * 256 >= cnt) return;   // uniform
     bool keep = false;
     Cand k;
     if (ci < cnt) keep = localize_one(a, lp, raw[(size_t)f * raw_cap + ci], f, k);
@@ -867,7 +869,7 @@ __global__ void __launch_bounds__(256)
 bucket_rank(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cnt, int raw_cap, int nb,
             const int32_t *__restrict__ bstart, const uint32_t *__restrict__ mem,
             uint32_t *__restrict__ sorted) {
-    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int f = blockIdx.x, i = blockIdx.y * 256 + threadIdx.x;   // (frame, block): see localize
     const int cnt = raw_cnt[f * kCntStride];
     if (cnt > raw_cap || i >= cnt) return;
     const RawKp *rec = raw + (size_t)f * raw_cap;
@@ -1718,7 +1720,7 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         sift_join_tail(ctx);
         rc = launch_scan(da.tile_start[o_split], tiles);
         if (rc) return rc;
-        dim3 g2((unsigned)((ext_cap + 255) / 256), n);
+        dim3 g2(n, (unsigned)((ext_cap + 255) / 256));
         {
             PanoProf prof_(ctx, PK_EXTREMA);
             localize<<<g2, 256, 0, ctx->stream>>>(da, lp, raw_ext, ext_cnt, (int)ext_cap, ctx->cands,
@@ -1774,7 +1776,7 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         return PANO_OK;
     }
     {
-        dim3 grid((unsigned)((raw_cap + 255) / 256), n);
+        dim3 grid(n, (unsigned)((raw_cap + 255) / 256));       // bucket_rank: (frame, block)
         if (nb > kSortMaxBuckets) return pano_fail(ctx, PANO_E_UNSUPPORTED, "frame too wide for the keypoint sort");
         {
             PanoProf prof_(ctx, PK_SORT);
