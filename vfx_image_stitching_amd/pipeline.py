@@ -32,6 +32,7 @@ from ._lib import PanoError, context, ptr
 
 
 BBOX_SLOTS = 64                         # include/pano.h PANO_BBOX_SLOTS
+_BOX_SIGN = np.array([1, -1, 1, -1], np.int32)
 
 
 class Features(tuple):
@@ -477,15 +478,25 @@ class Stitcher:
             recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1)
             hdr = head[off_plan:off_plan + 32].view(np.int32)
             t["features_match_ransac"] = tick() - t0
-            self._check_records(recs)
+            status = head[:off_bb].view(np.int32).reshape(-1, 16)[:, 15]     # PAIR_NP.status
+            if status.any():
+                self._check_records(recs)
             if hdr[0] == _lib.PANO_E_NOMATCH:
                 raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
             if hdr[0] == _lib.PANO_OK:
-                shifts, best_pairs = self._shifts(recs)
+                if self.method == "sift" and not status.any():
+                    # the records' six doubles (dx dy xA yA xB yB) in one conversion
+                    rows = head[:off_bb].view(np.float64).reshape(-1, 8)[:, :6].tolist()
+                    shifts = [(r[0], r[1]) for r in rows]
+                    best_pairs = [((r[2], r[3]), (r[4], r[5])) for r in rows]
+                else:
+                    shifts, best_pairs = self._shifts(recs)
                 H, W = int(hdr[1]), int(hdr[2])
+                # crop box: min of ymin / xmin and max of ymax / xmax over the partial boxes,
+                # as one min over the sign-flipped columns
                 slots = head[off_bb:off_bb + 16 * BBOX_SLOTS].view(np.int32).reshape(BBOX_SLOTS, 4)
-                mn, mx = slots.min(axis=0), slots.max(axis=0)
-                bb = (int(mn[0]), int(mx[1]), int(mn[2]), int(mx[3]))
+                m = (slots * _BOX_SIGN).min(axis=0).tolist()
+                bb = (m[0], -m[1], m[2], -m[3])
                 return self._crop_planned(canvas, H, W, bb, margin, shifts, best_pairs, recs, t, t0)
             # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
             return self._finish(cyl, colnz, recs, margin, graph, t, t0)
