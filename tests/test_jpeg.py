@@ -114,6 +114,19 @@ def test_sim_decode_equals_pil_on_variants(jpeg_sim, tmp_path, i):
     assert np.array_equal(out, _pil_bgr(buf))
 
 
+def _with_trailer(buf: bytes) -> bytes:
+    """A phone-style file: a second complete JPEG (an MPF secondary image / thumbnail) and a
+    few junk bytes appended after EOI.  libjpeg stops at the first EOI and ignores the rest."""
+    return buf + _encode(_texture(24, 40, 5), quality=60) + b"\x00\xffjunk"
+
+
+def test_sim_decode_ignores_data_after_eoi(jpeg_sim, tmp_path):
+    for buf in (_set_jpegs("parrington")[0], _variant_jpeg(2)):
+        st, out = _sim(jpeg_sim, _with_trailer(buf), tmp_path)
+        assert st["status"] == 0, st
+        assert np.array_equal(out, _pil_bgr(buf))
+
+
 def test_sim_without_warmup_still_exact(jpeg_sim, tmp_path):
     """No warm-up window (every warm candidate a guess at its subsequence's first bit): the
     fix candidates and the resolve fallback decode the subsequences from their true starts,
@@ -204,6 +217,16 @@ def test_gpu_decode_truncated_and_corrupt_streams(gpu):
     out, st = jpeg.decode_batch([good[0], bytes(bad), good[2]], status=True)
     o = out.cpu().numpy()
     assert np.array_equal(o[0], _pil_bgr(good[0])) and np.array_equal(o[2], _pil_bgr(good[2]))
+
+
+@pytest.mark.gpu
+def test_gpu_decode_ignores_data_after_eoi(gpu):
+    from vfx_image_stitching_amd import jpeg
+    bufs = _set_jpegs("parrington")[:2]
+    out, st = jpeg.decode_batch([_with_trailer(bufs[0]), bufs[1]], status=True)
+    assert st.cpu().numpy().tolist() == [0, 0]
+    o = out.cpu().numpy()
+    assert np.array_equal(o[0], _pil_bgr(bufs[0])) and np.array_equal(o[1], _pil_bgr(bufs[1]))
 
 
 @pytest.mark.gpu

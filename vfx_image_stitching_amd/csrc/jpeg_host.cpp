@@ -276,11 +276,19 @@ int parse(const uint8_t *buf, size_t len, Parsed *P, std::string *err) {
                 if (order[q] != q) return fail(err, PANO_E_UNSUPPORTED, "scan order differs from frame order");
             const uint8_t *t = s + 1 + 2 * ns;
             if (t[0] != 0 || t[1] != 63 || t[2] != 0) return fail(err, PANO_E_UNSUPPORTED, "JPEG scan is not sequential DCT");
-            // Entropy-coded segment: from here to the last EOI, without trailing fill bytes.
+            // Entropy-coded segment: from here up to the first marker that is neither a stuffed
+            // 0xFF00 nor an RSTn (fill bytes 0xFF before it included), as libjpeg's
+            // next_marker() finds it.  Whatever follows EOI (MPF secondary images, gain maps,
+            // appended thumbnails) is never part of the scan.
             const size_t e0 = i + seglen;
             size_t e1 = len;
-            for (size_t q = len; q >= e0 + 2; --q)
-                if (buf[q - 2] == 0xFF && buf[q - 1] == 0xD9) { e1 = q - 2; break; }
+            for (size_t q = e0; q + 1 < len; ++q) {
+                if (buf[q] != 0xFF) continue;
+                const uint8_t nx = buf[q + 1];
+                if (nx == 0x00 || (nx >= 0xD0 && nx <= 0xD7)) { ++q; continue; }
+                e1 = q;
+                break;
+            }
             while (e1 > e0 && buf[e1 - 1] == 0xFF) --e1;
             P->ecs = buf + e0;
             P->ecs_len = e1 - e0;
