@@ -387,9 +387,11 @@ def main():
         parity = check_parity(st, dev, focals, margin, args.workload, args.method, args.graph)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "synthetic" \
-            and len(frames) == 18:
-        cpu = cpu_baseline(frames, focals, args.cpu_frames, args.method, h, w)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if args.workload == "synthetic" and args.method == "sift":
+            cpu = cpu_baseline_synthetic(h, w, distinct)
+        elif len(frames) == 18:
+            cpu = cpu_baseline(frames, focals, args.cpu_frames, args.method, h, w)
 
     line = {
         "metric": "Mpixels/s stitched (18-img parrington, SIFT path)" if args.workload == "parrington"
@@ -624,6 +626,39 @@ def cpu_baseline(frames, focals, n, method, h, w):
             "reference_container_note": "the reference's own sift path, single-threaded, "
                                         "re-measured in the build container: 789.35 s for 18 "
                                         "frames (BASELINE.md)"}
+
+
+def cpu_baseline_synthetic(h, w, n_frames_job):
+    """the reference would need ~25 min per 1080p frame and ~50 min of NN
+    loop per pair, so the oracle (bit-exact restatement, tests/test_oracle.py) runs ONE seeded
+    pair -- frames 0 and 1 of the synthetic sequence: cylindrical + SIFT of both frames in two
+    single-threaded processes, then the NN match and RANSAC on one core -- and the job time is
+    that pair's wall time x the job's pairs (the reference computes a pair's two frames for
+    every pair, image_stitching_sift.py:59-60), stated as extrapolated."""
+    import multiprocessing as mp
+    from threadpoolctl import threadpool_limits
+    from oracle import stitch as ostitch
+    from vfx_image_stitching_amd import data
+    frames, focals, _ = data.synthetic_sequence(n_frames=SYNTH_FRAMES, h=h, w=w, start=0, count=2)
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(2, initializer=_warm_worker) as pool:
+        pool.map(_ready, range(2), chunksize=1)
+        t0 = time.perf_counter()
+        feats = pool.map(_oracle_features, [(frames[i], focals[i], "sift") for i in range(2)], chunksize=1)
+        t1 = time.perf_counter()
+        with threadpool_limits(1):
+            (dx, dy), _ = ostitch.pair_shift_sift(*feats[0], *feats[1])
+        el = time.perf_counter() - t0
+    pairs = n_frames_job - 1
+    job_s = el * pairs
+    return {"value": round(n_frames_job * h * w / 1e6 / job_s, 6), "unit": "Mpx/s", "cores": 2,
+            "kind": "port", "extrapolated": True,
+            "sample": f"oracle on ONE seeded pair (config 5 frames 0, 1; {len(feats[0][0])} + "
+                      f"{len(feats[1][0])} keypoints): features of both frames in 2 single-threaded "
+                      f"processes ({t1 - t0:.1f} s), NN match + RANSAC on one core ({el - (t1 - t0):.1f} s); "
+                      f"{el:.1f} s per pair x {pairs} pairs = {job_s:.0f} s extrapolated for the "
+                      f"{n_frames_job}-frame job",
+            "per_pair_s": round(el, 3), "pair_shift": [round(dx, 4), round(dy, 4)]}
 
 
 if __name__ == "__main__":

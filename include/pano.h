@@ -165,6 +165,28 @@ int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int do
  *                        must hold every Gaussian level (pano_sift_pyramid, _pyramid_base or
  *                        _reserve_levels): d_desc [n][cap][128] f32.  A keypoint whose octave
  *                        or layer lies outside the pyramid gets a zero descriptor. */
+/* Per-candidate helpers of find_scale_space_extrema on caller data of ONE octave (the batched
+ * kernels' own device code, for callers of the reference's scalar helpers):
+ *
+ * pano_sift_localize     localize_extremum_via_quadratic_fit(x, y, layer, octave, num_intervals,
+ *                        dog_octave, sigma, contrast_threshold, border, eigen_ratio, max_iter)
+ *                        sift_impl.py:169-211 for n candidates d_cand [n][3] = (x, y, layer) of
+ *                        octave `octave`, whose num_intervals + 2 DoG levels (h x w f32 device
+ *                        planes) are h_dog[] (a host array of device pointers).  d_out [n]: the
+ *                        keypoint (base-image coordinates, angle -1); d_layer [n]: its final
+ *                        layer, -1 when the fit rejects it (the reference's None), -2 when the
+ *                        candidate's 3x3x3 cube leaves the levels.
+ * pano_sift_orient       compute_keypoints_with_orientations(keypoint, octave, gauss_img)
+ *                        sift_impl.py:246-293 for n keypoints d_kps [n] of octave `octave` on its
+ *                        Gaussian level d_gauss (h x w f32): d_out [n][PANO_ORI_MAX_PEAKS], the
+ *                        oriented copies of keypoint i in peak order, d_counts [n] of them. */
+#define PANO_ORI_MAX_PEAKS 18
+int pano_sift_localize(pano_ctx *ctx, const pano_sift_params *params, const float *const *h_dog, int n_dog,
+                       int h, int w, int octave, const int32_t *d_cand, int n, pano_kp *d_out,
+                       int32_t *d_layer);
+int pano_sift_orient(pano_ctx *ctx, const pano_sift_params *params, const float *d_gauss, int h, int w,
+                     int octave, const pano_kp *d_kps, int n, pano_kp *d_out, int32_t *d_counts);
+
 int pano_sift_base(pano_ctx *ctx, const float *d_gray, int n, int h, int w,
                    const pano_sift_params *params, float *d_base);
 int pano_sift_pyramid_base(pano_ctx *ctx, const float *d_base, int n, int H0, int W0, int n_octaves,

@@ -78,11 +78,18 @@ def nn_match_sift(descA, descB, thresh=25000):
     """-> (best index per row, best distance); distances are exact integers here."""
     if len(descA) == 0 or len(descB) == 0:
         return np.full(len(descA), -1, np.int64), np.full(len(descA), np.inf)
-    a = descA.astype(np.float64)
+    # row chunks of 2048 (the whole f64 matrix at 1080p, 25k x 25k, is 5 GB); exact integers in
+    # any chunking
     b = descB.astype(np.float64)
-    d = (a * a).sum(1)[:, None] + (b * b).sum(1)[None, :] - 2 * a @ b.T
-    j = np.argmin(d, axis=1)
-    return j, d[np.arange(len(a)), j]
+    nb = (b * b).sum(1)
+    js, ds = [], []
+    for i0 in range(0, len(descA), 2048):
+        a = descA[i0:i0 + 2048].astype(np.float64)
+        d = (a * a).sum(1)[:, None] + nb[None, :] - 2 * a @ b.T
+        j = np.argmin(d, axis=1)
+        js.append(j)
+        ds.append(d[np.arange(len(a)), j])
+    return np.concatenate(js), np.concatenate(ds)
 
 
 def sift_matches(kpsA, descA, kpsB, descB, thresh=25000):

@@ -24,6 +24,7 @@ PANO_E_OVERFLOW = -3
 PANO_E_NOMATCH = -4
 PANO_E_UNSUPPORTED = -5
 DESC_DIM = 128
+ORI_MAX_PEAKS = 18          # PANO_ORI_MAX_PEAKS
 
 
 class PanoError(RuntimeError):
@@ -113,6 +114,9 @@ SIGNATURES = {
     "pano_sift_dog": (_I, [_P]),
     "pano_sift_extrema": (_I, [_P, ctypes.POINTER(SiftParams), _P, _I, _P]),
     "pano_sift_describe": (_I, [_P, ctypes.POINTER(SiftParams), _P, _P, _I, _P]),
+    "pano_sift_localize": (_I, [_P, ctypes.POINTER(SiftParams), ctypes.POINTER(_P), _I, _I, _I, _I, _P, _I,
+                                _P, _P]),
+    "pano_sift_orient": (_I, [_P, ctypes.POINTER(SiftParams), _P, _I, _I, _I, _P, _I, _P, _P]),
     "pano_sift_level_shape": (_I, [_P, _I, _PI32, _PI32, _PI32]),
     "pano_sift_copy_level": (_I, [_P, _I, _I, _I, _I, _P]),
     "pano_harris": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),

@@ -284,6 +284,33 @@ int pano_sift_describe(pano_ctx *ctx, const pano_sift_params *params, const pano
     return launch_sift_describe(ctx, &p, kps, counts, cap, desc);
 }
 
+int pano_sift_localize(pano_ctx *ctx, const pano_sift_params *params, const float *const *dog, int n_dog, int h,
+                       int w, int octave, const int32_t *cand, int n, pano_kp *out, int32_t *layer) {
+    if (!ctx) return PANO_E_ARG;
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    if (n < 0 || (n > 0 && (!cand || !out || !layer || !dog)))
+        return pano_fail(ctx, PANO_E_ARG, "pano_sift_localize: bad arguments");
+    if (p.num_intervals < 1 || p.num_intervals + 3 > PANO_MAX_LEVELS || n_dog != p.num_intervals + 2)
+        return pano_fail(ctx, PANO_E_ARG, "pano_sift_localize: needs num_intervals + 2 DoG levels");
+    if (octave < 0 || octave >= PANO_MAX_OCTAVES || h < 3 || w < 3 || h > 65535 || w > 65535 || p.border < 1 ||
+        p.max_iter < 1)
+        return pano_fail(ctx, PANO_E_ARG, "pano_sift_localize: bad octave, level shape, border or max_iter");
+    for (int l = 0; l < n_dog && n > 0; ++l)
+        if (!dog[l]) return pano_fail(ctx, PANO_E_ARG, "pano_sift_localize: null DoG level");
+    return launch_sift_localize(ctx, &p, dog, h, w, octave, cand, n, out, layer);
+}
+
+int pano_sift_orient(pano_ctx *ctx, const pano_sift_params *params, const float *gauss, int h, int w, int octave,
+                     const pano_kp *kps, int n, pano_kp *out, int32_t *counts) {
+    if (!ctx) return PANO_E_ARG;
+    pano_sift_params p;
+    if (params) p = *params; else pano_sift_default_params(&p);
+    if (n < 0 || (n > 0 && (!gauss || !kps || !out || !counts)) || h < 1 || w < 1 || octave < 0 || octave > 30)
+        return pano_fail(ctx, PANO_E_ARG, "pano_sift_orient: bad arguments");
+    return launch_sift_orient(ctx, &p, gauss, h, w, octave, kps, n, out, counts);
+}
+
 int pano_sift_level_shape(pano_ctx *ctx, int octave, int *h_out, int *w_out, int *n_octaves) {
     if (!ctx || octave < 0 || octave >= ctx->n_oct) return PANO_E_ARG;
     if (h_out) *h_out = ctx->oct_h[octave];

@@ -208,6 +208,10 @@ int launch_sift_dog(pano_ctx *ctx);
 // reference's scan order, base coordinates: d_raw [n][cap], d_counts [n].
 int launch_sift_extrema(pano_ctx *ctx, const pano_sift_params *p, pano_kp *raw, int cap, int32_t *counts);
 // generate_descriptors for caller keypoints on the resident pyramid: d_desc f32 [n][cap][128].
+int launch_sift_localize(pano_ctx *ctx, const pano_sift_params *p, const float *const *dog, int h, int w,
+                         int octave, const int32_t *cand, int n, pano_kp *out, int32_t *layer_out);
+int launch_sift_orient(pano_ctx *ctx, const pano_sift_params *p, const float *gauss, int h, int w, int octave,
+                       const pano_kp *kps, int n, pano_kp *out, int32_t *counts);
 int launch_sift_describe(pano_ctx *ctx, const pano_sift_params *p, const pano_kp *kps,
                          const int32_t *counts, int cap, float *desc);
 // desc: f32 [n][cap][128] (drop-in form) or, when NULL, desc_u8 [n][cap][128] + norms [n][cap]

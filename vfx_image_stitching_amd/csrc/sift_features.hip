@@ -600,6 +600,122 @@ struct FrameIndex {
     }
 };
 
+// One candidate's orientations (sift_impl.py:246-293) by one wave: the (side+2)^2 neighbourhood
+// of the keypoint staged in LDS (pt), each lane its run of column-major samples into 2^40
+// fixed-point u64 LDS atomics (hs: kOriCopies copies), smoothing and peak interpolation in f64
+// (the reference's).  Returns per lane p < 36 whether bin p is an emitted peak, and its angle.
+// img: the octave's Gaussian level (H x W) the reference passes as gauss_img; kx, ky: the
+// keypoint in base-image coordinates.  Shared by the batched kernel (orientation) and the
+// per-keypoint entry (orient_list, pano_sift_orient).
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H, int W, int o, float kx, float ky,
+                                           float ksize, const OriParams &op,
+                                           unsigned long long (*hs)[PANO_ORI_BINS], double *hd, double *sm,
+                                           float *pt, int lane, double &angle) {
+    for (int i = lane; i < kOriCopies * PANO_ORI_BINS; i += 64) (&hs[0][0])[i] = 0ull;
+    {
+        const float scale = (float)(op.scale_factor * (double)ksize) / (float)(1 << (o + 1));
+        const int radius = (int)rintf((float)op.radius_factor * scale);
+        const float wfac = -0.5f / (scale * scale);
+        const int cy = (int)rintf(ky / (float)(1 << o));
+        const int cx = (int)rintf(kx / (float)(1 << o));
+        const int side = 2 * radius + 1;
+        const int S = side * side;
+        // stage the (side+2)^2 neighbourhood (clamped; out-of-image samples are skipped
+        // below) so each sample's four gradient taps are LDS reads
+        const int P = side + 2;
+        const bool staged = P <= kOriPatch;
+        if (staged) {
+            const int by = cy - radius - 1, bx = cx - radius - 1;
+            for (int e = lane; e < P * P; e += 64) {
+                const int r = e / P, c = e - (e / P) * P;
+                const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
+                pt[r * kOriPatch + c] = img[(size_t)yy * W + xx];
+            }
+        }
+        wave_sync_lds();
+        // lane l walks its own run of Q consecutive column-major samples (neighbouring
+        // lanes are Q samples apart: different bins, fewer same-address LDS atomics)
+        const int Q = (S + 63) / 64;
+        const int j0 = lane * Q;
+        int xi = j0 / side, yi = j0 - (j0 / side) * side;
+        const int jend = min(j0 + Q, S);
+        for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
+            const int dx = xi - radius, dy = yi - radius;
+            const int yy = cy + dy, xx = cx + dx;
+            if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
+            float gx, gy;
+            if (staged) {
+                const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
+                gx = q[1] - q[-1];
+                gy = q[-kOriPatch] - q[kOriPatch];
+            } else {
+                gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
+                gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+            }
+            const float mag = sqrtf(gx * gx + gy * gy);
+#if PANO_ORI_ABL & 1                                  // timing ablation: no atan2f
+            const float ang = fabsf(gy + gx) * 3.0f;
+#else
+            const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+#endif
+#if PANO_ORI_ABL & 2                                  // timing ablation: no expf
+            const float w = wfac * (float)(dx * dx + dy * dy) + 1.0f;
+#else
+            const float w = expf(wfac * (float)(dx * dx + dy * dy));
+#endif
+            // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same
+            // bin as the IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
+            const float a36 = ang * 36.0f;
+            const float q0 = a36 * kInv360;
+            int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
+            bin = bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
+            const double val = (double)(w * mag);
+            atomicAdd(&hs[lane % kOriCopies][bin], rint_fix(val * kHistScale));
+        }
+    }
+    wave_sync_lds();
+    if (lane < PANO_ORI_BINS) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int c = 0; c < kOriCopies; ++c) t += hs[c][lane];
+        hd[lane] = (double)(long long)t * kHistInv;
+    }
+    wave_sync_lds();
+    const int nb = PANO_ORI_BINS;
+    double svl = -1.0;                 // this lane's smoothed bin (histogram values are >= 0)
+    if (lane < nb) {
+        const int b = lane;
+        svl = ((6 * hd[b] + 4 * (hd[(b + nb - 1) % nb] + hd[(b + 1) % nb])) + hd[(b + nb - 2) % nb]) +
+              hd[(b + 2) % nb];
+        svl = svl / 16.0;
+        sm[b] = svl;
+    }
+    double mx = svl;                   // the maximum: exact in any order
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) mx = fmax(mx, __shfl_xor(mx, d));
+    wave_sync_lds();
+    // peaks: lane p < 36 is bin p
+    const int p = lane;
+    bool emit = false;
+    angle = 0.0;
+    if (lane < nb) {
+        const double l = sm[(p + nb - 1) % nb], r = sm[(p + 1) % nb];
+        if (svl > l && svl > r && svl >= op.peak_ratio * mx) {
+            const double interp = np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * svl) + r), (double)nb);
+            angle = 360.0 - interp * 360.0 / nb;
+            if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
+            emit = true;
+        }
+    }
+    return emit;
+}
+
 // One WAVE per candidate, persistent: the grid is the resident workgroups (a grid sized by the
 // candidate capacity dispatched ~37k mostly-empty workgroups at parrington, 410k at 1080p),
 // each XCD takes a contiguous eighth of the candidates and its waves pull them from the XCD's
@@ -629,11 +745,6 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     const int xcd = blockIdx.x & 7;                                   // gridDim.x % 8 == 0
     const int lo_k = (int)((long long)total * xcd / 8), hi_k = (int)((long long)total * (xcd + 1) / 8);
     int32_t *wq = work + xcd * kCntStride;
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
     FrameIndex fi;
     fi.init(cand_cnt, kCntStride, n_frames, cand_cap);
     int claim = 0;
@@ -648,110 +759,12 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         else if (!locate_strided(cand_cnt, n_frames, cand_cap, gk, f, ci)) break;
         f = __builtin_amdgcn_readfirstlane(f);
         ci = __builtin_amdgcn_readfirstlane(ci);
-        for (int i = lane; i < kOriCopies * PANO_ORI_BINS; i += 64) (&hist[wv][0][0])[i] = 0ull;
         const Cand k = cands[(size_t)f * cand_cap + ci];
-        {
-            const int o = k.octave;
-            const int H = pa.H[o], W = pa.W[o];
-            const float *img = pa.gauss[o][k.layer] + (size_t)f * H * W;
-            const float scale = (float)(op.scale_factor * (double)k.size) / (float)(1 << (o + 1));
-            const int radius = (int)rintf((float)op.radius_factor * scale);
-            const float wfac = -0.5f / (scale * scale);
-            const int cy = (int)rintf(k.y / (float)(1 << o));
-            const int cx = (int)rintf(k.x / (float)(1 << o));
-            const int side = 2 * radius + 1;
-            const int S = side * side;
-            // stage the (side+2)^2 neighbourhood (clamped; out-of-image samples are skipped
-            // below) so each sample's four gradient taps are LDS reads
-            const int P = side + 2;
-            const bool staged = P <= kOriPatch;
-            float *pt = patch[wv];
-            if (staged) {
-                const int by = cy - radius - 1, bx = cx - radius - 1;
-                for (int e = lane; e < P * P; e += 64) {
-                    const int r = e / P, c = e - (e / P) * P;
-                    const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
-                    pt[r * kOriPatch + c] = img[(size_t)yy * W + xx];
-                }
-            }
-            wave_sync();
-            // lane l walks its own run of Q consecutive column-major samples (neighbouring
-            // lanes are Q samples apart: different bins, fewer same-address LDS atomics)
-            const int Q = (S + 63) / 64;
-            const int j0 = lane * Q;
-            int xi = j0 / side, yi = j0 - (j0 / side) * side;
-            const int jend = min(j0 + Q, S);
-            for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
-                const int dx = xi - radius, dy = yi - radius;
-                const int yy = cy + dy, xx = cx + dx;
-                if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
-                float gx, gy;
-                if (staged) {
-                    const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
-                    gx = q[1] - q[-1];
-                    gy = q[-kOriPatch] - q[kOriPatch];
-                } else {
-                    gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
-                    gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
-                }
-                const float mag = sqrtf(gx * gx + gy * gy);
-#if PANO_ORI_ABL & 1                                  // timing ablation: no atan2f
-                const float ang = fabsf(gy + gx) * 3.0f;
-#else
-                const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
-#endif
-#if PANO_ORI_ABL & 2                                  // timing ablation: no expf
-                const float w = wfac * (float)(dx * dx + dy * dy) + 1.0f;
-#else
-                const float w = expf(wfac * (float)(dx * dx + dy * dy));
-#endif
-                // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same
-                // bin as the IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
-                const float a36 = ang * 36.0f;
-                const float q0 = a36 * kInv360;
-                int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
-                bin = bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
-                const double val = (double)(w * mag);
-                atomicAdd(&hist[wv][lane % kOriCopies][bin], rint_fix(val * kHistScale));
-            }
-        }
-        wave_sync();
-        if (lane < PANO_ORI_BINS) {
-            unsigned long long t = 0;
-#pragma unroll
-            for (int c = 0; c < kOriCopies; ++c) t += hist[wv][c][lane];
-            hd[wv][lane] = (double)(long long)t * kHistInv;
-        }
-        wave_sync();
-        const int nb = PANO_ORI_BINS;
-        double svl = -1.0;                 // this lane's smoothed bin (histogram values are >= 0)
-        if (lane < nb) {
-            const int b = lane;
-            const double *h = hd[wv];
-            svl = ((6 * h[b] + 4 * (h[(b + nb - 1) % nb] + h[(b + 1) % nb])) + h[(b + nb - 2) % nb]) +
-                  h[(b + 2) % nb];
-            svl = svl / 16.0;
-            sm[wv][b] = svl;
-        }
-        double mx = svl;                   // the maximum: exact in any order
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) mx = fmax(mx, __shfl_xor(mx, d));
-        wave_sync();
-        // peaks -> keypoints; one (wave-aggregated) append per candidate
+        double angle;
         const int p = lane;
-        bool emit = false;
-        double angle = 0.0;
-        if (lane < nb) {
-            const double *sv = sm[wv];
-            const double l = sv[(p + nb - 1) % nb], r = sv[(p + 1) % nb];
-            if (svl > l && svl > r && svl >= op.peak_ratio * mx) {
-                const double interp =
-                    np_remainder((double)p + 0.5 * (l - r) / ((l - 2 * svl) + r), (double)nb);
-                angle = 360.0 - interp * 360.0 / nb;
-                if (fabs(angle - 360.0) < 1e-7) angle = 0.0;
-                emit = true;
-            }
-        }
+        const bool emit = orient_one(pa.gauss[k.octave][k.layer] + (size_t)f * pa.H[k.octave] * pa.W[k.octave],
+                                     pa.H[k.octave], pa.W[k.octave], k.octave, k.x, k.y, k.size, op, hist[wv],
+                                     hd[wv], sm[wv], patch[wv], lane, angle);
         const unsigned long long m = __ballot(emit);
         if (m) {
             int base = 0;
@@ -771,7 +784,74 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
                 if (slot < raw_cap) raw[(size_t)f * raw_cap + slot] = q;
             }
         }
-        wave_sync();                       // hist / hd / sm / patch reused by the next candidate
+        wave_sync_lds();                   // hist / hd / sm / patch reused by the next candidate
+    }
+}
+
+// ------------------------------------------------------------------ S6 / S7 per caller candidate
+// The reference's per-candidate helpers (localize_extremum_via_quadratic_fit :169-211,
+// compute_keypoints_with_orientations :246-293) on caller-given candidates of ONE octave, through
+// the batched kernels' own device functions (localize_one, orient_one): pano_sift_localize /
+// pano_sift_orient.
+//
+// localize_list, thread per candidate (x, y, layer) of octave a.octave's DoG levels: out[i] is the
+// keypoint (angle -1, cv2.KeyPoint's default) and layer_out[i] its final layer, or -1 when the
+// fit rejects it; a candidate whose 3x3x3 cube leaves the levels is refused (-2) before any read.
+__global__ void __launch_bounds__(256)
+localize_list(DogArgs a, LocParams lp, int o, const int32_t *__restrict__ cand, int n,
+              pano_kp *__restrict__ out, int32_t *__restrict__ layer_out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int x = cand[3 * i], y = cand[3 * i + 1], layer = cand[3 * i + 2];
+    if (x < 1 || y < 1 || x > a.W[o] - 2 || y > a.H[o] - 2 || layer < 1 || layer > lp.ni) {
+        layer_out[i] = -2;
+        return;
+    }
+    Cand k;
+    const bool keep = localize_one(a, lp, scan_key(o, layer, y, x), 0, k);
+    layer_out[i] = keep ? (int32_t)k.layer : -1;
+    pano_kp q;
+    q.x = keep ? k.x : 0.0f;
+    q.y = keep ? k.y : 0.0f;
+    q.size = keep ? k.size : 0.0f;
+    q.angle = -1.0f;
+    q.response = keep ? k.response : 0.0f;
+    q.octave = keep ? k.octave_field : 0;
+    out[i] = q;
+}
+
+// orient_list, wave per caller keypoint (base-image coordinates, the octave's Gaussian level
+// img): out[i][0 .. counts[i]) are the oriented copies in peak order, as the reference appends
+// them (at most PANO_ORI_MAX_PEAKS: a peak exceeds both neighbours); counts[i] = -1 refuses a
+// keypoint with a non-finite position or a window radius above 1024 px.
+__global__ void __launch_bounds__(256)
+orient_list(const float *__restrict__ img, int H, int W, int o, OriParams op, const pano_kp *__restrict__ kps,
+            int n, pano_kp *__restrict__ out, int32_t *__restrict__ counts) {
+    __shared__ unsigned long long hist[4][kOriCopies][PANO_ORI_BINS];
+    __shared__ double hd[4][PANO_ORI_BINS];
+    __shared__ double sm[4][PANO_ORI_BINS];
+    __shared__ float patch[4][kOriPatch * kOriPatch];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = blockIdx.x * 4 + wv; i < n; i += gridDim.x * 4) {      // wave-uniform
+        const pano_kp k = kps[i];
+        // a caller keypoint whose window would be absurd (radius > 1024 px, non-finite fields)
+        // is refused (count -1) instead of walking it
+        const float rr = (float)op.radius_factor * ((float)(op.scale_factor * (double)k.size) / (float)(1 << (o + 1)));
+        if (!(rr >= 0.0f && rr <= 1024.0f) || !isfinite(k.x) || !isfinite(k.y)) {
+            if (lane == 0) counts[i] = -1;
+            continue;
+        }
+        double angle;
+        const bool emit = orient_one(img, H, W, o, k.x, k.y, k.size, op, hist[wv], hd[wv], sm[wv], patch[wv],
+                                     lane, angle);
+        const unsigned long long m = __ballot(emit);
+        if (emit) {
+            pano_kp q = k;
+            q.angle = (float)angle;
+            out[(size_t)i * PANO_ORI_MAX_PEAKS + __popcll(m & ((1ull << lane) - 1))] = q;
+        }
+        if (lane == 0) counts[i] = __popcll(m);
+        wave_sync_lds();
     }
 }
 
@@ -1899,3 +1979,44 @@ int launch_sift_describe(pano_ctx *ctx, const pano_sift_params *p, const pano_kp
 }
 
 int sift_set_attributes(pano_ctx *) { return PANO_OK; }
+
+// pano_sift_localize / pano_sift_orient (argument checks in pano_abi.cpp)
+int launch_sift_localize(pano_ctx *ctx, const pano_sift_params *p, const float *const *dog, int h, int w,
+                         int octave, const int32_t *cand, int n, pano_kp *out, int32_t *layer_out) {
+    if (n <= 0) return PANO_OK;
+    LocParams lp;
+    const int ni = p->num_intervals;
+    lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);
+    lp.contrast = (float)p->contrast_threshold;
+    lp.edge_lhs = (float)p->eigen_ratio;
+    lp.edge_rhs = (float)((p->eigen_ratio + 1) * (p->eigen_ratio + 1));
+    lp.sigma_f = (float)p->sigma;
+    lp.ni = ni;
+    lp.border = p->border;
+    lp.max_iter = p->max_iter;
+    lp.octave = octave;
+    DogArgs da{};
+    da.n_oct = octave + 1;
+    da.H[octave] = h;
+    da.W[octave] = w;
+    for (int l = 0; l < ni + 2; ++l) da.dog[octave][l] = dog[l];
+    {
+        PanoProf prof_(ctx, PK_EXTREMA);
+        localize_list<<<(n + 255) / 256, 256, 0, ctx->stream>>>(da, lp, octave, cand, n, out, layer_out);
+    }
+    PANO_LAUNCH_CHECK(ctx, "localize_list");
+    return PANO_OK;
+}
+
+int launch_sift_orient(pano_ctx *ctx, const pano_sift_params *p, const float *gauss, int h, int w, int octave,
+                       const pano_kp *kps, int n, pano_kp *out, int32_t *counts) {
+    if (n <= 0) return PANO_OK;
+    OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio};
+    const unsigned blocks = (unsigned)std::min(4096, (n + 3) / 4);
+    {
+        PanoProf prof_(ctx, PK_ORIENT);
+        orient_list<<<blocks, 256, 0, ctx->stream>>>(gauss, h, w, octave, op, kps, n, out, counts);
+    }
+    PANO_LAUNCH_CHECK(ctx, "orient_list");
+    return PANO_OK;
+}

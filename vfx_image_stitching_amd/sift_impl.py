@@ -316,114 +316,153 @@ def generate_descriptors(keypoints, gaussian_images, window_width=4, num_bins=8,
     return desc[0].cpu().numpy()
 
 
-# ------------------------------------------------------------------ per-pixel helpers
-# The reference's scalar helpers (one pixel / one keypoint at a time).  libpano evaluates the
-# same definitions batched inside find_scale_space_extrema; these host versions keep the
-# reference's per-call API for callers that use them directly.
+# ------------------------------------------------------------------ per-candidate helpers
+# find_scale_space_extrema's building blocks (sift_impl.py:143-293).  The two that do real work
+# -- the quadratic-fit localisation and the orientation histogram -- run on the GPU through
+# pano_sift_localize / pano_sift_orient, i.e. the batched kernels' own device code
+# (localize_one, orient_one in sift_features.hip); they also take whole candidate lists
+# (localize_extrema, orient_keypoints), which is how a caller should use them.  The 3 x 3 x 3
+# predicates are written in the separable / stencil form the extrema kernel evaluates.
+_AXES_XYS = (2, 1, 0)          # cube axes of the reference's derivative order (x, y, scale)
+
+
+def _nb(cube, **shift):
+    """The cube value at the centre (1, 1, 1) moved by shift {axis: +-1}."""
+    at = [1, 1, 1]
+    for ax, d in shift.items():
+        at[int(ax[1:])] += d
+    return cube[tuple(at)]
+
+
 def is_pixel_an_extremum(prev_patch, curr_patch, next_patch, threshold):
-    """sift_impl.py:143-163: v >= (<=) all 26 neighbours, |v| > threshold."""
-    val = curr_patch[1, 1]
-    if abs(val) <= threshold:
+    """sift_impl.py:143-163.  The centre belongs to its own 3 x 3 x 3 cube, so "v >= every one
+    of the 26 neighbours" is v == max(cube) (and "<=" is v == min(cube)): the form
+    extrema_stream / extrema_scan evaluate.  NaN anywhere fails both, as in the reference."""
+    cube = np.stack((np.asarray(prev_patch), np.asarray(curr_patch), np.asarray(next_patch)))
+    v = cube[1, 1, 1]
+    if not abs(v) > threshold:
         return False
-    cube = np.stack([np.asarray(prev_patch), np.asarray(curr_patch), np.asarray(next_patch)])
-    return bool(np.all(val >= cube)) if val > 0 else bool(np.all(val <= cube))
+    return bool(v == (cube.max() if v > 0 else cube.min()))
 
 
 def compute_gradient_at_center_pixel(cube):
-    """sift_impl.py:217-224: central differences (dx, dy, ds)."""
-    return np.array([0.5 * (cube[1, 1, 2] - cube[1, 1, 0]),
-                     0.5 * (cube[1, 2, 1] - cube[1, 0, 1]),
-                     0.5 * (cube[2, 1, 1] - cube[0, 1, 1])])
+    """sift_impl.py:217-224: half the difference of the centre's +1 / -1 neighbours along x, y
+    and scale."""
+    c = np.asarray(cube)
+    return np.array([0.5 * (_nb(c, **{f"a{ax}": 1}) - _nb(c, **{f"a{ax}": -1})) for ax in _AXES_XYS])
 
 
 def compute_hessian_at_center_pixel(cube):
-    """sift_impl.py:227-240: the 3 x 3 Hessian by central differences."""
-    v = cube[1, 1, 1]
-    dxx = cube[1, 1, 2] - 2 * v + cube[1, 1, 0]
-    dyy = cube[1, 2, 1] - 2 * v + cube[1, 0, 1]
-    dss = cube[2, 1, 1] - 2 * v + cube[0, 1, 1]
-    dxy = 0.25 * (cube[1, 2, 2] - cube[1, 2, 0] - cube[1, 0, 2] + cube[1, 0, 0])
-    dxs = 0.25 * (cube[2, 1, 2] - cube[2, 1, 0] - cube[0, 1, 2] + cube[0, 1, 0])
-    dys = 0.25 * (cube[2, 2, 1] - cube[2, 0, 1] - cube[0, 2, 1] + cube[0, 0, 1])
-    return np.array([[dxx, dxy, dxs], [dxy, dyy, dys], [dxs, dys, dss]])
+    """sift_impl.py:227-240: the (x, y, scale) Hessian of the cube.  Diagonal: (v+ - 2v) + v-;
+    mixed terms: ((v++ - v+-) - v-+) + v--, over (slower axis, faster axis), times 1/4."""
+    c = np.asarray(cube)
+    v = c[1, 1, 1]
+
+    def d2(i, j):
+        a, b = _AXES_XYS[i], _AXES_XYS[j]
+        if a == b:
+            return (_nb(c, **{f"a{a}": 1}) - 2 * v) + _nb(c, **{f"a{a}": -1})
+        s, f = f"a{min(a, b)}", f"a{max(a, b)}"
+        return 0.25 * (((_nb(c, **{s: 1, f: 1}) - _nb(c, **{s: 1, f: -1})) - _nb(c, **{s: -1, f: 1}))
+                       + _nb(c, **{s: -1, f: -1}))
+
+    return np.array([[d2(i, j) for j in range(3)] for i in range(3)])
+
+
+def _dog_planes(dog_octave, num_intervals):
+    """The octave's DoG levels as device tensors (ni + 2 planes of one shape)."""
+    _, torch, dev = _dev()
+    levels = [_f32_2d(d, "dog_octave") for d in dog_octave]
+    if len(levels) != int(num_intervals) + 2:
+        raise ValueError(f"dog_octave: {len(levels)} levels for num_intervals={num_intervals} "
+                         f"(expected {int(num_intervals) + 2})")
+    shape = levels[0].shape
+    if any(l.shape != shape for l in levels):
+        raise ValueError("dog_octave: levels of different shapes")
+    return [torch.from_numpy(l).to(dev) for l in levels], shape
+
+
+def localize_extrema(candidates, octave, num_intervals, dog_octave, sigma, contrast_threshold, border,
+                     eigen_ratio=10, max_iter=5):
+    """localize_extremum_via_quadratic_fit for every (x, y, layer) of ``candidates`` (one
+    octave) in one launch (pano_sift_localize): a list with, per candidate, (KeyPoint, layer)
+    or None."""
+    import ctypes
+    cand = np.ascontiguousarray(np.asarray(candidates, dtype=np.int64).reshape(-1, 3))
+    n = len(cand)
+    if n == 0:
+        return []
+    if cand.min() < -(1 << 31) or cand.max() >= (1 << 31):
+        raise IndexError("candidate coordinates out of range")
+    ctx, torch, dev = _dev()
+    planes, (h, w) = _dog_planes(dog_octave, num_intervals)
+    ptrs = (ctypes.c_void_p * len(planes))(*[t.data_ptr() for t in planes])
+    c_dev = torch.from_numpy(cand.astype(np.int32)).to(dev)
+    out = torch.empty((n, 6), dtype=torch.int32, device=dev)
+    layer = torch.empty((n,), dtype=torch.int32, device=dev)
+    p = _lib.default_sift_params(sigma=float(sigma), num_intervals=int(num_intervals), border=int(border),
+                                 contrast_threshold=float(contrast_threshold),
+                                 eigen_ratio=float(eigen_ratio), max_iter=int(max_iter))
+    ctx.check(ctx.lib.pano_sift_localize(ctx.h, ctypes.byref(p), ptrs, len(planes), h, w, int(octave),
+                                         _lib.ptr(c_dev), n, _lib.ptr(out), _lib.ptr(layer)))
+    rec = out.cpu().numpy().view(_lib.KP_NP).reshape(-1)
+    lay = layer.cpu().numpy()
+    if (lay == -2).any():
+        i = int(np.argmax(lay == -2))
+        raise IndexError(f"candidate {i} {tuple(cand[i])}: its 3x3x3 cube leaves the DoG levels")
+    return [None if l < 0 else (KeyPoint(float(r["x"]), float(r["y"]), float(r["size"]), -1.0,
+                                         float(r["response"]), int(r["octave"])), int(l))
+            for r, l in zip(rec, lay)]
 
 
 def localize_extremum_via_quadratic_fit(x, y, layer, octave, num_intervals, dog_octave, sigma,
                                         contrast_threshold, border, eigen_ratio=10, max_iter=5):
-    """sift_impl.py:169-211 for one extremum: <= max_iter Newton steps on the 3x3x3 cube / 255
-    (np.linalg.lstsq), contrast and edge tests; (KeyPoint, layer) or None.  Keeps the
-    reference's quirk of using the last cube after max_iter non-converged steps."""
-    shape = np.asarray(dog_octave[0]).shape
-    for _ in range(max_iter):
-        prev, curr, nxt = dog_octave[layer - 1:layer + 2]
-        cube = np.stack([prev[y - 1:y + 2, x - 1:x + 2], curr[y - 1:y + 2, x - 1:x + 2],
-                         nxt[y - 1:y + 2, x - 1:x + 2]]).astype("float32") / 255.
-        grad = compute_gradient_at_center_pixel(cube)
-        hess = compute_hessian_at_center_pixel(cube)
-        update = -np.linalg.lstsq(hess, grad, rcond=None)[0]
-        if np.all(np.abs(update) < 0.5):
-            break
-        x += int(np.round(update[0]))
-        y += int(np.round(update[1]))
-        layer += int(np.round(update[2]))
-        if y < border or y >= shape[0] - border or x < border or x >= shape[1] - border \
-                or layer < 1 or layer > num_intervals:
-            return None
-    val = cube[1, 1, 1] + 0.5 * np.dot(grad, update)
-    if abs(val) * num_intervals < contrast_threshold:
-        return None
-    h2 = hess[:2, :2]
-    tr = np.trace(h2)
-    d = np.linalg.det(h2)
-    if d <= 0 or eigen_ratio * (tr ** 2) >= ((eigen_ratio + 1) ** 2) * d:
-        return None
-    kp = KeyPoint()
-    kp.pt = ((x + update[0]) * (2 ** octave), (y + update[1]) * (2 ** octave))
-    kp.octave = octave + layer * (2 ** 8) + int(np.round((update[2] + 0.5) * 255)) * (2 ** 16)
-    kp.size = sigma * (2 ** ((layer + update[2]) / np.float32(num_intervals))) * (2 ** (octave + 1))
-    kp.response = abs(val)
-    return kp, layer
+    """sift_impl.py:169-211 for one extremum on the GPU (pano_sift_localize): at most max_iter
+    Newton steps on the 3x3x3 cube / 255, the contrast and edge tests; (KeyPoint, layer) or
+    None, the reference's max_iter quirk included."""
+    return localize_extrema([(x, y, layer)], octave, num_intervals, dog_octave, sigma, contrast_threshold,
+                            border, eigen_ratio, max_iter)[0]
+
+
+def orient_keypoints(keypoints, octave, gauss_img, radius_factor=3, num_bins=36, peak_ratio=0.8,
+                     scale_factor=1.5):
+    """compute_keypoints_with_orientations for every keypoint of one octave in one launch
+    (pano_sift_orient): a list of lists of oriented KeyPoints, peak order."""
+    import ctypes
+    if num_bins != 36:
+        raise NotImplementedError("libpano's orientation histogram has the reference's 36 bins")
+    kps = list(keypoints)
+    if not kps:
+        return []
+    img = _f32_2d(gauss_img, "gauss_img")
+    ctx, torch, dev = _dev()
+    rec = np.zeros(len(kps), _lib.KP_NP)
+    for i, kp in enumerate(kps):
+        rec[i] = (kp.pt[0], kp.pt[1], kp.size, kp.angle, kp.response, kp.octave)
+    n = len(kps)
+    g = torch.from_numpy(img).to(dev)
+    k_dev = torch.from_numpy(rec.view(np.int32).reshape(n, 6).copy()).to(dev)
+    out = torch.empty((n, _lib.ORI_MAX_PEAKS, 6), dtype=torch.int32, device=dev)
+    counts = torch.empty((n,), dtype=torch.int32, device=dev)
+    p = _lib.default_sift_params(radius_factor=float(radius_factor), peak_ratio=float(peak_ratio),
+                                 scale_factor=float(scale_factor))
+    ctx.check(ctx.lib.pano_sift_orient(ctx.h, ctypes.byref(p), _lib.ptr(g), img.shape[0], img.shape[1],
+                                       int(octave), _lib.ptr(k_dev), n, _lib.ptr(out), _lib.ptr(counts)))
+    o = out.cpu().numpy().view(_lib.KP_NP).reshape(n, _lib.ORI_MAX_PEAKS)
+    c = counts.cpu().numpy()
+    if (c < 0).any():
+        i = int(np.argmax(c < 0))
+        raise ValueError(f"keypoint {i}: non-finite position or an orientation window above 1024 px")
+    return [[KeyPoint(*kps[i].pt, kps[i].size, float(r["angle"]), kps[i].response, kps[i].octave)
+             for r in o[i, :c[i]]] for i in range(n)]
 
 
 def compute_keypoints_with_orientations(keypoint, octave, gauss_img, radius_factor=3, num_bins=36,
                                         peak_ratio=0.8, scale_factor=1.5):
-    """sift_impl.py:246-293 for one keypoint: the 36-bin weighted gradient-orientation
-    histogram, [1 4 6 4 1]/16 smoothing, peaks >= peak_ratio * max with parabolic
-    interpolation; one KeyPoint per peak."""
-    gauss_img = np.asarray(gauss_img)
-    scale = scale_factor * keypoint.size / np.float32(2 ** (octave + 1))
-    radius = int(np.round(radius_factor * scale))
-    weight_fac = -0.5 / (scale ** 2)
-    cy = int(np.round(keypoint.pt[1] / np.float32(2 ** octave)))
-    cx = int(np.round(keypoint.pt[0] / np.float32(2 ** octave)))
-    dy, dx = np.mgrid[-radius:radius + 1, -radius:radius + 1]
-    dy, dx = dy.ravel(), dx.ravel()                # the reference's dy-outer, dx-inner order
-    yy, xx = cy + dy, cx + dx
-    ok = (xx > 0) & (xx < gauss_img.shape[1] - 1) & (yy > 0) & (yy < gauss_img.shape[0] - 1)
-    raw_hist = np.zeros(num_bins)
-    for ddy, ddx, y, x in zip(dy[ok].tolist(), dx[ok].tolist(), yy[ok].tolist(), xx[ok].tolist()):
-        gx = gauss_img[y, x + 1] - gauss_img[y, x - 1]
-        gy = gauss_img[y - 1, x] - gauss_img[y + 1, x]
-        mag = np.sqrt(gx * gx + gy * gy)
-        ang = np.rad2deg(np.arctan2(gy, gx)) % 360
-        w = np.exp(weight_fac * (ddx * ddx + ddy * ddy))
-        raw_hist[int(np.round(ang * num_bins / 360.)) % num_bins] += w * mag
-    smooth = np.zeros(num_bins)
-    for i in range(num_bins):
-        smooth[i] = (6 * raw_hist[i] + 4 * (raw_hist[i - 1] + raw_hist[(i + 1) % num_bins]) +
-                     raw_hist[i - 2] + raw_hist[(i + 2) % num_bins]) / 16.
-    maxv = np.max(smooth)
-    peaks = np.where(np.logical_and(smooth > np.roll(smooth, 1), smooth > np.roll(smooth, -1)))[0]
-    out = []
-    for p in peaks:
-        if smooth[p] >= peak_ratio * maxv:
-            left, right = smooth[(p - 1) % num_bins], smooth[(p + 1) % num_bins]
-            interp = (p + 0.5 * (left - right) / (left - 2 * smooth[p] + right)) % num_bins
-            angle = 360. - interp * 360. / num_bins
-            if abs(angle - 360.) < float_tolerance:
-                angle = 0
-            out.append(KeyPoint(*keypoint.pt, keypoint.size, angle, keypoint.response, keypoint.octave))
-    return out
+    """sift_impl.py:246-293 for one keypoint on the GPU (pano_sift_orient): one KeyPoint per
+    orientation-histogram peak >= peak_ratio * max, parabolically interpolated."""
+    return orient_keypoints([keypoint], octave, gauss_img, radius_factor, num_bins, peak_ratio,
+                            scale_factor)[0]
 
 
 __all__ = ["KeyPoint", "compute_keypoints_and_descriptors", "compute_number_of_octaves",
@@ -432,4 +471,5 @@ __all__ = ["KeyPoint", "compute_keypoints_and_descriptors", "compute_number_of_o
            "generate_gaussian_images", "generate_DoG_images", "find_scale_space_extrema",
            "is_pixel_an_extremum", "localize_extremum_via_quadratic_fit",
            "compute_gradient_at_center_pixel", "compute_hessian_at_center_pixel",
-           "compute_keypoints_with_orientations", "generate_descriptors"]
+           "compute_keypoints_with_orientations", "generate_descriptors", "localize_extrema",
+           "orient_keypoints"]
