@@ -193,3 +193,116 @@ def test_gloo_world2_gather_plan_bands_bbox(gold_json, which):
         if which == "synthetic_strong":
             assert W >= 143 * 1229                       # the full 144-frame canvas
     assert out[0][1:] == out[1][1:]                      # identical replay on every rank
+
+
+# ------------------------------------------------- panorama assembly at N > 1 (gloo, world 2)
+def _assemble_worker(rank, world, port, q):
+    """Each rank holds only its own band of the parrington canvas (the oracle's fold of the
+    reference's golden shifts, cut at the rank's owned columns), exchanges the layout, sends its
+    band to rank 0, and rank 0 crops: the panorama must be the reference's, byte for byte."""
+    import torch
+    import torch.distributed as dist
+    from conftest import digest, load_json
+    from oracle import stitch as ostitch
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import data
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        gold = load_json("sift_parrington.json")
+        names, frames, focals, margin = data.load_set("parrington")
+        shifts = [tuple(s["move"]) for s in gold["shifts"]]
+        pairs = [tuple(tuple(p) for p in s["pair"]) for s in gold["shifts"]]
+        h, w = frames.shape[1:3]
+        steps, first, (H, W) = D.global_plan(drift_correct(shifts), pairs, len(frames), h, w)
+        s0, c = D.shard_ranges(len(shifts), world)[rank]
+        _, _, _, _, (lo, hi) = D.band_plan(steps, first, w, H, s0, c, len(frames))
+        # this rank's band: the oracle's canvas at the owned columns (the rest is discarded)
+        cyl = [ostitch.cylindrical(f, fl) for f, fl in zip(frames, focals)]
+        mosaic = ostitch.compose(cyl, ostitch.drift_correct(shifts), pairs)
+        assert mosaic.shape[:2] == (H, W)
+        band = torch.from_numpy(np.ascontiguousarray(mosaic[:, lo:hi]))
+        del mosaic
+        ys, xs = np.nonzero(bgr_to_gray_u8(band.numpy()) > 0)
+        box = (int(ys.min()), int(ys.max()), int(xs.min()) + lo, int(xs.max()) + lo) if ys.size else D.NO_BOX
+        layout = D.exchange_layout(box, (lo, hi), False)
+        canvas = D.assemble_bands(band, layout, (H, W))
+        if rank == 0:
+            y0, y1, x0, x1 = D.crop_box(D.layout_box(layout), H, W, margin)
+            pano = canvas[y0:y1 + 1, x0:x1 + 1].numpy()
+            q.put((rank, digest(pano), gold["pano_digest"], layout.tolist()))
+        else:
+            assert canvas is None
+            q.put((rank, None, None, layout.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_assembles_the_parrington_panorama():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_assemble_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][1] == out[0][2], "assembled panorama differs from the reference's"
+    assert out[0][3] == out[1][3]                               # every rank sees the same layout
+    (l0, h0), (l1, h1) = sorted((r[4], r[5]) for r in out[0][3])   # the bands tile [0, W)
+    assert l0 == 0 and h0 == l1 and h1 > h0
+
+
+class _RootStitcher:
+    """Stands in for Stitcher on rank 0 of the fallback: records what _finish received."""
+
+    def _finish(self, cyl, colnz, recs, margin, graph, t, t0):
+        return (cyl.clone(), colnz.clone(), len(recs), margin)
+
+
+def _fold_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n_frames = 8
+        counts = [c for _, c in D.shard_ranges(n_frames - 1, world)]
+        s0 = sum(counts[:rank])
+        # frame f is filled with the value f: the root must receive 0 .. n_frames - 1 in order
+        fr = torch.arange(s0, s0 + counts[rank] + 1, dtype=torch.uint8)
+        cyl = fr[:, None, None, None].expand(-1, 4, 5, 3).contiguous()
+        colnz = fr[:, None].expand(-1, 5).contiguous()
+        recs = np.zeros(n_frames - 1, _lib.PAIR_NP)
+        layout = D.exchange_layout(D.NO_BOX, (0, 0), rank == 1)      # rank 1's band refused
+        assert layout[:, 6].tolist() == [0, 1, 0][:world]
+        res = D.fold_on_root(_RootStitcher(), cyl, colnz, recs, counts, 15)
+        q.put((rank, None if res is None else (res[0][:, 0, 0, 0].tolist(), res[1][:, 0].tolist(),
+                                               res[2], res[3])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_fallback_gathers_frames_to_root():
+    """A refused band at world > 1: the layout exchange tells every rank, and the frames go to
+    rank 0 in sequence order (each rank's first frame is its predecessor's last) for the
+    sequential fold."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fold_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[1][1] is None and out[2][1] is None
+    frames, colnz, nrec, margin = out[0][1]
+    assert frames == list(range(8)) and colnz == list(range(8)) and nrec == 7 and margin == 15

@@ -11,7 +11,13 @@ SURVEY.md section 8(e): pairs are independent until drift correction / compositi
      Bands are independent when no column is covered by three frames (frame i never
      reaches frame i-2: true whenever |dx| > w/2, e.g. parrington / grail / synthetic);
      otherwise band compositing is refused (``BandError``).
-  4. rectangle_crop needs the global bounding box: a 4-int all_reduce (min/max).
+  4. rectangle_crop needs the global bounding box, and rank 0 needs every band's place: ONE
+     all_gather of 8 int64 per rank (box, owned columns, fallback flag);
+  5. the owned bands go to rank 0 point to point (RCCL send / recv over xGMI), which places
+     them into the final canvas and crops it: the panorama exists on rank 0 at the end of
+     every step, as on one GPU.  If any rank's band is refused (a column covered by three
+     frames, a band above its capacity), every rank sees it in the layout exchange and the
+     frames go to rank 0 instead, which runs the sequential fold (the reference's blend order).
 
 The host logic here is device-agnostic so it is unit-tested with gloo on the CPU; the
 GPU work is the libpano calls of pipeline.Stitcher.
@@ -353,6 +359,115 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
     return recs, view, own_lo, (H, W), box
 
 
+LAYOUT_INTS = 8                # per rank: ymin ymax xmin xmax own_lo own_hi fallback 0
+
+
+def _root(group):
+    import torch.distributed as dist
+    return dist.get_global_rank(group, 0) if group is not None else 0
+
+
+def exchange_layout(box, own, fallback, group=None, device=None):
+    """The layout collective of a sharded step: all_gather of LAYOUT_INTS int64 per rank --
+    this rank's crop box (ymin, ymax, xmin, xmax in global columns, NO_BOX when its band has no
+    pixel above the threshold), its owned columns [lo, hi) and whether its band was refused.
+    Returns the int64 [world, LAYOUT_INTS] numpy table every rank then reads."""
+    import torch
+    import torch.distributed as dist
+    row = torch.tensor([[*box, own[0], own[1], int(bool(fallback)), 0]], dtype=torch.int64, device=device)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return row.cpu().numpy()
+    out = torch.empty((world, LAYOUT_INTS), dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(out, row, group=group)
+    return out.cpu().numpy()
+
+
+def layout_box(layout):
+    """The global crop box from the layout table: min / max over the ranks' boxes."""
+    return (int(layout[:, 0].min()), int(layout[:, 1].max()), int(layout[:, 2].min()), int(layout[:, 3].max()))
+
+
+def assemble_bands(owned, layout, canvas_hw, group=None, out=None):
+    """The owned bands of every rank into rank 0's [H, W, 3] canvas: each rank != 0 sends its
+    contiguous band to rank 0 (P2P; RCCL over xGMI on device tensors, gloo on CPU ones), rank 0
+    receives them all in one batch and places them at their owned columns.  Returns the canvas
+    on rank 0 and None elsewhere.  owned: this rank's [H, own_hi - own_lo, 3] uint8 band."""
+    import torch
+    import torch.distributed as dist
+    H, W = canvas_hw
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    root = _root(group) if world > 1 else 0
+    if rank != 0:
+        if owned.numel():
+            for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, owned.contiguous(), root, group)]):
+                q.wait()
+        return None
+    canvas = out if out is not None else torch.empty((H, W, 3), dtype=torch.uint8, device=owned.device)
+    lo0, hi0 = int(layout[0, 4]), int(layout[0, 5])
+    canvas[:, lo0:hi0].copy_(owned)
+    ops, tmps = [], []
+    for r in range(1, world):
+        lo, hi = int(layout[r, 4]), int(layout[r, 5])
+        if hi <= lo:
+            continue
+        t = torch.empty((H, hi - lo, 3), dtype=torch.uint8, device=owned.device)
+        src = dist.get_global_rank(group, r) if group is not None else r
+        ops.append(dist.P2POp(dist.irecv, t, src, group))
+        tmps.append((lo, hi, t))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    for lo, hi, t in tmps:
+        canvas[:, lo:hi].copy_(t)
+    return canvas
+
+
+def crop_box(box, H, W, margin):
+    """rectangle_crop's rows / columns (image_stitching_sift.py:208-247) from a global box."""
+    if box[1] < 0:
+        return 0, H - 1, 0, W - 1
+    return max(0, box[0] + margin), min(H - 1, box[1] - margin), box[2], box[3]
+
+
+def fold_on_root(stitcher, cyl, colnz, recs, pair_counts, margin=15, group=None):
+    """The fallback of a sharded step whose bands are not independent: every rank sends its
+    cylindrical frames (all but its first, which the previous rank holds) to rank 0, which
+    composites the whole sequence with the host plan (the sequential fold where three frames
+    cover a column, exactly like Stitcher.run's own fallback).  Returns the StitchResult on
+    rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    st = stitcher
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if rank != 0:
+        if cyl.shape[0] > 1:
+            ops = [dist.P2POp(dist.isend, cyl[1:].contiguous(), _root(group), group),
+                   dist.P2POp(dist.isend, colnz[1:].contiguous(), _root(group), group)]
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        return None
+    parts_c, parts_z, ops = [cyl], [colnz], []
+    for r in range(1, world):
+        c = int(pair_counts[r])
+        if c == 0:
+            continue
+        tc = torch.empty((c,) + tuple(cyl.shape[1:]), dtype=cyl.dtype, device=cyl.device)
+        tz = torch.empty((c,) + tuple(colnz.shape[1:]), dtype=colnz.dtype, device=colnz.device)
+        src = dist.get_global_rank(group, r) if group is not None else r
+        ops += [dist.P2POp(dist.irecv, tc, src, group), dist.P2POp(dist.irecv, tz, src, group)]
+        parts_c.append(tc)
+        parts_z.append(tz)
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    cyl_all = torch.cat(parts_c).contiguous()
+    colnz_all = torch.cat(parts_z).contiguous()
+    return st._finish(cyl_all, colnz_all, recs, margin, False, {}, time.perf_counter())
+
+
 def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, margin=15,
              graph=False):
     """One rank's share of a sharded stitch (frames_dev = its pair range + boundary frame):
@@ -361,7 +476,9 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
     all_reduce.  At world 1 it is Stitcher.run's device-planned stitch over the whole canvas.
 
     Returns dict(records=global PAIR_NP, band=device canvas of the owned band,
-    bbox=global crop box, x_offset=band's first column in the final canvas)."""
+    bbox=global crop box (y0, y1, x0, x1), x_offset=band's first column in the final canvas,
+    canvas_hw, and on rank 0 panorama / canvas: the cropped panorama and the whole canvas,
+    assembled from every rank's band (None on the other ranks))."""
     import torch
     import torch.distributed as dist
     st = stitcher
@@ -374,18 +491,38 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
     try:
         recs, owned, own_lo, (H, W), box = rank_band(st, cyl, colnz, gathered, pair_counts,
                                                      pair_start, margin, graph)
+        refused = None
     except BandError as e:
-        if world != 1:
-            raise
-        # one rank holds every frame: composite with the host plan, as Stitcher.run does when
-        # the device plan refuses (three frames over a column, a canvas above the capacity)
-        res = st._finish(cyl, colnz, e.records, margin, graph, {}, time.perf_counter())
+        if world == 1:
+            # one rank holds every frame: composite with the host plan, as Stitcher.run does
+            # when the device plan refuses (three frames over a column, a canvas above capacity)
+            res = st._finish(cyl, colnz, e.records, margin, graph, {}, time.perf_counter())
+            return {"records": res.records, "band": res.canvas, "x_offset": 0,
+                    "canvas_hw": tuple(res.canvas.shape[:2]), "bbox": res.bbox,
+                    "panorama": res.panorama, "canvas": res.canvas}
+        refused, recs, owned, own_lo, box = e, e.records, None, 0, NO_BOX
+    if world == 1:
+        y0, y1, x0, x1 = crop_box(box, H, W, margin)
+        canvas = owned                          # the whole canvas is rank 0's band
+        pano = canvas if (y0 > y1 or x0 > x1) else canvas[y0:y1 + 1, x0:x1 + 1]
+        return {"records": recs, "band": owned, "x_offset": own_lo, "canvas_hw": (H, W),
+                "bbox": (y0, y1, x0, x1), "panorama": pano, "canvas": canvas}
+    own = (own_lo, own_lo + (owned.shape[1] if owned is not None else 0))
+    layout = exchange_layout(box, own, refused is not None, group, device=cyl.device)
+    if layout[:, 6].any():
+        # some band was refused: every rank saw it in the layout, so all take the fallback
+        res = fold_on_root(st, cyl, colnz, recs, pair_counts, margin, group)
+        if res is None:
+            return {"records": recs, "band": None, "x_offset": 0, "canvas_hw": None, "bbox": None,
+                    "panorama": None, "canvas": None}
         return {"records": res.records, "band": res.canvas, "x_offset": 0,
-                "canvas_hw": tuple(res.canvas.shape[:2]), "bbox": res.bbox}
-    g = box if world == 1 else global_bbox(torch.tensor(box, dtype=torch.int64, device=owned.device), group)
-    if g[1] >= 0:
-        y0, y1 = max(0, g[0] + margin), min(H - 1, g[1] - margin)
-    else:
-        y0, y1 = 0, H - 1
+                "canvas_hw": tuple(res.canvas.shape[:2]), "bbox": res.bbox, "panorama": res.panorama,
+                "canvas": res.canvas}
+    y0, y1, x0, x1 = crop_box(layout_box(layout), H, W, margin)
+    canvas = assemble_bands(owned, layout, (H, W), group, out=st._get("full_canvas", (H, W, 3), torch.uint8)
+                            if dist.get_rank(group) == 0 else None)
+    pano = None
+    if canvas is not None:
+        pano = canvas if (y0 > y1 or x0 > x1) else canvas[y0:y1 + 1, x0:x1 + 1]
     return {"records": recs, "band": owned, "x_offset": own_lo, "canvas_hw": (H, W),
-            "bbox": (y0, y1, g[2], g[3])}
+            "bbox": (y0, y1, x0, x1), "panorama": pano, "canvas": canvas}
