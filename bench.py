@@ -7,7 +7,9 @@
 A step = one whole stitch of one rank's sequence, inputs resident in HBM:
 cylindrical projection -> SIFT features of every frame -> NN match (exact i8 MFMA) -> RANSAC
 -> [N>1: all_gather of per-pair records] -> drift correction + composite plan -> composite
-(band) -> crop bounding box [N>1: 4-int all_reduce].  Rank r stitches the parrington loop
+(band) -> crop bounding box [N>1: one 8-int-per-rank layout all_gather, every band sent to
+rank 0 (RCCL P2P over xGMI), which assembles the canvas and crops the panorama -- inside the
+timed step].  Rank r stitches the parrington loop
 starting at frame 17 r (18 frames, 17 pairs): per-GPU work is fixed ("weak" scaling) and the
 job is one panorama of N laps, N*17 + 1 distinct frames.
 
@@ -410,6 +412,8 @@ def main():
                                f"frames ({args.scaling} scaling)",
                    "frames": distinct, "frame_hw": [h, w], "parallelism": f"pairs sharded x{world}",
                    "method": args.method, "match_gemm": st.match,
+                   "assembly": "one canvas on one GPU" if world == 1 else
+                   "bands sent to rank 0 (RCCL P2P), canvas assembled and cropped there, in the timed step",
                    "launch": "hipGraph replay" if args.graph else "eager"},
         "roofline": roof,
         "roofline_match": roof_match,
