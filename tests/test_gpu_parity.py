@@ -766,3 +766,77 @@ def test_frame_above_2047_px_vs_oracle_golden(gpu, gold_json, gold_npz):
     np.testing.assert_allclose(rec["size"], g["size"], rtol=3e-7, atol=0)
     sel = np.arange(0, n, meta["sub"])
     _compare_features(rec[sel], d[sel], {k: v[sel] for k, v in g.items()}, z["desc_sub"])
+
+
+# ------------------------------------------------------------------ streaming cascade (S1-S4)
+def _full_pyramid(st, frames_dev):
+    """Every Gaussian and DoG level of a resident full pyramid (pano_sift_pyramid)."""
+    from vfx_image_stitching_amd import _lib
+    import torch
+    ctx = st.ctx
+    n, hh, ww = frames_dev.shape[:3]
+    ctx.check(ctx.lib.pano_sift_pyramid(ctx.h, _lib.ptr(frames_dev), n, hh, ww, ctypes.byref(st.params)))
+    no = ctypes.c_int32()
+    ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, 0, None, None, ctypes.byref(no)))
+    out = {}
+    for o in range(no.value):
+        h, w = ctypes.c_int32(), ctypes.c_int32()
+        ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(h), ctypes.byref(w), None))
+        for dog, nl in ((0, 6), (1, 5)):
+            for l in range(nl):
+                for fi in range(n):
+                    t = torch.empty((h.value, w.value), dtype=torch.float32, device=st.device)
+                    ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, fi, o, l, dog, _lib.ptr(t)))
+                    out[(fi, o, l, dog)] = t.cpu().numpy()
+    return out
+
+
+@pytest.mark.parametrize("bh", ["256", "40"])
+def test_cascade_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl, outset, monkeypatch, bh):
+    """The streaming cascades (PANO_BLUR_CASCADE=1: walker A = base/1/2 or 1/2, walker B = 3/4/5
+    per octave, strips walked down in 8-row chunks) give every level and DoG of the full
+    pyramid bit for bit: against the oracle on parrington, and against the level-by-level
+    launches on the out/ frames (571 x 428: widths off the 64-column strip grid), with the
+    default band height and a short one (band edges in every plane)."""
+    from vfx_image_stitching_amd import _lib
+    monkeypatch.setenv("PANO_CAS_BH", bh)
+    dev, cyl, _ = parr_dev
+    one = cyl[:2].contiguous()
+    monkeypatch.setenv("PANO_BLUR_CASCADE", "1")
+    got = _full_pyramid(st_sift, one)
+    for fi in range(2):
+        _, _, stg = osift.detect_and_describe(parrington_cyl[fi], return_stages=True)
+        for o in range(len(stg["gauss"])):
+            for dog, levels in ((0, stg["gauss"][o]), (1, stg["dog"][o])):
+                for l, ref in enumerate(levels):
+                    assert np.array_equal(got[(fi, o, l, dog)], ref), (fi, o, l, dog)
+    names, frames, focals, _ = outset
+    ocyl = st_sift.upload(np.stack([ostitch.cylindrical(frames[i], focals[i]) for i in range(2)]))
+    on = _full_pyramid(st_sift, ocyl)
+    monkeypatch.setenv("PANO_BLUR_CASCADE", "0")
+    off = _full_pyramid(st_sift, ocyl)
+    assert on.keys() == off.keys()
+    for k in off:
+        assert on[k].tobytes() == off[k].tobytes(), k
+
+
+def test_cascade_features_and_stitch_identical(gpu, parrington, monkeypatch):
+    """The Stitcher's own path (pano_sift_u8: levels 4 and 5 never written) with the cascade:
+    the same keypoints, descriptors and panorama bytes as the level-by-level launches."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    _, frames, focals, margin = parrington
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PANO_BLUR_CASCADE", mode)
+        st = Stitcher("sift")
+        dev = st.upload(frames)
+        cyl, _ = st.cylindrical(dev, focals)
+        k, d, c = st.features(cyl)
+        r = st.run(dev, focals, margin=margin)
+        cnt = c.cpu().numpy()
+        kh, dh = k.cpu().numpy(), d.cpu().numpy()
+        res[mode] = (cnt, *[kh[i, :cnt[i]] for i in range(len(cnt))], *[dh[i, :cnt[i]] for i in range(len(cnt))],
+                     r.panorama.cpu().numpy())
+        st.release_graphs()
+    for a, b in zip(res["0"], res["1"]):
+        assert a.tobytes() == b.tobytes()

@@ -20,9 +20,11 @@
 // register mapping that keeps this per-output operation order is bit-identical.  The x2
 // bilinear upsample of integer gray levels is exact.
 #include "pano_internal.h"
+#include "cas_taps.h"
 
 #include <algorithm>
 #include <cstring>
+#include <utility>
 
 namespace {
 
@@ -863,6 +865,336 @@ int launch_chain(pano_ctx *ctx, const LoadArgs &la, const ChainOut &co, int n, i
     return PANO_OK;
 }
 
+// ------------------------------------------------------------------ streaming cascade
+// Two or three consecutive levels of an octave in ONE launch WITHOUT the 2-D halo of the tile
+// chains above: a workgroup owns a strip of kCasSW output columns of one band of rows and
+// WALKS DOWN it, kCasK rows (one "chunk") per step.  Level j keeps its row-pass output (T_j)
+// in an LDS ring of 2 d_j + 1 chunks, d_j = ceil(R_j / K): the column pass of chunk c needs T_j
+// rows up to R_j beyond it, so level j runs d_j chunks behind its row pass, and level j+1's
+// row pass consumes level j's chunk as soon as it is produced (from the staging buffer S).
+// Vertically every intermediate row is computed once (only the band edges recompute the
+// later levels' radii); horizontally level j is computed on the strip plus the halo the
+// remaining levels need (sum of their radii).  The written planes are only those later
+// stages read (the levels asked for and the DoGs); the intermediate levels never touch HBM.
+//
+// Wave roles.  Waves 0..3 compute and touch only LDS.  Wave 4 (the store wave) writes the
+// outputs of the previous step to HBM from owned-column rings of every level (the DoG is its
+// subtraction), and wave 5 (the loader) fetches the next chunk of the input level while the
+// current one is computed.  On gfx9 a wait for a load also waits for every store issued
+// before it (vmcnt is in order): a compute wave that stored its outputs would stall on HBM
+// write latency at its next load; here no wave that waits on a load ever stores.
+//
+// Exactness: per output the arithmetic is blur_fast's -- RowVec_32f's sequential f32 FMA over
+// the taps, SymmColumnVec_32f's symmetric column form -- with BORDER_REFLECT_101 taken on the
+// LEVEL values: image rows outside the plane are read at their reflected row (the ring holds
+// every row a chunk needs, reflected ones included), and the columns of S outside the plane
+// are overwritten with their mirror before the next level reads them (a blur of reflected
+// inputs would run its taps in the opposite order and round differently).  Hence the same
+// bits as the level-by-level launches.  The taps are the reference's default ones compiled in
+// (cas_taps.h, tools/gen_cas_taps.py); the launcher uses the cascade only when the run-time
+// taps equal them bit for bit.
+constexpr int kCasK = 8;                 // rows per step (one chunk)
+constexpr int kCasSW = 64;               // owned output columns of a strip
+constexpr int kCasCW = 4;                // compute waves
+constexpr int kCasThreads = 64 * (kCasCW + 2);
+constexpr int kCasStoreWave = kCasCW, kCasLoadWave = kCasCW + 1;
+constexpr int kCasSR = 4;                // row-pass outputs per item
+constexpr int kCasSC = kCasK / 2;        // column-pass outputs per item (two row halves)
+
+struct CasOut {
+    float *gin;                          // MODE_DOWN: the input (the octave's G0), or null
+    float *g[3];                         // level j at its owned positions, or null
+    float *d[3];                         // level j minus its predecessor (the input for j = 0), or null
+};
+
+template <int NL, int L0, bool HAS_IN>
+struct Cas {
+    static constexpr int nt(int j) { return kCasDefTaps[L0 + j]; }
+    static constexpr int r(int j) { return (nt(j) - 1) / 2; }
+    static constexpr int hx(int j) {     // rows / columns level j computes beyond the owned ones
+        int s = 0;
+        for (int i = j + 1; i < NL; ++i) s += r(i);
+        return s;
+    }
+    static constexpr int hin() { return hx(0) + r(0); }
+    static constexpr int w(int j) { return kCasSW + 2 * hx(j); }
+    static constexpr int nsg(int j) { return (w(j) + kCasSR - 1) / kCasSR; }
+    static constexpr int pt(int j) { return (nsg(j) * kCasSR) | 1; }             // T ring pitch (odd)
+    static constexpr int d(int j) { return (r(j) + kCasK - 1) / kCasK; }         // chunk lookahead
+    static constexpr int ns(int j) { return 2 * d(j) + 1; }                      // T ring chunks
+    static constexpr int lag(int j) {
+        int s = 0;
+        for (int i = 0; i < j; ++i) s += d(i);
+        return s;
+    }
+    static constexpr int win() { return w(0) + 2 * r(0); }
+    static constexpr int pin() { return (nsg(0) * kCasSR + nt(0) - 1) | 1; }    // IN pitch (odd)
+    static constexpr int ps() {                                                  // S pitch (odd)
+        int m = 1;
+        for (int j = 1; j < NL; ++j) {
+            const int q = nsg(j) * kCasSR + nt(j) - 1;
+            m = m > q ? m : q;
+        }
+        return m | 1;
+    }
+    // owned-column rings read by the store wave: level j's rows are kept until its successor's
+    // DoG is stored (d_{j+1} steps later, plus the store's own step); the input's until DoG 0
+    static constexpr int gs(int j) { return j + 1 < NL ? d(j + 1) + 2 : 2; }
+    static constexpr int is() { return HAS_IN ? d(0) + 3 : 0; }
+    static constexpr int off_s() { return kCasK * pin(); }
+    static constexpr int off_t(int j) {
+        int o = off_s() + kCasK * ps();
+        for (int i = 0; i < j; ++i) o += ns(i) * kCasK * pt(i);
+        return o;
+    }
+    static constexpr int off_g(int j) {
+        int o = off_t(NL);
+        for (int i = 0; i < j; ++i) o += gs(i) * kCasK * kCasSW;
+        return o;
+    }
+    static constexpr int off_i() { return off_g(NL); }
+    static constexpr int floats() { return off_i() + is() * kCasK * kCasSW; }
+};
+
+template <int MODE, int NL, int L0>
+__global__ void __launch_bounds__(kCasThreads)
+blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
+    constexpr bool HAS_IN = MODE != MODE_BASE && MODE != MODE_BASEF;   // the input is a level
+    using S = Cas<NL, L0, HAS_IN>;
+    static_assert(S::win() <= 128 && S::w(0) <= 128, "two staged columns per lane, one column per col item");
+    static_assert(kCasK * S::nsg(0) <= 64 * kCasCW, "one row-pass item per compute thread");
+    static_assert(kCasK == 8 && kCasCW == 4, "two row halves over waves 0-1 / 2-3");
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const unsigned tb = xcd_swizzle(linear_block_id(), gridDim.x * gridDim.y * gridDim.z);
+    const int sx = (int)(tb % gridDim.x), by = (int)((tb / gridDim.x) % gridDim.y);
+    const int f = (int)(tb / (gridDim.x * gridDim.y));
+    const int ox0 = sx * kCasSW, ox1 = min(W, ox0 + kCasSW);      // owned columns
+    const int xs = min(ox0, W - kCasSW);                            // strip origin (W >= kCasSW)
+    const int yb0 = by * BH, yb1 = min(H, yb0 + BH);               // owned rows
+    const int ybase = max(0, yb0 - S::hin()), yend = min(H, yb1 + S::hin());
+    int Y[NL], E[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        Y[j] = max(0, yb0 - S::hx(j));
+        E[j] = min(H, yb1 + S::hx(j));
+    }
+    const int nsteps = ((E[NL - 1] - 1 - ybase) >> 3) + S::lag(NL - 1) + S::d(NL - 1) + 1;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool border = xs - S::hx(0) < 0 || xs + kCasSW + S::hx(0) > W;
+    const size_t fo = (size_t)f * H * W;
+    float *IN = lds, *SB = lds + S::off_s();
+
+    // ---- the loader: chunk c of the input level (reflected columns) into registers, then
+    // into IN (and its owned columns into the input ring) once the current step is done with IN
+    const Stager<MODE> sg(la, f, H, W);
+    const bool has1 = 64 + lane < S::win();
+    const ColMap m0 = sg.col(xs - S::hin() + lane);
+    const ColMap m1 = sg.col(xs - S::hin() + (has1 ? 64 + lane : lane));
+    float lv0[kCasK], lv1[kCasK];
+    auto load_issue = [&](int c) {
+        const int r0 = ybase + c * kCasK;
+#pragma unroll
+        for (int q = 0; q < kCasK; ++q) {
+            if (r0 + q < yend) {
+                lv0[q] = sg.get(r0 + q, m0);
+                lv1[q] = has1 ? sg.get(r0 + q, m1) : 0.0f;
+            }
+        }
+    };
+    auto load_commit = [&](int c) {
+        const int r0 = ybase + c * kCasK;
+#pragma unroll
+        for (int q = 0; q < kCasK; ++q) {
+            if (r0 + q < yend) {
+                if (lane < S::win()) IN[q * S::pin() + lane] = lv0[q];
+                if (has1) IN[q * S::pin() + 64 + lane] = lv1[q];
+            }
+        }
+        if constexpr (HAS_IN) {
+            // the wave's own LDS writes are in order: read the owned centres back
+            float *ring = lds + S::off_i() + (c % S::is()) * kCasK * kCasSW;
+#pragma unroll
+            for (int q = 0; q < kCasK; ++q)
+                if (r0 + q < yend) ring[q * kCasSW + lane] = IN[q * S::pin() + lane + S::hin()];
+        }
+    };
+    // ---- the store wave: level j's outputs produced at step s, from the rings (all the
+    // chunk's LDS reads first, then its stores)
+    const int sgx = xs + lane;
+    const bool own_c = sgx >= ox0 && sgx < ox1;
+    auto store_level = [&](auto jc, int s) {
+        constexpr int j = decltype(jc)::value;
+        const int cg = s - S::lag(j) - S::d(j);
+        if (cg < 0 || (!co.g[j] && !co.d[j])) return;
+        const int g0 = ybase + cg * kCasK;
+        const int lo = max(g0, yb0), hi = min(g0 + kCasK, yb1);
+        if (lo >= hi) return;
+        const float *gr = lds + S::off_g(j) + (cg % S::gs(j)) * kCasK * kCasSW + lane;
+        const float *pr = nullptr;
+        if constexpr (j > 0) pr = lds + S::off_g(j > 0 ? j - 1 : 0) + (cg % S::gs(j > 0 ? j - 1 : 0)) * kCasK * kCasSW + lane;
+        else if constexpr (HAS_IN) pr = lds + S::off_i() + (cg % (S::is() > 0 ? S::is() : 1)) * kCasK * kCasSW + lane;
+        float v[kCasK], dv[kCasK];
+#pragma unroll
+        for (int q = 0; q < kCasK; ++q) {
+            v[q] = gr[q * kCasSW];
+            dv[q] = pr ? v[q] - pr[q * kCasSW] : 0.0f;
+        }
+        if (!own_c) return;
+#pragma unroll
+        for (int q = 0; q < kCasK; ++q) {
+            const int y = g0 + q;
+            if (y < lo || y >= hi) continue;
+            const size_t gi = fo + (size_t)y * W + sgx;
+            if (co.g[j]) co.g[j][gi] = v[q];
+            if (co.d[j] && pr) co.d[j][gi] = dv[q];
+        }
+    };
+    auto store_input = [&](int s) {
+        // the input chunk s (MODE_DOWN: the octave's G0 plane when a full pyramid is asked)
+        if constexpr (HAS_IN) {
+            if (!co.gin || !own_c) return;
+            const int g0 = ybase + s * kCasK;
+            const float *ir = lds + S::off_i() + (s % S::is()) * kCasK * kCasSW + lane;
+            float v[kCasK];
+#pragma unroll
+            for (int q = 0; q < kCasK; ++q) v[q] = ir[q * kCasSW];
+#pragma unroll
+            for (int q = 0; q < kCasK; ++q) {
+                const int y = g0 + q;
+                if (y >= max(g0, yb0) && y < min(g0 + kCasK, yb1)) co.gin[fo + (size_t)y * W + sgx] = v[q];
+            }
+        }
+    };
+
+    if (wv == kCasLoadWave) {
+        load_issue(0);
+        load_commit(0);
+    }
+    lds_barrier();
+    for (int s = 0; s < nsteps; ++s) {
+        if (wv == kCasLoadWave) load_issue(s + 1);
+        else if (wv == kCasStoreWave && s > 0) store_input(s - 1);
+        auto level = [&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int NT = S::nt(j), R = S::r(j);
+            constexpr const float *KT = kCasDefK[L0 + j];
+            if (wv == kCasStoreWave && s > 0) store_level(jc, s - 1);   // beside the row pass
+            // ---- row pass of level j, chunk ct (the input's chunk for j = 0, else the chunk
+            // of level j - 1 its column pass just left in S)
+            const int ct = s - S::lag(j);
+            const int t0 = ybase + ct * kCasK;
+            const int tlo = max(t0, j == 0 ? ybase : Y[j > 0 ? j - 1 : 0]);
+            const int thi = min(t0 + kCasK, j == 0 ? yend : E[j > 0 ? j - 1 : 0]);
+            if (wv < kCasCW && ct >= 0 && tlo < thi) {
+                const int q = tid / S::nsg(j), g = tid - q * S::nsg(j);
+                const int y = t0 + q;
+                if (q < kCasK && y >= tlo && y < thi) {
+                    const float *src = (j == 0 ? IN + q * S::pin() : SB + q * S::ps()) + g * kCasSR;
+                    float acc[kCasSR];
+                    row_seg<NT, kCasSR>(src, KT, acc);
+                    float *dst = lds + S::off_t(j) + ((ct % S::ns(j)) * kCasK + q) * S::pt(j) + g * kCasSR;
+#pragma unroll
+                    for (int k = 0; k < kCasSR; ++k) dst[k] = acc[k];
+                }
+            }
+            lds_barrier();
+            // ---- column pass of level j, chunk cg = ct - d_j: two row halves, one column per
+            // lane; rows (and their ring slots) are wave-uniform
+            const int cg = ct - S::d(j);
+            const int g0 = ybase + cg * kCasK;
+            const int glo = max(g0, Y[j]), ghi = min(g0 + kCasK, E[j]);
+            const int h = wv >> 1, i = lane + 64 * (wv & 1);
+            if (wv < kCasCW && cg >= 0 && glo < ghi && i < S::w(j)) {
+                constexpr int NV = kCasSC + 2 * R, RS = S::ns(j) * kCasK;   // ring rows
+                const float *T = lds + S::off_t(j) + i;
+                const int yt = g0 + h * kCasSC - R;                          // first tap row
+                float v[NV];
+                if (yt >= 0 && yt + NV <= H) {
+                    // no reflection: consecutive ring rows, wrapping once
+                    int p = (yt - ybase) % RS;
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) {
+                        v[k] = T[p * S::pt(j)];
+                        p = p + 1 == RS ? 0 : p + 1;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) {
+                        int lr = reflect101(yt + k, H) - ybase;
+                        lr = lr < 0 ? 0 : lr;                 // rows no valid output reads
+                        v[k] = T[(lr % RS) * S::pt(j)];
+                    }
+                }
+                float o[kCasSC];
+#pragma unroll
+                for (int qq = 0; qq < kCasSC; ++qq) o[qq] = v[qq + R] * KT[R];
+#pragma unroll
+                for (int dd = 1; dd <= R; ++dd)
+#pragma unroll
+                    for (int qq = 0; qq < kCasSC; ++qq)
+                        o[qq] = __builtin_fmaf(v[qq + R + dd] + v[qq + R - dd], KT[R + dd], o[qq]);
+#pragma unroll
+                for (int qq = 0; qq < kCasSC; ++qq) asm volatile("" ::"v"(o[qq]));   // all outputs first
+                const int hc = i - S::hx(j);                              // owned column index
+                const bool own = hc >= 0 && hc < kCasSW;
+                float *gr = lds + S::off_g(j) + (cg % S::gs(j)) * kCasK * kCasSW + hc;
+#pragma unroll
+                for (int qq = 0; qq < kCasSC; ++qq) {
+                    const int qr = h * kCasSC + qq, y = g0 + qr;
+                    if (y < glo || y >= ghi) continue;
+                    if (j + 1 < NL) SB[qr * S::ps() + i] = o[qq];
+                    if (own) gr[qr * kCasSW] = o[qq];
+                }
+            }
+            lds_barrier();
+            if (j + 1 < NL && border && cg >= 0 && glo < ghi) {
+                // S's columns outside the plane <- their BORDER_REFLECT_101 mirror
+                constexpr int WJ = S::w(j);
+                if (wv < kCasCW) {
+                    for (int e = tid; e < kCasK * WJ; e += 64 * kCasCW) {
+                        const int q = e / WJ, ii = e - q * WJ;
+                        const int gx = xs - S::hx(j) + ii;
+                        if (gx >= 0 && gx < W) continue;
+                        SB[q * S::ps() + ii] = SB[q * S::ps() + reflect101(gx, W) - (xs - S::hx(j))];
+                    }
+                }
+                lds_barrier();
+            }
+        };
+        level(std::integral_constant<int, 0>{});
+        if constexpr (NL > 1) level(std::integral_constant<int, 1>{});
+        if constexpr (NL > 2) level(std::integral_constant<int, 2>{});
+        if (wv == kCasLoadWave) load_commit(s + 1);
+        lds_barrier();
+    }
+    if (wv == kCasStoreWave) {
+        store_input(nsteps - 1);
+        store_level(std::integral_constant<int, 0>{}, nsteps - 1);
+        if constexpr (NL > 1) store_level(std::integral_constant<int, 1>{}, nsteps - 1);
+        if constexpr (NL > 2) store_level(std::integral_constant<int, 2>{}, nsteps - 1);
+    }
+}
+
+template <int MODE, int NL, int L0>
+int launch_cascade(pano_ctx *ctx, const LoadArgs &la, const CasOut &co, int n, int H, int W, int BH) {
+    using S = Cas<NL, L0, MODE != MODE_BASE && MODE != MODE_BASEF>;
+    const size_t sm = (size_t)S::floats() * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        PANO_HIP(ctx, hipFuncSetAttribute((const void *)blur_cascade<MODE, NL, L0>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        attr = true;
+    }
+    dim3 grid((W + kCasSW - 1) / kCasSW, (H + BH - 1) / BH, n);
+    {
+        PanoProf prof_(ctx, PK_BLUR);
+        blur_cascade<MODE, NL, L0><<<grid, kCasThreads, sm, ctx->stream>>>(la, co, H, W, BH);
+    }
+    PANO_LAUNCH_CHECK(ctx, "blur_cascade");
+    return PANO_OK;
+}
+
 // ------------------------------------------------------------------ small-octave tail
 // Octaves whose levels fit one 64 x 64 tile are latency-bound as separate launches (one
 // tiny workgroup per frame, ~7 us each, 5 per octave).  blur_tail runs them all in ONE
@@ -1384,6 +1716,22 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
                             tl[4].n == 21 && tl[5].n == 27;
     auto chain_ok = [&](int o) { return chain_taps && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= 64; };
     const bool chain_base = src.bgr && !src.base_only && chain_ok(0) && tb.n == 11;
+    // streaming cascades (blur_cascade, PANO_BLUR_CASCADE=1): per octave walker A (octave 0 from
+    // the gray frames: base, 1, 2; else levels 1, 2) and walker B (levels 3, 4, 5 from G2)
+    const char *cas_env = getenv("PANO_BLUR_CASCADE");     // read per call: tests compare both forms
+    const int cas_on = cas_env ? atoi(cas_env) : 0;
+    static const int cas_bh = [] {
+        const char *e = getenv("PANO_CAS_BH");   // band rows per workgroup
+        return e ? std::max(8, atoi(e)) : 256;
+    }();
+    // the cascade compiles in the reference's default taps (cas_taps.h): only when they are the
+    // run-time ones, bit for bit
+    bool cas_taps = cas_on && !chain_on && nl == kCasDefLevels && tb.n == kCasDefTaps[0] &&
+                    memcmp(tb.k, kCasDefK[0], sizeof(float) * tb.n) == 0;
+    for (int l = 1; cas_taps && l < nl; ++l)
+        cas_taps = tl[l].n == kCasDefTaps[l] && memcmp(tl[l].k, kCasDefK[l], sizeof(float) * tl[l].n) == 0;
+    auto cas_ok = [&](int o) { return cas_taps && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= kCasSW; };
+    const bool cas_base = src.bgr && !src.base_only && cas_ok(0);
     if (src.base) {
         // generate_gaussian_images(base, ...): the caller's base is level 0 of octave 0
         PANO_HIP(ctx, hipMemcpyAsync(G + ctx->gauss_off[0][0], src.base,
@@ -1397,7 +1745,7 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         rc = launch_blur<MODE_BASEF>(ctx, la, G + ctx->gauss_off[0][0], nullptr, nullptr, n,
                                      ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
-    } else if (chain_base) {
+    } else if (chain_base || cas_base) {
         // gray frames only: the base level is the first level of octave 0's first chain
         const size_t npx = (size_t)n * h * w;
         rc = pano_grow(ctx, (void **)&ctx->gray, &ctx->gray_bytes, npx + 16);
@@ -1533,7 +1881,52 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
         ctx->stream = o >= o_side ? ctx->side : main_stream;     // side-stream octaves
-        const bool fork_lvl = oct_fork >= 0 && o >= oct_fork && o < o_side && nl >= 4 && !chain_ok(o);
+        const bool fork_lvl = oct_fork >= 0 && o >= oct_fork && o < o_side && nl >= 4 && !chain_ok(o) && !cas_ok(o);
+        if (cas_ok(o)) {
+            auto Gp = [&](int l) { return G + ctx->gauss_off[o][l]; };
+            auto Dp = [&](int l) { return D + ctx->dog_off[o][l]; };
+            const int bh = std::min(H, cas_bh);
+            LoadArgs la{};
+            CasOut ca{};
+            if (o == 0 && cas_base) {
+                la.gray = ctx->gray;
+                la.sh = h;
+                la.sw = w;
+                ca.g[0] = full ? Gp(0) : nullptr;
+                ca.g[1] = Gp(1); ca.d[1] = Dp(0);
+                ca.g[2] = Gp(2); ca.d[2] = Dp(1);
+                rc = launch_cascade<MODE_BASE, 3, 0>(ctx, la, ca, n, H, W, bh);
+            } else {
+                ca.g[0] = Gp(1); ca.d[0] = Dp(0);
+                ca.g[1] = Gp(2); ca.d[1] = Dp(1);
+                if (o == 0) {
+                    la.src = Gp(0);
+                    rc = launch_cascade<MODE_LEVEL, 2, 1>(ctx, la, ca, n, H, W, bh);
+                } else {
+                    la.src = G + ctx->gauss_off[o - 1][nl - 3];
+                    la.sh = ctx->oct_h[o - 1];
+                    la.sw = ctx->oct_w[o - 1];
+                    la.ifx = 1.0 / ((double)W / la.sw);
+                    la.ify = 1.0 / ((double)H / la.sh);
+                    ca.gin = full ? Gp(0) : nullptr;
+                    rc = launch_cascade<MODE_DOWN, 2, 1>(ctx, la, ca, n, H, W, bh);
+                }
+            }
+            if (rc) { ctx->stream = main_stream; return rc; }
+            LoadArgs lb{};
+            lb.src = Gp(2);
+            CasOut cb{};
+            cb.g[0] = Gp(3); cb.d[0] = Dp(2);
+            cb.g[1] = full ? Gp(4) : nullptr; cb.d[1] = Dp(3);
+            cb.g[2] = full ? Gp(5) : nullptr; cb.d[2] = Dp(4);
+            rc = launch_cascade<MODE_LEVEL, 3, 3>(ctx, lb, cb, n, H, W, bh);
+            if (rc) { ctx->stream = main_stream; return rc; }
+            if (o == o_side - 1 && o_tail < no) {
+                rc = fork();
+                if (rc) { ctx->stream = main_stream; return rc; }
+            }
+            continue;
+        }
         if (chain_ok(o)) {
             // chain A: levels 1-2 (octave 0 from gray: base, 1, 2); chain B: levels 3-5 from G2.
             // Written: G1-G3 and DoG 0-4 (every level in a full pyramid)
