@@ -37,3 +37,23 @@ t4 = time.perf_counter()
 print(f"run(): {(t1 - t0) / N * 1e6:.1f} us/stitch; launch+wait only: {(t2 - t1) / N * 1e6:.1f} us; "
       f"launch only (async, {N} queued): {(t3 - t2) / N * 1e6:.1f} us CPU per launch, "
       f"drain {(t4 - t3) * 1e3:.1f} ms; back-to-back GPU time {(t4 - t2) / N * 1e6:.1f} us/graph")
+# wake-up: the same launch, then a busy poll of the stream instead of the blocking sync
+s = torch.cuda.current_stream()
+t5 = time.perf_counter()
+for _ in range(N):
+    lib.pano_graph_launch(c, g)
+    while not s.query():
+        pass
+t6 = time.perf_counter()
+# the host work of run() alone: its Python around a replay, with the GPU already done
+st.run(d, focals, margin=margin, graph=True)
+torch.cuda.synchronize()
+launch_sync = lib.pano_graph_launch_sync
+lib.pano_graph_launch_sync = lambda *a: 0            # no GPU work: pure host path
+t7 = time.perf_counter()
+for _ in range(N):
+    st.run(d, focals, margin=margin, graph=True)
+t8 = time.perf_counter()
+lib.pano_graph_launch_sync = launch_sync
+print(f"launch + spin on hipStreamQuery: {(t6 - t5) / N * 1e6:.1f} us/stitch; "
+      f"run()'s host path alone: {(t8 - t7) / N * 1e6:.1f} us")

@@ -956,6 +956,20 @@ struct Cas {
     static constexpr int floats() { return off_i() + is() * kCasK * kCasSW; }
 };
 
+#ifndef PANO_CAS_TIMING
+#define PANO_CAS_TIMING 0     // 1: per-phase clock stamps of one workgroup (diagnostics build)
+#endif
+#if PANO_CAS_TIMING
+__device__ unsigned long long g_cas_clock[3][96][16];   // [compute / store / load wave][step][event]
+#define PANO_CAS_STAMP(role, ev)                                                                      \
+    do {                                                                                            \
+        if (lane == 0 && blockIdx.x == PANO_CAS_TIMING - 1 && blockIdx.y == 0 && blockIdx.z == 0 && s < 96) \
+            g_cas_clock[role][s][ev] = __builtin_amdgcn_s_memtime();                                 \
+    } while (0)
+#else
+#define PANO_CAS_STAMP(role, ev) do {} while (0)
+#endif
+
 template <int MODE, int NL, int L0>
 __global__ void __launch_bounds__(kCasThreads)
 blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
@@ -993,13 +1007,15 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
     const ColMap m1 = sg.col(xs - S::hin() + (has1 ? 64 + lane : lane));
     float lv0[kCasK], lv1[kCasK];
     auto load_issue = [&](int c) {
+        // branch-free: rows past the input's end load the last row again (never stored), lanes
+        // without a second column load their first column twice, so all 16 loads are in flight
+        // together (a predicated load made the compiler wait for each one before the next)
         const int r0 = ybase + c * kCasK;
 #pragma unroll
         for (int q = 0; q < kCasK; ++q) {
-            if (r0 + q < yend) {
-                lv0[q] = sg.get(r0 + q, m0);
-                lv1[q] = has1 ? sg.get(r0 + q, m1) : 0.0f;
-            }
+            const int rr = min(r0 + q, yend - 1);
+            lv0[q] = sg.get(rr, m0);
+            lv1[q] = sg.get(rr, m1);
         }
     };
     auto load_commit = [&](int c) {
@@ -1023,6 +1039,8 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
     // chunk's LDS reads first, then its stores)
     const int sgx = xs + lane;
     const bool own_c = sgx >= ox0 && sgx < ox1;
+    // 16-byte output rows: plane rows and the strip 4-float aligned, owned range on 4-column groups
+    const bool vec4 = (W & 3) == 0 && (xs & 3) == 0 && ((ox0 - xs) & 3) == 0 && ((ox1 - xs) & 3) == 0;
     auto store_level = [&](auto jc, int s) {
         constexpr int j = decltype(jc)::value;
         const int cg = s - S::lag(j) - S::d(j);
@@ -1034,6 +1052,27 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
         const float *pr = nullptr;
         if constexpr (j > 0) pr = lds + S::off_g(j > 0 ? j - 1 : 0) + (cg % S::gs(j > 0 ? j - 1 : 0)) * kCasK * kCasSW + lane;
         else if constexpr (HAS_IN) pr = lds + S::off_i() + (cg % (S::is() > 0 ? S::is() : 1)) * kCasK * kCasSW + lane;
+        if (vec4) {
+            // 16-byte stores: lane = (row 0..3 of a half chunk, 4-column group); a wave keeps at
+            // most 63 stores in flight, so fewer, wider ones keep the store wave off the barriers
+            const int qh = lane >> 4, cgp = (lane & 15) * 4;
+            const bool own4 = cgp >= ox0 - xs && cgp < ox1 - xs;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const int q = half * 4 + qh, y = g0 + q;
+                const float4 gv = *(const float4 *)(gr - lane + q * kCasSW + cgp);
+                float4 dv = gv;
+                if (pr) {
+                    const float4 pv = *(const float4 *)(pr - lane + q * kCasSW + cgp);
+                    dv = make_float4(gv.x - pv.x, gv.y - pv.y, gv.z - pv.z, gv.w - pv.w);
+                }
+                if (!own4 || y < lo || y >= hi) continue;
+                const size_t gi = fo + (size_t)y * W + xs + cgp;
+                if (co.g[j]) *(float4 *)(co.g[j] + gi) = gv;
+                if (co.d[j] && pr) *(float4 *)(co.d[j] + gi) = dv;
+            }
+            return;
+        }
         float v[kCasK], dv[kCasK];
 #pragma unroll
         for (int q = 0; q < kCasK; ++q) {
@@ -1073,13 +1112,19 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
     }
     lds_barrier();
     for (int s = 0; s < nsteps; ++s) {
-        if (wv == kCasLoadWave) load_issue(s + 1);
+        [[maybe_unused]] int ev = 0;
+        if (wv == 0) PANO_CAS_STAMP(0, ev);
+        if (wv == kCasLoadWave) { PANO_CAS_STAMP(2, 0); load_issue(s + 1); PANO_CAS_STAMP(2, 1); }
         else if (wv == kCasStoreWave && s > 0) store_input(s - 1);
         auto level = [&](auto jc) {
             constexpr int j = decltype(jc)::value;
             constexpr int NT = S::nt(j), R = S::r(j);
             constexpr const float *KT = kCasDefK[L0 + j];
-            if (wv == kCasStoreWave && s > 0) store_level(jc, s - 1);   // beside the row pass
+            if (wv == kCasStoreWave && s > 0) {
+                PANO_CAS_STAMP(1, 2 * j);
+                store_level(jc, s - 1);   // beside the row pass
+                PANO_CAS_STAMP(1, 2 * j + 1);
+            }
             // ---- row pass of level j, chunk ct (the input's chunk for j = 0, else the chunk
             // of level j - 1 its column pass just left in S)
             const int ct = s - S::lag(j);
@@ -1099,6 +1144,7 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
                 }
             }
             lds_barrier();
+            if (wv == 0) PANO_CAS_STAMP(0, ++ev);
             // ---- column pass of level j, chunk cg = ct - d_j: two row halves, one column per
             // lane; rows (and their ring slots) are wave-uniform
             const int cg = ct - S::d(j);
@@ -1148,6 +1194,7 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
                 }
             }
             lds_barrier();
+            if (wv == 0) PANO_CAS_STAMP(0, ++ev);
             if (j + 1 < NL && border && cg >= 0 && glo < ghi) {
                 // S's columns outside the plane <- their BORDER_REFLECT_101 mirror
                 constexpr int WJ = S::w(j);
@@ -1165,8 +1212,9 @@ blur_cascade(LoadArgs la, CasOut co, int H, int W, int BH) {
         level(std::integral_constant<int, 0>{});
         if constexpr (NL > 1) level(std::integral_constant<int, 1>{});
         if constexpr (NL > 2) level(std::integral_constant<int, 2>{});
-        if (wv == kCasLoadWave) load_commit(s + 1);
+        if (wv == kCasLoadWave) { PANO_CAS_STAMP(2, 2); load_commit(s + 1); PANO_CAS_STAMP(2, 3); }
         lds_barrier();
+        if (wv == 0) PANO_CAS_STAMP(0, 15);
     }
     if (wv == kCasStoreWave) {
         store_input(nsteps - 1);
@@ -1973,7 +2021,11 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
             }
             continue;
         }
-        const bool pairs_here = o >= 1 && nl == 6 && H >= 32 && W >= 32 &&
+        static const bool pair_o0 = [] {      // A/B: fused pairs on octave 0 too
+            const char *e = getenv("PANO_BLUR_PAIR_O0");
+            return e && atoi(e) != 0;
+        }();
+        const bool pairs_here = (o >= 1 || pair_o0) && nl == 6 && H >= 32 && W >= 32 &&
                                 (long)((W + 63) / 64) * ((H + 63) / 64) * n < pair_tiles;
         for (int l = 1; l < nl; ++l) {
             if (fork_lvl && l == nl - 2) {
@@ -1998,7 +2050,7 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
                 float *dg2 = D + ctx->dog_off[o][l];
                 const bool keep1 = full || l + 1 < nl - 1 || l < nl - 2;   // G[l] read downstream
                 const bool keep2 = full || l + 1 < nl - 1;
-                if (l == 1) {
+                if (l == 1 && o > 0) {
                     la.src = G + ctx->gauss_off[o - 1][nl - 3];
                     la.sh = ctx->oct_h[o - 1];
                     la.sw = ctx->oct_w[o - 1];
@@ -2056,6 +2108,13 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     ctx->pyr_full = full;
     return PANO_OK;
 }
+
+#if PANO_CAS_TIMING
+// diagnostics build only (not in pano.h): the stamps of the last blur_cascade launch
+extern "C" int pano_dbg_cas_clock(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cas_clock), sizeof(g_cas_clock)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if PANO_TAIL_TIMING
 // diagnostics build only (not in pano.h): the stamps of the last blur_tail, after a sync
