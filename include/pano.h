@@ -91,6 +91,10 @@ int pano_ctx_destroy(pano_ctx *ctx);
 int pano_ctx_set_stream(pano_ctx *ctx, void *hip_stream);
 /* Pre-size scratch for n frames of h x w with cap keypoints per frame (allocates). */
 int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap);
+/* Free every scratch buffer the context grew (after a large batch; the next call re-allocates
+ * what it needs).  Waits for the stream; bumps the generation (captured graphs are stale).
+ * No reference counterpart: memory management of this library. */
+int pano_ctx_release_scratch(pano_ctx *ctx);
 int pano_sync(pano_ctx *ctx);
 const char *pano_last_error(pano_ctx *ctx);
 /* Scratch generation: incremented whenever the context frees and re-allocates scratch

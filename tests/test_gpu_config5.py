@@ -33,6 +33,9 @@ def batch(gpu):
     res = st.run(dev, focals, margin=15)
     yield st, dev, focals, jit, res
     st.release_graphs()
+    del dev, res
+    # the shared context's scratch grew to the 144-frame 1080p pyramid (~70 GB): give it back
+    st.ctx.release_scratch()
 
 
 def test_config5_every_pair_recovers_the_generator_shift(batch):

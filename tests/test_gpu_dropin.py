@@ -189,3 +189,20 @@ def test_graph_cache_survives_scratch_reallocation(gpu, parrington, grail, gold_
         st.run(short, pfo[:6], margin=pm, graph=True)      # alternate sequence lengths
     assert digest(st.run(dev, pfo, margin=pm, graph=True).panorama.cpu().numpy()) == want
     st.release_graphs()
+
+
+def test_release_scratch_then_replay_recaptures(gpu, parrington, gold_json):
+    """pano_ctx_release_scratch frees the grown scratch and bumps the generation: the cached
+    graph is not replayed over freed memory, the next run re-allocates and re-captures."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    _, pf, pfo, pm = parrington
+    want = gold_json("sift_parrington.json")["pano_digest"]
+    st = Stitcher("sift")
+    dev = st.upload(pf)
+    assert digest(st.run(dev, pfo, margin=pm, graph=True).panorama.cpu().numpy()) == want
+    gen = st.ctx.generation()
+    st.ctx.release_scratch()
+    assert st.ctx.generation() > gen
+    for _ in range(2):
+        assert digest(st.run(dev, pfo, margin=pm, graph=True).panorama.cpu().numpy()) == want
+    st.release_graphs()

@@ -840,3 +840,24 @@ def test_cascade_features_and_stitch_identical(gpu, parrington, monkeypatch):
         st.release_graphs()
     for a, b in zip(res["0"], res["1"]):
         assert a.tobytes() == b.tobytes()
+
+
+def test_descriptor_register_budgets_identical(gpu, parrington, monkeypatch):
+    """descriptor_wave is built for 3 and 4 waves per SIMD (chosen by the base octave's size);
+    both budgets give the same descriptor bytes and norms (the histogram sums are integers, so
+    the sample -> lane schedule cannot change them)."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    _, frames, focals, _ = parrington
+    res = {}
+    for occ in ("3", "4"):
+        monkeypatch.setenv("PANO_DESC_OCC", occ)
+        st = Stitcher("sift")
+        dev = st.upload(frames[:4])
+        cyl, _ = st.cylindrical(dev, focals[:4])
+        k, d, c = st.features(cyl)
+        cnt = c.cpu().numpy()
+        dh = d.cpu().numpy()
+        res[occ] = (cnt, [dh[i, :cnt[i]] for i in range(len(cnt))])
+    assert np.array_equal(res["3"][0], res["4"][0])
+    for a, b in zip(res["3"][1], res["4"][1]):
+        assert a.tobytes() == b.tobytes()

@@ -97,6 +97,7 @@ SIGNATURES = {
     "pano_ctx_set_stream": (_I, [_P, _P]),
     "pano_ctx_reserve": (_I, [_P, _I, _I, _I, _I]),
     "pano_sync": (_I, [_P]),
+    "pano_ctx_release_scratch": (_I, [_P]),
     "pano_last_error": (ctypes.c_char_p, [_P]),
     "pano_ctx_generation": (ctypes.c_uint64, [_P]),
     "pano_version": (ctypes.c_char_p, []),
@@ -219,6 +220,11 @@ class Context:
 
     def sync(self):
         self.check(self.lib.pano_sync(self.h))
+
+    def release_scratch(self):
+        """Free the scratch this context grew (pano_ctx_release_scratch); graphs captured
+        before are stale afterwards (the generation changes)."""
+        self.check(self.lib.pano_ctx_release_scratch(self.h))
 
     def generation(self) -> int:
         """Scratch generation (include/pano.h): changes when the context re-allocates scratch,

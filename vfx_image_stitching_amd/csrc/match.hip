@@ -582,21 +582,31 @@ row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
 #ifndef PANO_I8_QLDS
 #define PANO_I8_QLDS 1                   // query tile in LDS (0: in registers)
 #endif
+#ifndef PANO_I8_STAGGER
+#define PANO_I8_STAGGER 1                // waves 4-7 run each tile's epilogue one barrier late
+#endif
 #ifndef PANO_I8_WAVES
 #define PANO_I8_WAVES 4                  // 4 waves per SIMD (two workgroups per CU): measured 2.87 -> 2.57 ms at 1080p
 #endif
+// The per-row constants R = |a|^2 - 256 sum(a) (query rows) and C = |b|^2 - 256 sum(b)
+// (candidate rows) are formed while the rows are staged: the lanes staging one row sum its
+// bytes with v_dot4_u32_u8 and a shuffle reduction (no separate row_consts launch; with
+// PANO_I8_QLDS=0 the query rows stay in registers and row_consts still runs).
 template <bool SECOND>
 __global__ void __launch_bounds__(512, PANO_I8_WAVES)
-dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
+dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, const int32_t *__restrict__ cst,
         const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
         int n_split) {
     __shared__ __attribute__((aligned(16))) unsigned char Bs2[2][BT * BPI];
-    __shared__ __attribute__((aligned(16))) int Cs2[2][BT];
+    __shared__ __attribute__((aligned(16))) int Cs2[3][BT];   // C32 of tile t in Cs2[t % 3] (a lagging epilogue reads t - 1)
 #if PANO_I8_QLDS
     // the query tile (B operand of every MFMA) in LDS, sign-flipped once: read per tile
     // instead of held in 32 VGPRs (register pressure spilled the staging state to scratch
     // inside the tile loop)
     __shared__ __attribute__((aligned(16))) unsigned char Qs[QT * BPI];
+    // R of query row r sits in the row's pitch padding (bytes 128..131), so the workgroup's
+    // LDS stays within half a CU (two workgroups per CU)
+    auto rq = [&](int r) -> int & { return *(int *)(Qs + r * BPI + PANO_DESC_DIM); };
 #endif
     struct IPart { int best, idx, second; };
     __shared__ IPart red[2][QT];
@@ -615,12 +625,21 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
     const uint8_t *dB = desc + (size_t)fb * cap * PANO_DESC_DIM;
     // query fragments (B operand): rows i0 + wi 64 + m 32 + lr, K step k = bytes 32 k + 16 lh
 #if PANO_I8_QLDS
-    for (int e = tid; e < QT * (PANO_DESC_DIM / 16); e += 512) {   // 16-byte pieces
+    for (int e = tid; e < QT * (PANO_DESC_DIM / 16); e += 512) {   // 16-byte pieces, 8 lanes a row
         const int r = e >> 3, q = e & 7, row = i0 + r;
         uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
         if (row < NA) v = *(const uint4 *)(dA + (size_t)row * PANO_DESC_DIM + 16 * q);
         *(uint4 *)(Qs + r * BPI + 16 * q) = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u,
                                                        v.z ^ 0x80808080u, v.w ^ 0x80808080u);
+        unsigned int sum = 0;
+        sum = __builtin_amdgcn_udot4(v.x, 0x01010101u, sum, false);
+        sum = __builtin_amdgcn_udot4(v.y, 0x01010101u, sum, false);
+        sum = __builtin_amdgcn_udot4(v.z, 0x01010101u, sum, false);
+        sum = __builtin_amdgcn_udot4(v.w, 0x01010101u, sum, false);
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        sum += __shfl_xor(sum, 4);
+        if (q == 0 && row < NA) rq(r) = norms[(size_t)fa * cap + row] - 256 * (int)sum;
     }
     auto qfrag = [&](int m, int k) {
         return *(const i32x4 *)(Qs + (wi * 64 + m * 32 + lr) * BPI + 32 * k + 16 * lh);
@@ -640,40 +659,97 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
     }
     auto qfrag = [&](int m, int k) { return fi[m][k]; };
 #endif
-    // candidate tile staging: thread t copies row t % 128, bytes 32 (t / 128) .. + 32, with
-    // the sign flip; the first quarter also its C
+    // candidate tile staging: four adjacent lanes copy one row (thread t: row t / 4, bytes
+    // 32 (t % 4) .. + 32), with the sign flip; the row's C from their byte sums
+#if PANO_I8_QLDS
+    const int sr = tid >> 2, sp = tid & 3;
+#else
     const int sr = tid & (BT - 1), sp = tid / BT;
+#endif
     uint4 pre[2];
     int pre_c = kPadC;
     auto fetch = [&](int jt) {
         const int row = jt * BT + sr;
         pre[0] = pre[1] = make_uint4(0u, 0u, 0u, 0u);
-        pre_c = kPadC;                                  // past the count: never a best
         if (row < NB) {
             const uint4 *src = (const uint4 *)(dB + (size_t)row * PANO_DESC_DIM + 32 * sp);
             pre[0] = src[0];
             pre[1] = src[1];
-            if (sp == 0) pre_c = cst[(size_t)fb * cap + row] + (1 << 22);
         }
+#if PANO_I8_QLDS
+        unsigned int sum = 0;
+        const unsigned int w[8] = {pre[0].x, pre[0].y, pre[0].z, pre[0].w, pre[1].x, pre[1].y, pre[1].z, pre[1].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum = __builtin_amdgcn_udot4(w[i], 0x01010101u, sum, false);
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        pre_c = row < NB ? norms[(size_t)fb * cap + row] - 256 * (int)sum + (1 << 22)
+                         : kPadC;                       // past the count: never a best
+#else
+        pre_c = row < NB && sp == 0 ? cst[(size_t)fb * cap + row] + (1 << 22) : kPadC;
+#endif
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int cbuf) {
         uint4 *d4 = (uint4 *)(Bs2[buf] + sr * BPI + 32 * sp);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
             d4[q] = make_uint4(pre[q].x ^ 0x80808080u, pre[q].y ^ 0x80808080u, pre[q].z ^ 0x80808080u,
                                pre[q].w ^ 0x80808080u);
-        if (sp == 0) Cs2[buf][sr] = pre_c * 32 + key_idx(sr);      // C32: the key's base
+        if (sp == 0) Cs2[cbuf][sr] = pre_c * 32 + key_idx(sr);     // C32: the key's base
     };
     int best[2] = {kBig, kBig}, second[2] = {kBig, kBig};
     int bj[2] = {0x7fffffff, 0x7fffffff};
-    int jt = blockIdx.x, cur = 0;
+    i32x16 acc[2][2];
+    // the epilogue of one tile: its least / second-least key per query row folded into the
+    // running state (keys are unique per lane; tiles come in increasing j, so strict < keeps
+    // the first index on a tie)
+    auto epilogue = [&](const int *Cs, int jt_e) {
+        const int jb = jt_e * BT + wj * 64 + 4 * lh;
+        int tb[2] = {0x7fffffff, 0x7fffffff}, ts[2] = {0x7fffffff, 0x7fffffff};
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            // C32 of this lane's 16 candidate rows: rows (r & 3) + 8 (r >> 2) + 4 lh of block a
+            int cj[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int4 c4 = *(const int4 *)(&Cs[wj * 64 + a * 32 + 8 * g + 4 * lh]);
+                cj[4 * g] = c4.x; cj[4 * g + 1] = c4.y; cj[4 * g + 2] = c4.z; cj[4 * g + 3] = c4.w;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = mad_i24(acc[a][b][r], -64, cj[r]);
+                    if (SECOND) ts[b] = med3_i32(tb[b], key, ts[b]);
+                    tb[b] = min(tb[b], key);
+                }
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int d1 = tb[b] >> 5, idx = tb[b] & 31;   // arithmetic shift: floor(key / 32)
+            const int j = jb + (idx >> 4) * 32 + ((idx >> 2) & 3) * 8 + (idx & 3);
+            if (SECOND) {
+                const int d2 = ts[b] >> 5;
+                second[b] = d1 < best[b] ? min(best[b], d2) : min(second[b], d1);
+            }
+            bj[b] = d1 < best[b] ? j : bj[b];
+            best[b] = min(best[b], d1);
+        }
+    };
+    // Stagger (MI355X_MICROARCH "two waves per SIMD", item 9): a SIMD holds waves w and w + 4
+    // of a workgroup, which would otherwise reach their MFMAs and their VALU epilogues
+    // together.  Waves 4-7 pass each tile's barrier before that tile's epilogue, the others
+    // after it (the same number of barriers; the accumulators wait across it), so one wave's
+    // epilogue runs beside its partner's MFMAs.  C32 is triple-buffered: a late epilogue of
+    // tile t runs while tile t + 2 is staged.
+    const bool lag = PANO_I8_STAGGER && wj == 1;
+    int jt = blockIdx.x, cur = 0, c3 = 0;
     fetch(jt);
-    store(0);
+    store(0, 0);
     if (jt + n_split < n_jt) fetch(jt + n_split);
-    for (; jt < n_jt; jt += n_split, cur ^= 1) {
-        __syncthreads();        // tile jt complete in buffer cur; every wave done with cur ^ 1
+    __syncthreads();                // tile jt complete in buffer cur
+    for (; jt < n_jt; jt += n_split, cur ^= 1, c3 = c3 == 2 ? 0 : c3 + 1) {
         const unsigned char *Bs = Bs2[cur];
-        i32x16 acc[2][2];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             i32x4 fj[2], fq[2];
@@ -690,43 +766,13 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
                                                                       k == 0 ? i32x16{} : acc[a][b], 0, 0, 0);
         }
         if (jt + n_split < n_jt) {
-            store(cur ^ 1);
+            store(cur ^ 1, c3 == 2 ? 0 : c3 + 1);
             if (jt + 2 * n_split < n_jt) fetch(jt + 2 * n_split);
         }
-        const int jb = jt * BT + wj * 64 + 4 * lh;
-        // this tile's least / second-least key per query row (keys are unique per lane)
-        int tb[2] = {0x7fffffff, 0x7fffffff}, ts[2] = {0x7fffffff, 0x7fffffff};
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            // C32 of this lane's 16 candidate rows: rows (r & 3) + 8 (r >> 2) + 4 lh of block a
-            int cj[16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int4 c4 = *(const int4 *)(&Cs2[cur][wj * 64 + a * 32 + 8 * g + 4 * lh]);
-                cj[4 * g] = c4.x; cj[4 * g + 1] = c4.y; cj[4 * g + 2] = c4.z; cj[4 * g + 3] = c4.w;
-            }
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = mad_i24(acc[a][b][r], -64, cj[r]);
-                    if (SECOND) ts[b] = med3_i32(tb[b], key, ts[b]);
-                    tb[b] = min(tb[b], key);
-                }
-        }
-        // fold the tile into the running state: tiles come in increasing j, so strict < keeps
-        // the first index on a tie
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int d1 = tb[b] >> 5, idx = tb[b] & 31;   // arithmetic shift: floor(key / 32)
-            const int j = jb + (idx >> 4) * 32 + ((idx >> 2) & 3) * 8 + (idx & 3);
-            if (SECOND) {
-                const int d2 = ts[b] >> 5;
-                second[b] = d1 < best[b] ? min(best[b], d2) : min(second[b], d1);
-            }
-            bj[b] = d1 < best[b] ? j : bj[b];
-            best[b] = min(best[b], d1);
-        }
+        // past this barrier: tile jt + n_split complete in cur ^ 1, every wave done with cur
+        if (lag) __syncthreads();
+        epilogue(Cs2[c3], jt);
+        if (!lag) __syncthreads();
     }
     auto imerge = [](int &b, int &j, int &s, int b2, int j2, int s2) {
         if (b2 < b || (b2 == b && j2 < j)) {
@@ -751,7 +797,11 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ cst,
         imerge(x.best, x.idx, x.second, y.best, y.idx, y.second);
         const int gi = i0 + tid;
         if (gi < NA) {
+#if PANO_I8_QLDS
+            const int ra = rq(tid);
+#else
             const int ra = cst[(size_t)fa * cap + gi];
+#endif
             const float db = x.best >= kNone ? INFINITY : (float)(ra + x.best);
             const float ds = x.second >= kNone ? INFINITY : (float)(ra + x.second);
             parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{db, x.idx, ds};
@@ -895,17 +945,19 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
             if (rc) return rc;
             parts = (Part *)ctx->mscratch;
             int32_t *cst = (int32_t *)((char *)ctx->mscratch + part_bytes);
-            {
-                PanoProf prof_(ctx, PK_NORMS);
-                row_consts<<<dim3(nf, (cap + 63) / 64), 256, 0, ctx->stream>>>(desc, norms, counts, cap, cst);
+            if (!PANO_I8_QLDS) {   // the row constants are formed in dist_i8's staging otherwise
+                {
+                    PanoProf prof_(ctx, PK_NORMS);
+                    row_consts<<<dim3(nf, (cap + 63) / 64), 256, 0, ctx->stream>>>(desc, norms, counts, cap, cst);
+                }
+                PANO_LAUNCH_CHECK(ctx, "row_consts");
             }
-            PANO_LAUNCH_CHECK(ctx, "row_consts");
             {
                 PanoProf prof_(ctx, PK_DIST_MFMA);
                 if (p2)
-                    dist_i8<true><<<grid, 512, 0, ctx->stream>>>(desc, cst, counts, cap, pa, parts, n_split);
+                    dist_i8<true><<<grid, 512, 0, ctx->stream>>>(desc, norms, cst, counts, cap, pa, parts, n_split);
                 else
-                    dist_i8<false><<<grid, 512, 0, ctx->stream>>>(desc, cst, counts, cap, pa, parts, n_split);
+                    dist_i8<false><<<grid, 512, 0, ctx->stream>>>(desc, norms, cst, counts, cap, pa, parts, n_split);
             }
             PANO_LAUNCH_CHECK(ctx, "dist_i8");
         } else {

@@ -136,6 +136,43 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     return PANO_OK;
 }
 
+int pano_ctx_release_scratch(pano_ctx *ctx) {
+    if (!ctx) return PANO_E_ARG;
+    if (ctx->capturing) return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_ctx_release_scratch inside a graph capture");
+    sift_join_tail(ctx);
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return pano_hip_check(ctx, e, "release sync");
+    struct Slot { void **p; size_t *bytes; };
+    size_t dummy = 0;
+    const Slot slots[] = {
+        {(void **)&ctx->pyr, &ctx->pyr_bytes},           {(void **)&ctx->cands, &ctx->cand_cap},
+        {(void **)&ctx->raw, &ctx->raw_cap},             {(void **)&ctx->counters, &ctx->counters_n},
+        {(void **)&ctx->frame_off, &ctx->ext_bytes},     {(void **)&ctx->sorted, &ctx->sorted_bytes},
+        {(void **)&ctx->dorder, &ctx->dorder_bytes},     {(void **)&ctx->gray, &ctx->gray_bytes},
+        {(void **)&ctx->boxslots, &ctx->boxslots_bytes}, {&ctx->mscratch, &ctx->mscratch_bytes},
+        {&ctx->hmscratch, &ctx->hmscratch_bytes},        {(void **)&ctx->flags, &ctx->flags_bytes},
+        {&ctx->hscratch, &ctx->hscratch_bytes},          {&ctx->bscratch, &ctx->bscratch_bytes},
+        {&ctx->jscratch, &ctx->jscratch_bytes},          {(void **)&ctx->raw_sorted, &dummy},
+    };
+    for (const Slot &s : slots) {
+        if (*s.p) (void)hipFree(*s.p);
+        *s.p = nullptr;
+        *s.bytes = 0;
+    }
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->jev[i]) (void)hipEventSynchronize(ctx->jev[i]);
+        if (ctx->jpin[i]) (void)hipHostFree(ctx->jpin[i]);
+        ctx->jpin[i] = nullptr;
+        ctx->jpin_bytes[i] = 0;
+    }
+    ctx->dog = nullptr;
+    ctx->jstats = nullptr;
+    ctx->jstats_n = 0;
+    ctx->n = ctx->h = ctx->w = 0;
+    ++ctx->generation;                   // every captured graph points at freed memory now
+    return PANO_OK;
+}
+
 int pano_ctx_set_stream(pano_ctx *ctx, void *stream) {
     if (!ctx) return PANO_E_ARG;
     sift_join_tail(ctx);

@@ -1213,13 +1213,21 @@ __device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ coun
     return false;
 }
 
-#ifndef PANO_DESC_OCC
-#define PANO_DESC_OCC 3               // waves per SIMD the register budget is sized for (measured:
-                                      // 3 -> 168 VGPRs, no spills, 250-257 us parrington; 4 -> 128
-                                      // VGPRs with spills, 260 us; 5 -> 264 us)
-#endif
-template <bool OUT_U8>
-__global__ void __launch_bounds__(64 * kDescWaves, PANO_DESC_OCC)
+// OCC: waves per SIMD the register budget is sized for.  Measured (same box): at parrington
+// 3 -> 168 VGPRs, no spills, 250-257 us against 4 -> 128 VGPRs with spills, 260 us (5: 264 us);
+// at 1080p the other way, 3.25 ms at 3 against 3.12 ms at 4.  Both are built and the launch
+// picks by the size of the base octave (desc_occ).
+constexpr long long kDescOcc4Px = 4 << 20;   // base-octave pixels from which OCC 4 is used
+
+// PANO_DESC_OCC=3|4 forces the budget (read per call, for the A/B tests).
+static int desc_occ(long long base_px) {
+    const char *e = getenv("PANO_DESC_OCC");
+    if (e && (e[0] == '3' || e[0] == '4') && !e[1]) return e[0] - '0';
+    return base_px >= kDescOcc4Px ? 4 : 3;
+}
+
+template <bool OUT_U8, int OCC>
+__global__ void __launch_bounds__(64 * kDescWaves, OCC)
 descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int32_t *__restrict__ counts, int n_frames, int cap, int32_t *__restrict__ work,
                 float *__restrict__ desc, uint8_t *__restrict__ desc_u8, int32_t *__restrict__ norms,
@@ -1918,26 +1926,36 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
             PANO_LAUNCH_CHECK(ctx, "desc_order");
         }
     }
-    static int resident = 0;
-    if (!resident) {
+    const int occ = desc_occ((long long)pa.H[0] * pa.W[0]);
+    static int resident[2] = {0, 0};
+    int &res = resident[occ == 4];
+    if (!res) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, descriptor_wave<true>, 64 * kDescWaves, 0) != hipSuccess ||
+        const hipError_t e = occ == 4
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, descriptor_wave<true, 4>, 64 * kDescWaves, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, descriptor_wave<true, 3>, 64 * kDescWaves, 0);
+        if (e != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
             per_cu <= 0 || cus <= 0)
             per_cu = 4, cus = 256;
-        resident = per_cu * cus;
+        res = per_cu * cus;
     }
     const size_t slots = ((size_t)n * cap + kDescWaves - 1) / kDescWaves;
     const unsigned blocks = (unsigned)std::max<size_t>(
-        8, std::min<size_t>((slots + 7) & ~size_t(7), (size_t)resident & ~size_t(7)));
+        8, std::min<size_t>((slots + 7) & ~size_t(7), (size_t)res & ~size_t(7)));
     {
         PanoProf prof_(ctx, PK_DESC);
-        if (desc_u8)
-            descriptor_wave<true><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
-                pa, dp, kps, counts, n, cap, desc_work, nullptr, desc_u8, norms, order);
-        else
-            descriptor_wave<false><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
-                pa, dp, kps, counts, n, cap, desc_work, desc, nullptr, nullptr, order);
+        auto go = [&](auto occ_c) {
+            constexpr int O = decltype(occ_c)::value;
+            if (desc_u8)
+                descriptor_wave<true, O><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                    pa, dp, kps, counts, n, cap, desc_work, nullptr, desc_u8, norms, order);
+            else
+                descriptor_wave<false, O><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                    pa, dp, kps, counts, n, cap, desc_work, desc, nullptr, nullptr, order);
+        };
+        if (occ == 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 3>{});
     }
     PANO_LAUNCH_CHECK(ctx, "descriptor");
     return PANO_OK;
