@@ -303,7 +303,10 @@ extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
 // are gathered in a per-wave LDS buffer and appended with one atomic per flush.
 constexpr int XSW = 62;          // output columns per strip
 constexpr int XSR = 32;          // output rows per item (default; PANO_EXTREMA_XSR=16 halves it)
-constexpr int XPD = 3;           // rows prefetched ahead
+#ifndef PANO_XPD
+#define PANO_XPD 3
+#endif
+constexpr int XPD = PANO_XPD;    // rows prefetched ahead
 
 struct XArgs {
     const float *dog[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
@@ -1163,6 +1166,13 @@ constexpr int kDescWaves = 4;         // waves (keypoints in flight) per workgro
 constexpr int kDescCols = 128;        // patch sides up to this use the dense index (default
                                       // parameters: side <= 73)
 constexpr int kHist = 6 * 6 * 8;      // padded histogram (reference: tensor of (ww+2, ww+2, nb))
+#ifndef PANO_DESC_SKEW
+#define PANO_DESC_SKEW 2              // u64 slots between histogram copies beyond kHist
+#endif
+// copy stride: kHist u64 is 576 dwords, a multiple of the 32 banks an LDS atomic's lane group
+// spreads over, so without the skew the copies alias bank for bank and the two lanes of a
+// pair (same row, adjacent strips: often the same bin) collide on a bank at different addresses
+constexpr int kHistStride = kHist + PANO_DESC_SKEW;
 constexpr float kFix = 4194304.0f;    // 2^22: contributions <= 255 sqrt(2) fit a u32
 #ifndef PANO_DESC_SW
 #define PANO_DESC_SW 4                // patch columns per strip: one (SW + 2)-float load per step
@@ -1176,9 +1186,10 @@ constexpr int kDescSW = PANO_DESC_SW;
 #endif
 constexpr int kDescGrp = PANO_DESC_GRP;
 constexpr int kDescSS = kDescSW * kDescGrp;   // columns of a group's super-strip
-// a group's lanes bin into different histogram copies: no same-address atomics among them
-constexpr int kDescCopies = PANO_DESC_COPIES > kDescGrp ? PANO_DESC_COPIES : kDescGrp;
-static_assert(kDescSS <= 16 && (kDescGrp & (kDescGrp - 1)) == 0, "super-strip divides 64");
+// copy = lane % copies: the two lanes of a pair (default) bin into different copies, so they
+// issue no same-address atomics (wider groups share copies: measured, the LDS is hidden)
+constexpr int kDescCopies = PANO_DESC_COPIES;
+static_assert(kDescSS <= 64 && (kDescGrp & (kDescGrp - 1)) == 0, "super-strip divides 64");
 
 static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "strip width divides 64");
 #ifndef PANO_DESC_ABL
@@ -1232,12 +1243,12 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int32_t *__restrict__ counts, int n_frames, int cap, int32_t *__restrict__ work,
                 float *__restrict__ desc, uint8_t *__restrict__ desc_u8, int32_t *__restrict__ norms,
                 const int32_t *__restrict__ order) {
-    __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHist];
+    __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHistStride];
     __shared__ int col_lo[kDescWaves][kDescCols / kDescSS], col_pre[kDescWaves][kDescCols / kDescSS + 1];   // per super-strip
     __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     unsigned long long *h0 = hist[wv];
-    unsigned long long *h = h0 + (lane & (kDescCopies - 1)) * kHist;   // this lane's copy
+    unsigned long long *h = h0 + (lane & (kDescCopies - 1)) * kHistStride;   // this lane's copy
     int *clo = col_lo[wv], *cpre = col_pre[wv];
     float *cbr = col_br[wv], *cbc = col_bc[wv];
     // XCD-aware split (workgroup b runs on XCD b % 8): each XCD takes one contiguous eighth of
@@ -1271,7 +1282,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         if (fi.regs) fi.locate(gk, f, k);
         else if (!locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
         if (order) k = order[(size_t)f * cap + k];     // locality order (desc_order)
-        for (int i = lane; i < kDescCopies * kHist; i += 64) h0[i] = 0ull;
+        for (int i = lane; i < kDescCopies * kHistStride; i += 64) h0[i] = 0ull;
         const pano_kp kp = kps[(size_t)f * cap + k];
         int oct = kp.octave & 255;
         if (oct >= 128) oct |= -128;
@@ -1523,7 +1534,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const int e = ((i >> 5) + 1) * 48 + (((i >> 3) & 3) + 1) * 8 + (i & 7);
             unsigned long long v = 0;
 #pragma unroll
-            for (int c = 0; c < kDescCopies; ++c) v += h0[c * kHist + e];
+            for (int c = 0; c < kDescCopies; ++c) v += h0[c * kHistStride + e];
             return (float)((double)v * (1.0 / 4194304.0));
         };
         float lo = interior(lane), hi = interior(64 + lane);
