@@ -78,10 +78,10 @@ cyl_columns(int w, FocalArg focal, int2 *__restrict__ cols, uint8_t *__restrict_
     const double fl = focal.f[f];
     const int cx = w / 2, k = xp - cx;
     {
-        // per SOURCE column x = xp: sqrt(xd^2 + f^2) and its ratio to f, the row map's
-        // column constants (cyl_inverse reads them instead of recomputing per pixel)
+        // per SOURCE column x = xp: 1 / sqrt(xd^2 + f^2) and sqrt(xd^2 + f^2) / f, the row
+        // map's column constants (cyl_inverse reads them instead of recomputing per pixel)
         const double den = sqrt((double)k * (double)k + fl * fl);
-        colden[(size_t)f * w + xp] = make_double2(den, den / fl);
+        colden[(size_t)f * w + xp] = make_double2(1.0 / den, den / fl);
     }
     // inverse images of k -+ 1/2 (arguments kept inside the atan range; clamped to the frame)
     const double lim = 1.5707963267948966 - 1e-12;
@@ -116,15 +116,28 @@ cyl_inverse(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const in
     const int2 cr = cols[(size_t)f * w + xp];
     long best = -1;                                   // largest row-major source index
     for (int x = cr.x; x <= cr.y; ++x) {
-        const double2 ds = colden[(size_t)f * w + x];     // the same two roundings, once per column
-        const double den = ds.x, s = ds.y;
+        const double2 ds = colden[(size_t)f * w + x];
+        const double inv_den = ds.x, s = ds.y;
         // rows whose forward y' can be k: a box around [(k - 1/2) s, (k + 1/2) s], scanned
         // from the top (the first hit is this column's largest row)
         const int r1 = (int)ceil((k + 0.5) * s) + 1, r0 = (int)floor((k - 0.5) * s) - 1;
         for (int yd = r1; yd >= r0; --yd) {
             const int y = yd + cy;
             if (y < 0 || y >= h) continue;
-            const int ym = (int)rint(fl * ((double)yd / den)) + cy;
+            // the forward map rint(f (yd / den)) in f64: yd * (1 / den) is within a few ulp of
+            // the quotient, so its rounding is the same unless the product lies within 1e-9 of
+            // a half-integer; there the exact expression decides (the reference's division)
+            const double v = fl * ((double)yd * inv_den);
+            const double t = v - floor(v);
+            double ymd;
+            if (fabs(t - 0.5) < 1e-9) {
+                const int xd = x - w / 2;
+                const double den = sqrt((double)xd * (double)xd + fl * fl);
+                ymd = rint(fl * ((double)yd / den));
+            } else {
+                ymd = rint(v);
+            }
+            const int ym = (int)ymd + cy;
             if (ym != yp) continue;
             const long li = (long)y * w + x;
             if (li > best) best = li;

@@ -116,6 +116,10 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->xside) (void)hipStreamSynchronize(ctx->xside);
+    if (ctx->xside) (void)hipStreamDestroy(ctx->xside);
+    if (ctx->ev_x_fork) (void)hipEventDestroy(ctx->ev_x_fork);
+    if (ctx->ev_x_join) (void)hipEventDestroy(ctx->ev_x_join);
     if (ctx->lvl_side) (void)hipStreamSynchronize(ctx->lvl_side);
     if (ctx->lvl_side) (void)hipStreamDestroy(ctx->lvl_side);
     for (hipEvent_t e : ctx->ev_lvl)
@@ -140,6 +144,7 @@ int pano_ctx_release_scratch(pano_ctx *ctx) {
     if (!ctx) return PANO_E_ARG;
     if (ctx->capturing) return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_ctx_release_scratch inside a graph capture");
     sift_join_tail(ctx);
+    sift_join_x(ctx);
     hipError_t e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return pano_hip_check(ctx, e, "release sync");
     struct Slot { void **p; size_t *bytes; };
@@ -223,9 +228,13 @@ int pano_sift(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     if (!ctx) return PANO_E_ARG;
     pano_sift_params p;
     if (params) p = *params; else pano_sift_default_params(&p);
+    ctx->early_armed = true;
     int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
+    ctx->early_armed = false;
     if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, desc, nullptr, nullptr, cap, counts);
-    sift_join_tail(ctx);                  // no-op unless an error left the tail unjoined
+    sift_join_tail(ctx);
+    sift_join_x(ctx);
+    ctx->early_oct = -1;                  // no-op unless an error left the tail unjoined
     return rc;
 }
 
@@ -236,9 +245,13 @@ int pano_sift_u8(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     if (!desc_u8 || !norms) return pano_fail(ctx, PANO_E_ARG, "pano_sift_u8: bad outputs");
     pano_sift_params p;
     if (params) p = *params; else pano_sift_default_params(&p);
+    ctx->early_armed = true;
     int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
+    ctx->early_armed = false;
     if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, nullptr, desc_u8, norms, cap, counts);
     sift_join_tail(ctx);
+    sift_join_x(ctx);
+    ctx->early_oct = -1;
     return rc;
 }
 

@@ -119,6 +119,13 @@ struct pano_ctx {
     hipStream_t lvl_side = nullptr;
     hipEvent_t ev_lvl[PANO_MAX_OCTAVES] = {};
     hipEvent_t ev_lvl_join = nullptr;
+    // third stream: the extrema scan of an octave launched right after its blur (early
+    // extrema, PANO_EARLY_EXTREMA), beside the next octaves' blur; joined before localize
+    hipStream_t xside = nullptr;
+    hipEvent_t ev_x_fork = nullptr, ev_x_join = nullptr;
+    bool x_pending = false;              // extrema enqueued on `xside`, not yet joined
+    bool early_armed = false;            // pano_sift(_u8): the pyramid may start the extrema
+    int early_oct = -1;                  // last octave whose extrema went out early (-1: none)
     int o_tail = 0;                      // first octave of the tail
     bool pyr_full = false;               // every Gaussian level materialised (see launch_sift_pyramid)
     // ---- hipGraph capture (pano_graph_begin / end)
@@ -136,6 +143,13 @@ inline void sift_join_tail(pano_ctx *ctx) {
     if (!ctx->tail_pending) return;
     (void)hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0);
     ctx->tail_pending = false;
+}
+
+// Make ctx->stream wait for pending early extrema (no-op otherwise).
+inline void sift_join_x(pano_ctx *ctx) {
+    if (!ctx->x_pending) return;
+    (void)hipStreamWaitEvent(ctx->stream, ctx->ev_x_join, 0);
+    ctx->x_pending = false;
 }
 
 // RAII: records a start/stop hipEvent pair on the context's stream around one launch
@@ -202,6 +216,10 @@ struct PyrSource {
 };
 int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, int w,
                             const pano_sift_params *p, bool defer_tail, bool full);
+// The extrema scan of octave o on the xside stream, forked from ctx->stream (whose work up to
+// here wrote octave o's DoG levels); called by the pyramid when early_armed.  The octaves must
+// come in order from 0; the keypoint stage then skips them and joins before localize.
+int sift_early_extrema(pano_ctx *ctx, const pano_sift_params *p, int o);
 int sift_reserve_dims(pano_ctx *ctx, int n, int H0, int W0, int max_oct, int nl);
 int launch_sift_dog(pano_ctx *ctx);
 // Raw oriented keypoints (find_scale_space_extrema) of the resident pyramid in the

@@ -536,6 +536,10 @@ localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
 constexpr int kOriCopies = PANO_ORI_COPIES;
 constexpr float kInv360 = 1.0f / 360.0f;   // RN(1 / 360)
 constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
+#ifndef PANO_ORI_STAGE
+#define PANO_ORI_STAGE 12
+#endif
+constexpr int kOriStage = PANO_ORI_STAGE;   // patch loads per lane in flight (37^2 / 64 <= 22: two rounds)
 
 struct OriParams {
     double scale_factor, radius_factor, peak_ratio;
@@ -634,11 +638,24 @@ __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H,
         const int P = side + 2;
         const bool staged = P <= kOriPatch;
         if (staged) {
+            // kOriStage loads per lane in flight before their LDS stores (a plain loop waited
+            // for each load in turn: one memory latency per 64 elements, up to 22 per candidate)
             const int by = cy - radius - 1, bx = cx - radius - 1;
-            for (int e = lane; e < P * P; e += 64) {
-                const int r = e / P, c = e - (e / P) * P;
-                const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
-                pt[r * kOriPatch + c] = img[(size_t)yy * W + xx];
+            for (int e0 = 0; e0 < P * P; e0 += 64 * kOriStage) {
+                float v[kOriStage];
+#pragma unroll
+                for (int u = 0; u < kOriStage; ++u) {
+                    const int e = e0 + 64 * u + lane;
+                    const int r = e / P, c = e - (e / P) * P;
+                    const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
+                    v[u] = e < P * P ? img[(size_t)yy * W + xx] : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < kOriStage; ++u) {
+                    const int e = e0 + 64 * u + lane;
+                    const int r = e / P, c = e - (e / P) * P;
+                    if (e < P * P) pt[r * kOriPatch + c] = v[u];
+                }
             }
         }
         wave_sync_lds();
@@ -1678,40 +1695,178 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
                        const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
                        int32_t *norms);
 
+// Scratch of the keypoint stage (per-frame capacities scaled with the pyramid, see kExtMin)
+// and the counter block: [err] [cand f] [raw f] [ext f] [descriptor, orientation work queues
+// per XCD x 8 each], one line apiece.
+struct KpBufs {
+    size_t ext_cap, cand_cap, raw_cap, cnt_ints;
+    uint64_t *raw_ext;
+    int32_t *err, *cand_cnt, *raw_cnt, *ext_cnt, *desc_work, *ori_work;
+};
+
+int kp_bufs(pano_ctx *ctx, KpBufs &b) {
+    const int n = ctx->n, no = ctx->n_oct;
+    size_t spo = 0;
+    for (int o = 0; o < no; ++o) spo += (size_t)ctx->oct_h[o] * ctx->oct_w[o];
+    b.ext_cap = std::max<size_t>(kExtMin, ((spo / 32) + 1023) & ~size_t(1023));
+    b.cand_cap = std::max<size_t>(kCandMin, b.ext_cap / 4);
+    b.raw_cap = b.cand_cap;
+    int rc = pano_grow(ctx, (void **)&ctx->cands, &ctx->cand_cap, b.cand_cap * n * sizeof(Cand));
+    if (rc) return rc;
+    rc = pano_grow(ctx, (void **)&ctx->raw, &ctx->raw_cap, b.raw_cap * n * sizeof(RawKp));
+    if (rc) return rc;
+    rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, b.ext_cap * n * sizeof(uint64_t));
+    if (rc) return rc;
+    b.raw_ext = (uint64_t *)ctx->frame_off;
+    b.cnt_ints = (3 * (size_t)n + 1 + 16) * kCntStride;
+    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, b.cnt_ints * sizeof(int32_t));
+    if (rc) return rc;
+    b.err = ctx->counters;
+    b.cand_cnt = b.err + kCntStride;
+    b.raw_cnt = b.cand_cnt + (size_t)n * kCntStride;
+    b.ext_cnt = b.raw_cnt + (size_t)n * kCntStride;
+    b.desc_work = b.ext_cnt + (size_t)n * kCntStride;
+    b.ori_work = b.desc_work + 8 * kCntStride;
+    return PANO_OK;
+}
+
+// Rows per streaming extrema item (PANO_EXTREMA_XSR=16 halves them) and the smallest octave
+// height the streaming kernel takes (0 disables it).  Measured (same box): 96 -- parrington's
+// octave 3 joins the streaming launch instead of its own scan -- 164-167 us per extrema class
+// against 175-178 us at 192; 48 within noise of 96.
+int extrema_xsr() {
+    static const int v = [] {
+        const char *e = getenv("PANO_EXTREMA_XSR");
+        return e && atoi(e) == 16 ? 16 : XSR;
+    }();
+    return v;
+}
+int extrema_min_h() {
+    static const int v = [] {
+        const char *e = getenv("PANO_EXTREMA_STREAM_MIN_H");
+        return e ? atoi(e) : 96;
+    }();
+    return v;
+}
+
+// The streaming kernel's items (strips of xsr rows) of every octave, octave-major.
+XArgs x_args(const pano_ctx *ctx, int border) {
+    XArgs xa{};
+    const int no = ctx->n_oct, nl = ctx->n_lvl, xsr = extrema_xsr();
+    int items = 0;
+    xa.n_oct = no;
+    for (int o = 0; o < no; ++o) {
+        xa.H[o] = ctx->oct_h[o];
+        xa.W[o] = ctx->oct_w[o];
+        for (int l = 0; l < nl - 1; ++l) xa.dog[o][l] = ctx->dog + ctx->dog_off[o][l];
+        const int iw = xa.W[o] - 2 * border, ih = xa.H[o] - 2 * border;
+        xa.item_start[o] = items;
+        xa.strips_x[o] = iw > 0 ? (iw + XSW - 1) / XSW : 1;
+        if (iw > 0 && ih > 0) items += xa.strips_x[o] * ((ih + xsr - 1) / xsr);
+    }
+    xa.item_start[no] = items;
+    return xa;
+}
+
+double extrema_thresh(const pano_sift_params *p) {
+    return floor(0.5 * p->contrast_threshold / p->num_intervals * 255);
+}
+
+int launch_extrema_stream(pano_ctx *ctx, const pano_sift_params *p, const XArgs &xa, const KpBufs &b,
+                          int t0, int t1, hipStream_t st) {
+    if (t1 <= t0) return PANO_OK;
+    const int n = ctx->n, ni = p->num_intervals, xsr = extrema_xsr();
+    const double thresh = extrema_thresh(p);
+    dim3 grid((unsigned)((t1 - t0 + 3) / 4), n);
+    {
+        PanoProf prof_(ctx, PK_EXTREMA, st);
+#define PANO_EXTREMA(NLV)                                                                          \
+    (xsr == 16 ? extrema_stream<NLV, 16><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext,   \
+                                                              b.ext_cnt, (int)b.ext_cap, t0, t1)  \
+               : extrema_stream<NLV, XSR><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext,  \
+                                                               b.ext_cnt, (int)b.ext_cap, t0, t1))
+        switch (ni + 2) {
+            case 3: PANO_EXTREMA(3); break;
+            case 4: PANO_EXTREMA(4); break;
+            case 5: PANO_EXTREMA(5); break;
+            case 6: PANO_EXTREMA(6); break;
+            case 7: PANO_EXTREMA(7); break;
+            default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "num_intervals above 5");
+        }
+#undef PANO_EXTREMA
+    }
+    PANO_LAUNCH_CHECK(ctx, "extrema_stream");
+    return PANO_OK;
+}
+
+// PANO_EARLY_EXTREMA=1 (read per call): each large octave's extrema scan goes out on a third
+// stream as soon as its DoG levels exist.  Measured on MI355X (same box): bit-exact
+// but 1.44-1.46 ms per graph-replayed parrington stitch against 1.09 ms, 11.9 against 11.0 ms at
+// 1080p -- the scan's waves take the CU slots the next octaves' short blur launches (the
+// critical path) need -- so off by default.
+bool early_extrema_enabled() {
+    const char *e = getenv("PANO_EARLY_EXTREMA");
+    return e && atoi(e) != 0;
+}
+}  // namespace
+
+int sift_early_extrema(pano_ctx *ctx, const pano_sift_params *p, int o) {
+    if (!early_extrema_enabled() || o != ctx->early_oct + 1) return PANO_OK;
+    if (extrema_min_h() <= 0 || ctx->oct_h[o] < extrema_min_h()) return PANO_OK;
+    if (p->num_intervals + 2 < 3 || p->num_intervals + 2 > 7) return PANO_OK;   // the keypoint stage reports it
+    if (ctx->h > 4096 || ctx->w > 4096) return PANO_OK;
+    KpBufs b;
+    int rc = kp_bufs(ctx, b);
+    if (rc) return rc;
+    if (ctx->early_oct < 0) {               // the counters start at zero before any scan
+        rc = launch_fill(ctx, ctx->counters, 0, b.cnt_ints * sizeof(int32_t));
+        if (rc) return rc;
+    }
+    if (!ctx->xside) {
+        int lo_prio = 0, hi_prio = 0;
+        PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+        PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->xside, hipStreamNonBlocking, lo_prio));
+        PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_x_fork, hipEventDisableTiming));
+        PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_x_join, hipEventDisableTiming));
+    }
+    PANO_HIP(ctx, hipEventRecord(ctx->ev_x_fork, ctx->stream));
+    PANO_HIP(ctx, hipStreamWaitEvent(ctx->xside, ctx->ev_x_fork, 0));
+    const XArgs xa = x_args(ctx, p->border);
+    rc = launch_extrema_stream(ctx, p, xa, b, xa.item_start[o], xa.item_start[o + 1], ctx->xside);
+    if (rc) return rc;
+    PANO_HIP(ctx, hipEventRecord(ctx->ev_x_join, ctx->xside));
+    ctx->x_pending = true;
+    ctx->early_oct = o;
+    return PANO_OK;
+}
+
+namespace {
+int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &pa, const pano_kp *kps,
+                       const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
+                       int32_t *norms);
+
 // raw_out != NULL: find_scale_space_extrema only (stops after the orientations and writes the
 // raw keypoints in scan order to raw_out [n][cap]; kps / desc unused)
 int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, float *desc,
                         uint8_t *desc_u8, int32_t *norms, int cap, int32_t *counts, pano_kp *raw_out) {
     const int n = ctx->n, no = ctx->n_oct, nl = ctx->n_lvl, ni = p->num_intervals;
+    // octaves 0 .. early whose extrema the pyramid already launched (sift_early_extrema)
+    const int early = ctx->early_oct;
+    ctx->early_oct = -1;
     if (cap <= 0 || !counts || (!raw_out && (!kps || (!desc && !(desc_u8 && norms)))))
         return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
     if (n > PANO_MAX_FRAMES) return pano_fail(ctx, PANO_E_ARG, "pano_sift: more than PANO_MAX_FRAMES frames");
-    // per-frame candidate / raw capacities, scaled with the pyramid (see kExtMin)
-    size_t spo = 0;
-    for (int o = 0; o < no; ++o) spo += (size_t)ctx->oct_h[o] * ctx->oct_w[o];
-    const size_t ext_cap = std::max<size_t>(kExtMin, ((spo / 32) + 1023) & ~size_t(1023));
-    const size_t cand_cap = std::max<size_t>(kCandMin, ext_cap / 4);
-    const size_t raw_cap = cand_cap;
-    int rc = pano_grow(ctx, (void **)&ctx->cands, &ctx->cand_cap, cand_cap * n * sizeof(Cand));
+    KpBufs kb;
+    int rc = kp_bufs(ctx, kb);
     if (rc) return rc;
-    rc = pano_grow(ctx, (void **)&ctx->raw, &ctx->raw_cap, raw_cap * n * sizeof(RawKp));
-    if (rc) return rc;
-    rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, ext_cap * n * sizeof(uint64_t));
-    if (rc) return rc;
-    uint64_t *raw_ext = (uint64_t *)ctx->frame_off;
-    // [err] [cand f] [raw f] [ext f] [descriptor, orientation work queues per XCD x 8 each],
-    // one line apiece
-    const size_t cnt_ints = (3 * (size_t)n + 1 + 16) * kCntStride;
-    rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, cnt_ints * sizeof(int32_t));
-    if (rc) return rc;
-    int32_t *err = ctx->counters;
-    int32_t *cand_cnt = err + kCntStride;
-    int32_t *raw_cnt = cand_cnt + (size_t)n * kCntStride;
-    int32_t *ext_cnt = raw_cnt + (size_t)n * kCntStride;
-    int32_t *desc_work = ext_cnt + (size_t)n * kCntStride;
-    int32_t *ori_work = desc_work + 8 * kCntStride;
-    rc = launch_fill(ctx, ctx->counters, 0, cnt_ints * sizeof(int32_t));
-    if (rc) return rc;
+    const size_t ext_cap = kb.ext_cap, cand_cap = kb.cand_cap, raw_cap = kb.raw_cap;
+    uint64_t *raw_ext = kb.raw_ext;
+    int32_t *err = kb.err, *cand_cnt = kb.cand_cnt, *raw_cnt = kb.raw_cnt, *ext_cnt = kb.ext_cnt;
+    int32_t *desc_work = kb.desc_work, *ori_work = kb.ori_work;
+    if (early < 0) {
+        rc = launch_fill(ctx, ctx->counters, 0, kb.cnt_ints * sizeof(int32_t));
+        if (rc) return rc;
+    }
 
     LocParams lp;
     lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);
@@ -1741,57 +1896,12 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
     // Extrema: the streaming kernel for the large octaves (a wave walks 32 rows of a strip),
     // the LDS-tiled scan for the small ones (few rows: more, shorter workgroups win); the
     // octaves of a pending blur tail are scanned after the join.
-    static const int xsr = [] {
-        const char *e = getenv("PANO_EXTREMA_XSR");
-        return e && atoi(e) == 16 ? 16 : XSR;
-    }();
-    static const int xmin_h = [] {
-        // 0 disables the streaming kernel.  Measured (same box): 96 -- parrington's octave 3
-        // joins the streaming launch instead of its own scan -- 164-167 us per extrema class
-        // against 175-178 us at 192; 48 within noise of 96
-        const char *e = getenv("PANO_EXTREMA_STREAM_MIN_H");
-        return e ? atoi(e) : 96;
-    }();
     if (tiles > 0) {
-        XArgs xa{};
-        int items = 0;
-        xa.n_oct = no;
-        for (int o = 0; o < no; ++o) {
-            xa.H[o] = da.H[o];
-            xa.W[o] = da.W[o];
-            for (int l = 0; l < nl - 1; ++l) xa.dog[o][l] = da.dog[o][l];
-            const int iw = da.W[o] - 2 * p->border, ih = da.H[o] - 2 * p->border;
-            xa.item_start[o] = items;
-            xa.strips_x[o] = iw > 0 ? (iw + XSW - 1) / XSW : 1;
-            if (iw > 0 && ih > 0) items += xa.strips_x[o] * ((ih + xsr - 1) / xsr);
-        }
-        xa.item_start[no] = items;
+        const XArgs xa = x_args(ctx, p->border);
+        const int xmin_h = extrema_min_h();
         const int o_split = ctx->tail_pending ? ctx->o_tail : no;
         int o_s = 0;
         while (xmin_h > 0 && o_s < o_split && da.H[o_s] >= xmin_h) ++o_s;
-        auto launch_stream = [&](int t0, int t1) -> int {
-            if (t1 <= t0) return PANO_OK;
-            dim3 grid((unsigned)((t1 - t0 + 3) / 4), n);
-            {
-                PanoProf prof_(ctx, PK_EXTREMA);
-#define PANO_EXTREMA(NLV)                                                                          \
-    (xsr == 16 ? extrema_stream<NLV, 16><<<grid, 256, 0, ctx->stream>>>(xa, p->border, lp.thresh, raw_ext, \
-                                                                      ext_cnt, (int)ext_cap, t0, t1)  \
-               : extrema_stream<NLV, XSR><<<grid, 256, 0, ctx->stream>>>(xa, p->border, lp.thresh, raw_ext, \
-                                                                       ext_cnt, (int)ext_cap, t0, t1))
-                switch (ni + 2) {
-                    case 3: PANO_EXTREMA(3); break;
-                    case 4: PANO_EXTREMA(4); break;
-                    case 5: PANO_EXTREMA(5); break;
-                    case 6: PANO_EXTREMA(6); break;
-                    case 7: PANO_EXTREMA(7); break;
-                    default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "num_intervals above 5");
-                }
-#undef PANO_EXTREMA
-            }
-            PANO_LAUNCH_CHECK(ctx, "extrema_stream");
-            return PANO_OK;
-        };
         auto launch_scan = [&](int t0, int t1) -> int {
             if (t1 <= t0) return PANO_OK;
             dim3 grid(t1 - t0, n);
@@ -1812,13 +1922,15 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
             PANO_LAUNCH_CHECK(ctx, "extrema_scan");
             return PANO_OK;
         };
-        rc = launch_stream(0, xa.item_start[o_s]);
+        rc = launch_extrema_stream(ctx, p, xa, kb, xa.item_start[std::min(early + 1, o_s)], xa.item_start[o_s],
+                                   ctx->stream);
         if (rc) return rc;
         rc = launch_scan(da.tile_start[o_s], da.tile_start[o_split]);
         if (rc) return rc;
         sift_join_tail(ctx);
         rc = launch_scan(da.tile_start[o_split], tiles);
         if (rc) return rc;
+        sift_join_x(ctx);
         dim3 g2(n, (unsigned)((ext_cap + 255) / 256));
         {
             PanoProf prof_(ctx, PK_EXTREMA);

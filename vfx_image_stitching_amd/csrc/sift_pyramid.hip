@@ -1738,6 +1738,8 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
 int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, int w,
                             const pano_sift_params *p, bool defer_tail, bool full) {
     sift_join_tail(ctx);                  // a previous call's tail must finish first
+    sift_join_x(ctx);
+    ctx->early_oct = -1;
     int no, nl;
     double sb, sl[PANO_MAX_LEVELS];
     const int gh = src.base ? std::max(1, h / 2) : h, gw = src.base ? std::max(1, w / 2) : w;
@@ -2091,6 +2093,12 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
                 rc = fork();
                 if (rc) { ctx->stream = main_stream; return rc; }
             }
+        }
+        // this octave's DoG levels are complete on the main stream: its extrema scan may start
+        // beside the next octaves' (latency-bound) blur launches
+        if (ctx->early_armed && !full && !fork_lvl && o < o_side) {
+            rc = sift_early_extrema(ctx, p, o);
+            if (rc) { ctx->stream = main_stream; return rc; }
         }
     }
     ctx->stream = main_stream;
