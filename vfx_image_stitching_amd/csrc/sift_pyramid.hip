@@ -1764,7 +1764,11 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     const bool chain_on = chain_env && atoi(chain_env) != 0;
     const bool chain_taps = chain_on && nl == 6 && tl[1].n == 11 && tl[2].n == 13 && tl[3].n == 17 &&
                             tl[4].n == 21 && tl[5].n == 27;
-    auto chain_ok = [&](int o) { return chain_taps && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= 64; };
+    // PANO_BLUR_CHAIN=k (k >= 1): chains from octave k - 1 on (1: every octave)
+    const int chain_min_oct = chain_on ? atoi(chain_env) - 1 : 0;
+    auto chain_ok = [&](int o) {
+        return chain_taps && o >= chain_min_oct && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= 64;
+    };
     const bool chain_base = src.bgr && !src.base_only && chain_ok(0) && tb.n == 11;
     // streaming cascades (blur_cascade, PANO_BLUR_CASCADE=1): per octave walker A (octave 0 from
     // the gray frames: base, 1, 2; else levels 1, 2) and walker B (levels 3, 4, 5 from G2)
@@ -1845,7 +1849,12 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     }();
     const int o_side = o_tail < no ? std::max(1, o_tail - std::max(0, side_oct)) : no;
     hipStream_t main_stream = ctx->stream;
+    // PANO_TAIL_MAIN=1 (read per call): the tail on the main stream, no fork in the launch
+    // sequence (a captured graph is then one chain)
+    const char *tail_main_env = getenv("PANO_TAIL_MAIN");
+    const bool tail_main = tail_main_env && atoi(tail_main_env) != 0;
     auto fork = [&]() -> int {
+        if (tail_main) return PANO_OK;
         if (!ctx->side) {
             int lo_prio = 0, hi_prio = 0;   // numerically lower = higher priority
             PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
@@ -1874,11 +1883,13 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
             for (int l = 0; l < nl; ++l) ta.G[oi][l] = G + ctx->gauss_off[o][l];
             for (int l = 0; l + 1 < nl; ++l) ta.D[oi][l] = D + ctx->dog_off[o][l];
         }
+        hipStream_t ts = tail_main ? main_stream : ctx->side;
         {
-            PanoProf prof_(ctx, PK_BLUR, ctx->side);
-            blur_tail<<<n, kTailThreads, 0, ctx->side>>>(ta);
+            PanoProf prof_(ctx, PK_BLUR, ts);
+            blur_tail<<<n, kTailThreads, 0, ts>>>(ta);
         }
         PANO_LAUNCH_CHECK(ctx, "blur_tail");
+        if (tail_main) return PANO_OK;
         PANO_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
         ctx->tail_pending = true;
         ctx->o_tail = o_side;
@@ -1930,7 +1941,7 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     bool lvl_forked = false;
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
-        ctx->stream = o >= o_side ? ctx->side : main_stream;     // side-stream octaves
+        ctx->stream = o >= o_side && !tail_main ? ctx->side : main_stream;     // side-stream octaves
         const bool fork_lvl = oct_fork >= 0 && o >= oct_fork && o < o_side && nl >= 4 && !chain_ok(o) && !cas_ok(o);
         if (cas_ok(o)) {
             auto Gp = [&](int l) { return G + ctx->gauss_off[o][l]; };
