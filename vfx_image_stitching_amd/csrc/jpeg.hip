@@ -29,6 +29,8 @@
 // from LDS (two-level lookup, jpeg_core.h).  The host parses headers only (jpeg_host.cpp) and
 // uploads tables + entropy bytes once.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -642,8 +644,26 @@ int jpeg_last_stats(pano_ctx *ctx, int32_t *h, int n) {
     return PANO_OK;
 }
 
+// PANO_JPEG_HOST_TIMING=1 (diagnostics): host microseconds of the call's phases on stderr
+struct HostClock {
+    bool on = false;
+    std::chrono::steady_clock::time_point t0;
+    HostClock() {
+        const char *e = getenv("PANO_JPEG_HOST_TIMING");
+        on = e && atoi(e) != 0;
+        t0 = std::chrono::steady_clock::now();
+    }
+    void mark(const char *what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[jpeg host] %s %.1f us\n", what, std::chrono::duration<double, std::micro>(t - t0).count());
+        t0 = t;
+    }
+};
+
 int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const size_t *lens, uint8_t *bgr,
                        int h, int w, int32_t *status) {
+    HostClock hc;
     // ---- host: parse, plan, tables
     std::vector<Parsed> ps((size_t)n);
     std::vector<Frame> fr((size_t)n);
@@ -691,6 +711,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
         }
         for (int c = F.ncomp; c < kMaxComp; ++c) { F.dc_tab[c] = F.dc_tab[0]; F.ac_tab[c] = F.ac_tab[0]; }
     }
+    hc.mark("parse + tables");
     // ---- layout: upload (frames, tables, quant, chunk map, entropy bytes) and device arenas
     size_t src_total = 0, stream_total = 0, coef_total = 0, samp_total = 0;
     uint32_t chunks = 0, subs = 0, nsub_max = 0, max_blocks = 0;
@@ -743,6 +764,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     const size_t o_scan = dv;    dv = align_up(dv + sizeof(SubStats) * (size_t)subs, 256);
     const size_t dev_bytes = dv;
 
+    hc.mark("layout");
     int rc = pano_grow(ctx, &ctx->jscratch, &ctx->jscratch_bytes, dev_bytes);
     if (rc) return rc;
     // pinned staging, two buffers in turn: wait until the upload out of this one (two calls
@@ -759,6 +781,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
         PANO_HIP(ctx, hipHostMalloc(&ctx->jpin[slot], sz, hipHostMallocDefault));
         ctx->jpin_bytes[slot] = sz;
     }
+    hc.mark("grow + staging wait");
     uint8_t *pin = (uint8_t *)ctx->jpin[slot];
     memcpy(pin + o_frames, fr.data(), sizeof(Frame) * n);
     if (!tabs.empty()) memcpy(pin + o_tabs, tabs.data(), sizeof(Huff) * tabs.size());
@@ -768,9 +791,11 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
         memcpy(pin + o_src + fr[f].src_off, ps[f].ecs, fr[f].src_len);
         memset(pin + o_src + fr[f].src_off + fr[f].src_len, 0, 16);
     }
+    hc.mark("pinned memcpy");
     uint8_t *dev = (uint8_t *)ctx->jscratch;
     PANO_HIP(ctx, hipMemcpyAsync(dev, pin, up_bytes, hipMemcpyHostToDevice, ctx->stream));
     PANO_HIP(ctx, hipEventRecord(ctx->jev[slot], ctx->stream));
+    hc.mark("upload enqueue");
 
     Dev D;
     D.frames = (const Frame *)(dev + o_frames);
@@ -822,5 +847,6 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     jpeg_idct<<<dim3((max_blocks + 31) / 32, n * kMaxComp), 256, 0, ctx->stream>>>(D);
     jpeg_color<<<dim3((unsigned)(((size_t)h * w + 255) / 256), n), 256, 0, ctx->stream>>>(D, bgr, h, w);
     PANO_LAUNCH_CHECK(ctx, "jpeg decode");
+    hc.mark("launches");
     return PANO_OK;
 }

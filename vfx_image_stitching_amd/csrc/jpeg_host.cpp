@@ -282,10 +282,13 @@ int parse(const uint8_t *buf, size_t len, Parsed *P, std::string *err) {
             // appended thumbnails) is never part of the scan.
             const size_t e0 = i + seglen;
             size_t e1 = len;
-            for (size_t q = e0; q + 1 < len; ++q) {
-                if (buf[q] != 0xFF) continue;
+            for (size_t q = e0; q + 1 < len;) {
+                // the next 0xFF (memchr: vectorised, ~1 in 256 entropy bytes is one)
+                const void *hit = memchr(buf + q, 0xFF, len - 1 - q);
+                if (!hit) break;
+                q = (size_t)((const uint8_t *)hit - buf);
                 const uint8_t nx = buf[q + 1];
-                if (nx == 0x00 || (nx >= 0xD0 && nx <= 0xD7)) { ++q; continue; }
+                if (nx == 0x00 || (nx >= 0xD0 && nx <= 0xD7)) { q += 2; continue; }
                 e1 = q;
                 break;
             }

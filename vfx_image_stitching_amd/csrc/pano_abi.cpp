@@ -561,30 +561,6 @@ int pano_graph_begin(pano_ctx *ctx) {
     if (!ctx || ctx->capturing) return PANO_E_ARG;
     sift_join_tail(ctx);
     sift_join_x(ctx);
-    // Each capture forks to newly created side streams and events.  Measured (same box,
-    // tools/graph_capture_ab.py): graphs captured over side streams that an earlier capture
-    // had used replay at 1.42 ms per parrington stitch instead of 1.05-1.07 -- every few
-    // kernels of the main chain then wait ~35 us -- while fresh streams give 1.05 ms on every
-    // capture.  PANO_FRESH_SIDE=0 keeps the streams (A/B only).
-    {
-        const char *e = getenv("PANO_FRESH_SIDE");
-        if (!(e && atoi(e) == 0)) {
-            PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            hipStream_t *ss[] = {&ctx->side, &ctx->xside, &ctx->lvl_side};
-            for (hipStream_t *sp : ss)
-                if (*sp) {
-                    (void)hipStreamSynchronize(*sp);
-                    (void)hipStreamDestroy(*sp);
-                    *sp = nullptr;
-                }
-            hipEvent_t *es[] = {&ctx->ev_fork, &ctx->ev_join, &ctx->ev_x_fork, &ctx->ev_x_join, &ctx->ev_lvl_join};
-            for (hipEvent_t *ep : es)
-                if (*ep) {
-                    (void)hipEventDestroy(*ep);
-                    *ep = nullptr;
-                }
-        }
-    }
     ctx->cap_prof_start = ctx->prof.used;
     PANO_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
     ctx->capturing = true;

@@ -1823,9 +1823,7 @@ int sift_early_extrema(pano_ctx *ctx, const pano_sift_params *p, int o) {
         if (rc) return rc;
     }
     if (!ctx->xside) {
-        int lo_prio = 0, hi_prio = 0;
-        PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-        PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->xside, hipStreamNonBlocking, lo_prio));
+        PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->xside, hipStreamNonBlocking));
         PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_x_fork, hipEventDisableTiming));
         PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_x_join, hipEventDisableTiming));
     }

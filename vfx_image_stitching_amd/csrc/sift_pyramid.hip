@@ -1858,7 +1858,15 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         if (!ctx->side) {
             int lo_prio = 0, hi_prio = 0;   // numerically lower = higher priority
             PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-            PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi_prio));
+            // Default priority.  Measured (tools/jpeg_run_check.py, same box): with the side
+            // stream at high priority, graphs captured after the first one in a process replayed
+            // at 1.42 ms per parrington stitch instead of 1.05 (every few main-chain kernels
+            // waiting ~35 us); at default priority every capture replays at 1.05-1.06 ms.
+            // PANO_SIDE_PRIO=1: high priority (A/B only).
+            const char *pe = getenv("PANO_SIDE_PRIO");
+            const bool hi = pe && atoi(pe) == 1;
+            if (hi) PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi_prio));
+            else PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
             PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
             PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
         }
@@ -2045,7 +2053,8 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
                 if (!ctx->lvl_side) {
                     int lo_prio = 0, hi_prio = 0;
                     PANO_HIP(ctx, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-                    PANO_HIP(ctx, hipStreamCreateWithPriority(&ctx->lvl_side, hipStreamNonBlocking, lo_prio));
+                    (void)lo_prio;
+                    PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->lvl_side, hipStreamNonBlocking));
                     PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_lvl_join, hipEventDisableTiming));
                 }
                 if (!ctx->ev_lvl[o]) PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_lvl[o], hipEventDisableTiming));
