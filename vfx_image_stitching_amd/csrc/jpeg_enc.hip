@@ -26,9 +26,9 @@ using namespace pj;
 
 namespace {
 
-constexpr int kEncThreads = 256;
-constexpr int kLenChunk = 1024;          // blocks per length-prefix chunk
-constexpr int kByteChunk = 4096;         // bytes per stuffing chunk
+constexpr int kEncThreads = 128;
+constexpr int kLenChunk = 128;           // blocks per length-prefix chunk: one per thread (a 2.2 Mpx panorama: ~420 workgroups)
+constexpr int kByteChunk = 16 * kEncThreads;   // bytes per stuffing chunk: 16 consecutive bytes per thread
 
 struct EncTabs {
     QRecip q[2][64];                     // luma, chroma reciprocals (natural order)
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(kEncThreads) jpeg_enc_stuff(EncDev D) {
     const uint32_t j0 = blockIdx.x * kByteChunk;
     if (threadIdx.x == 0) base = red[0] + j0;            // output position of byte j0
     __syncthreads();
-    // 16 consecutive bytes per thread (kByteChunk = 16 * 256)
+    // 16 consecutive bytes per thread (kByteChunk = 16 * kEncThreads)
     const uint32_t jt = j0 + threadIdx.x * 16;
     uint32_t by[16], ff = 0;
     for (int i = 0; i < 16; ++i) {
@@ -319,7 +319,12 @@ int launch_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t 
     int rc = pano_grow(ctx, &ctx->jscratch, &ctx->jscratch_bytes, dv);
     if (rc) return rc;
     uint8_t *dev = (uint8_t *)ctx->jscratch;
-    PANO_HIP(ctx, hipMemcpyAsync(dev + o_tabs, &tabs, sizeof(tabs), hipMemcpyHostToDevice, ctx->stream));
+    // pinned staging (a pageable source or destination makes each copy a staged, blocking
+    // one); the previous encode synchronised before returning, so the buffer is free
+    constexpr size_t kEpinTot = (sizeof(EncTabs) + 255) / 256 * 256;
+    if (!ctx->epin) PANO_HIP(ctx, hipHostMalloc(&ctx->epin, kEpinTot + 256, hipHostMallocDefault));
+    memcpy(ctx->epin, &tabs, sizeof(tabs));
+    PANO_HIP(ctx, hipMemcpyAsync(dev + o_tabs, ctx->epin, sizeof(tabs), hipMemcpyHostToDevice, ctx->stream));
     EncDev D;
     D.img = bgr;
     D.G = G;
@@ -344,7 +349,7 @@ int launch_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t 
         jpeg_enc_stuff<<<nbchunk, kEncThreads, 0, ctx->stream>>>(D);
         PANO_LAUNCH_CHECK(ctx, "jpeg encode");
     }
-    uint32_t tot[2] = {0, 0};
+    uint32_t *tot = (uint32_t *)((uint8_t *)ctx->epin + kEpinTot);
     PANO_HIP(ctx, hipMemcpyAsync(tot, D.total, 8, hipMemcpyDeviceToHost, ctx->stream));
     PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const size_t need = hdr.size() + tot[1] + 2;

@@ -135,6 +135,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
         if (ctx->jpin[i]) (void)hipHostFree(ctx->jpin[i]);
         if (ctx->jev[i]) (void)hipEventDestroy(ctx->jev[i]);
     }
+    if (ctx->epin) (void)hipHostFree(ctx->epin);
     for (hipEvent_t e : ctx->prof.ev) (void)hipEventDestroy(e);
     delete ctx;
     return PANO_OK;

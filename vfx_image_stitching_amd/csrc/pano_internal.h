@@ -106,6 +106,7 @@ struct pano_ctx {
     // host fills one while the other's upload may still be queued)
     void *jscratch = nullptr; size_t jscratch_bytes = 0;
     void *jpin[2] = {nullptr, nullptr}; size_t jpin_bytes[2] = {0, 0};
+    void *epin = nullptr;                // pinned: the encoder's tables (H2D) and totals (D2H)
     hipEvent_t jev[2] = {nullptr, nullptr};
     int jslot = 0;
     int32_t *jstats = nullptr; int jstats_n = 0;   // last decode's per-frame sync statistics

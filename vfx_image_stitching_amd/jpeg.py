@@ -99,11 +99,18 @@ def encode(img, quality: int = 95) -> bytes:
     ctx = context(img.device.index)
     cap = ctypes.c_size_t(0)
     size = 1024 + h * w * 4
-    out = np.empty(size, np.uint8)
+    # the file bytes come back through a pinned buffer kept per device (a pageable destination
+    # makes the device -> host copy a staged one)
+    out = _ENC_PIN.get(ctx.device)
+    if out is None or out.numel() < size:
+        out = _ENC_PIN[ctx.device] = torch.empty(max(size, 1 << 20), dtype=torch.uint8, pin_memory=True)
     rc = ctx.lib.pano_jpeg_encode(ctx.h, ctypes.c_void_p(img.data_ptr()), h, w, img.stride(0), int(quality),
-                                  out.ctypes.data_as(ctypes.c_void_p), size, ctypes.byref(cap))
+                                  ctypes.c_void_p(out.data_ptr()), size, ctypes.byref(cap))
     ctx.check(rc)
-    return out[:cap.value].tobytes()
+    return out.numpy()[:cap.value].tobytes()
+
+
+_ENC_PIN = {}                 # device -> pinned u8 buffer of pano_jpeg_encode's output
 
 
 def imwrite(path: str, img, quality: int = 95) -> bool:
