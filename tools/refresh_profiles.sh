@@ -7,7 +7,7 @@
 #   gpurun_out/refresh/; copy what is judged into profiles/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-R=${R:-r03}
+R=${R:-r04}
 O=gpurun_out/refresh
 rm -rf $O && mkdir -p $O
 for w in parrington synthetic; do
@@ -18,14 +18,16 @@ done
 echo "pmc done"
 timeout -k 10 600 python bench.py > $O/bench_parrington.txt 2>&1 || exit $?
 tail -1 $O/bench_parrington.txt | cut -c1-300
-timeout -k 10 600 python bench.py --workload synthetic --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_synthetic.txt 2>&1 || exit $?
+timeout -k 10 600 python bench.py --workload synthetic --steps 10 --warmup 2 > $O/bench_synthetic.txt 2>&1 || exit $?
 tail -1 $O/bench_synthetic.txt | cut -c1-300
-timeout -k 10 900 python bench.py --workload synthetic --scaling strong --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_synthetic_strong.txt 2>&1 || exit $?
+timeout -k 10 900 python bench.py --workload synthetic --scaling strong --steps 3 --warmup 1 > $O/bench_synthetic_strong.txt 2>&1 || exit $?
 tail -1 $O/bench_synthetic_strong.txt | cut -c1-300
 for w in parrington synthetic; do
   A="--steps 10 --warmup 2 --no-cpu-baseline"; [ $w = synthetic ] && A="--workload synthetic --steps 4 --warmup 1 --no-cpu-baseline"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o run -- python3 bench.py $A > $O/prof_$w.log 2>&1 || exit $?
 done
-K=$(find $O/prof_parrington -name "*kernel_trace.csv" | head -1)
-python3 tools/timeline.py $K --step 6 > $O/timeline_parrington.txt
+# the timeline of one graph-replayed step (only replays in that process)
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/steps -o run -- python3 tools/step_timeline.py > $O/steps.log 2>&1 || exit $?
+python3 tools/timeline.py $O/steps/run_kernel_trace.csv --step 10 > $O/timeline_parrington.txt
+tail -1 $O/timeline_parrington.txt
 echo refresh done

@@ -38,4 +38,14 @@ for s, e, n, g in step:
     gap = (s - busy_end) / 1e3
     print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap:7.1f}  {n[:60]}  {'x'.join(g)}")
     busy_end = max(busy_end, e)
-print(f"step span {(busy_end - t0) / 1e3:.1f} us, {len(step)} kernels")
+# busy = the union of the kernels' intervals (overlapping side-stream kernels counted once);
+# the step span runs to the next step's first kernel, so the host gap between steps counts
+nxt = rows[i1][0] if i1 < len(rows) else busy_end
+busy, cur = 0, t0
+for s, e, _, _ in step:
+    s = max(s, cur)
+    if e > s:
+        busy += e - s
+        cur = e
+print(f"step span {(busy_end - t0) / 1e3:.1f} us to the last kernel's end, {(nxt - t0) / 1e3:.1f} us to the next "
+      f"step; GPU busy {busy / 1e3:.1f} us; idle {(nxt - t0 - busy) / 1e3:.1f} us; {len(step)} kernels")
