@@ -1940,8 +1940,8 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     // octave o+1's first levels, which read only level nl-3 of octave o: the octaves' chains
     // of small latency-bound launches then overlap instead of running back to back.  From
     // octave PANO_OCT_FORK on (-1: off); joined into the main stream after the octave loop.
-    // Measured on MI355X: bit-exact, but 1.34-1.55 ms per graph-replayed
-    // parrington stitch against 1.16 ms unforked (from octave 0, 1 or 2), so off by default.
+    // Measured on MI355X: bit-exact; at default stream priority within noise of
+    // the unforked chain (1.067-1.075 against 1.05-1.07 ms per parrington stitch), so off.
     static const int oct_fork = [] {
         const char *e = getenv("PANO_OCT_FORK");
         return e ? atoi(e) : -1;
