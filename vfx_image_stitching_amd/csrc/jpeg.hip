@@ -60,6 +60,7 @@ struct Dev {
     SubStats *cstats;           // [S][nps]
     uint64_t *start;            // [S]
     SubStats *scan;             // [S] exclusive prefix
+    uint64_t *maps;             // [S] candidate map of subsequence t >= 1: slot of t-1 -> slot of t
     int n, np, nps;             // candidate slots: np phases (max bpm), nps = 2 np + 1
     int chain;                  // subsequences per warm chain (<= kChain)
 };
@@ -385,6 +386,41 @@ __device__ __forceinline__ uint64_t find_slot(const uint64_t *ct, int nps, uint6
     return jj;
 }
 
+// The candidate map of every subsequence t >= 1 of every frame, all in parallel (one thread
+// per subsequence): entry i is the slot of t that slot i of t-1 exits into (kNone if none).
+// jpeg_sync_resolve composes them per frame.  The candidate and exit records are loaded up
+// front (kMapSlots at a time, predicated) so their loads are in flight together.
+constexpr int kMapSlots = 2 * 6 + 1;    // nps at 6 blocks per MCU (4:2:0), the most the parser accepts
+__global__ void __launch_bounds__(256) jpeg_sync_maps(Dev D) {
+    const int f = blockIdx.y;
+    const Frame &F = D.frames[f];
+    const uint32_t nsub = frame_nsub(F, D.nbits[f]);
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t == 0 || t >= nsub) return;
+    const int nps = D.nps;
+    const size_t S = F.sub0 + t;
+    uint64_t ct[kMapSlots], xp[kMapSlots], cp[kMapSlots];
+#pragma unroll
+    for (int i = 0; i < kMapSlots; ++i) {
+        const bool in = i < nps;
+        ct[i] = in ? D.cand[S * nps + i] : kNoCand;
+        xp[i] = in ? D.cexit[(S - 1) * nps + i] : kNoCand;
+        cp[i] = in ? D.cand[(S - 1) * nps + i] : kNoCand;
+    }
+    uint64_t m = 0;
+#pragma unroll
+    for (int i = 0; i < kMapSlots; ++i) {
+        uint64_t jj = kNone;
+        if (cp[i] != kNoCand && xp[i] != kNoCand) {
+#pragma unroll
+            for (int j = kMapSlots - 1; j >= 0; --j)
+                if (j < nps && ct[j] == xp[i]) jj = (uint64_t)j;
+        }
+        if (i < nps) m |= jj << (4 * i);
+    }
+    D.maps[S] = m;
+}
+
 constexpr int kResolveThreads = 512;
 constexpr int kFixRun = 16;      // subsequences one serial fallback may decode in a row
 
@@ -445,15 +481,8 @@ __global__ void __launch_bounds__(kResolveThreads) jpeg_sync_resolve(Dev D) {
         uint64_t m = map_const(kNone, nps);
         if (in) {
             const uint64_t *ct = D.cand + (S0 + t) * nps;
-            if (threadIdx.x == 0) {
-                m = map_const(find_slot(ct, nps, s_exit), nps);
-            } else {
-                const uint64_t *xp = D.cexit + (S0 + t - 1) * nps;
-                const uint64_t *cp = D.cand + (S0 + t - 1) * nps;
-                m = 0;
-                for (int i = 0; i < nps; ++i)
-                    m |= (cp[i] == kNoCand ? kNone : find_slot(ct, nps, xp[i])) << (4 * i);
-            }
+            if (threadIdx.x == 0) m = map_const(find_slot(ct, nps, s_exit), nps);
+            else m = D.maps[S0 + t];                       // jpeg_sync_maps
         }
         maps[threadIdx.x] = m;
         if (threadIdx.x == 0) s_fail = NT;
@@ -732,6 +761,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
         subs += F.nsub;
         nsub_max = std::max(nsub_max, F.nsub);
         np = std::max(np, F.bpm);
+        if (F.bpm > 6) return pano_fail(ctx, PANO_E_UNSUPPORTED, "JPEG with more than 6 blocks per MCU");
         for (int c = 0; c < F.ncomp; ++c) {
             const size_t nbk = (size_t)F.comp_bw[c] * F.comp_bh[c];
             F.coef_off[c] = coef_total;
@@ -762,6 +792,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     const size_t o_cstats = dv;  dv = align_up(dv + sizeof(SubStats) * (size_t)subs * nps, 256);
     const size_t o_start = dv;   dv = align_up(dv + 8 * (size_t)subs, 256);
     const size_t o_scan = dv;    dv = align_up(dv + sizeof(SubStats) * (size_t)subs, 256);
+    const size_t o_maps = dv;    dv = align_up(dv + 8 * (size_t)subs, 256);
     const size_t dev_bytes = dv;
 
     hc.mark("layout");
@@ -818,6 +849,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
     D.cstats = (SubStats *)(dev + o_cstats);
     D.start = (uint64_t *)(dev + o_start);
     D.scan = (SubStats *)(dev + o_scan);
+    D.maps = (uint64_t *)(dev + o_maps);
     D.n = n;
     D.np = np;
     D.nps = nps;
@@ -842,6 +874,7 @@ int launch_jpeg_decode(pano_ctx *ctx, int n, const uint8_t *const *bufs, const s
         jpeg_sync_fix<<<dim3((nsub_max + spb - 1) / spb, n), kSyncThreads, 0, ctx->stream>>>(D);
         jpeg_sync_fix2<<<dim3((nsub_max + spb - 1) / spb, n), kSyncThreads, 0, ctx->stream>>>(D);
     }
+    jpeg_sync_maps<<<dim3((nsub_max + 255) / 256, n), 256, 0, ctx->stream>>>(D);
     jpeg_sync_resolve<<<n, kResolveThreads, 0, ctx->stream>>>(D);
     jpeg_write<<<dim3((nsub_max + kWriteThreads - 1) / kWriteThreads, n), kWriteThreads, 0, ctx->stream>>>(D);
     jpeg_idct<<<dim3((max_blocks + 31) / 32, n * kMaxComp), 256, 0, ctx->stream>>>(D);

@@ -27,7 +27,10 @@ namespace pj {
 
 constexpr int kMaxComp = 3;     // gray or YCbCr
 constexpr int kMaxBpm = 10;     // blocks per MCU (JPEG limit)
-constexpr int kSubBits = 512;   // bits per subsequence of the self-synchronising decode
+#ifndef PANO_JPEG_SUB_BITS
+#define PANO_JPEG_SUB_BITS 512
+#endif
+constexpr int kSubBits = PANO_JPEG_SUB_BITS;   // bits per subsequence of the self-synchronising decode
 constexpr int kChunk = 4096;    // stuffed bytes per unstuff chunk
 constexpr int kStreamPad = 64;  // zero bytes after each unstuffed stream
 constexpr int kHuffSub = 16;    // second-level lookup tables per Huffman table
