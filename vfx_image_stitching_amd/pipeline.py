@@ -99,6 +99,7 @@ class Stitcher:
         self._graph_mode = False
         self._fast = None                # (key, replay state) of run()'s graph fast path
         self._fast_key = None
+        self._views = None               # (key, canvas view, panorama view) of _crop_planned
 
     # ------------------------------------------------------------------ buffers
     def _get(self, name, shape, dtype):
@@ -539,16 +540,22 @@ class Stitcher:
     def _crop_planned(self, buf, H, W, bb, margin, shifts, best_pairs, recs, t, t0):
         """_crop on the device-planned canvas (an H x W x 3 view of the capacity buffer), with
         one strided view each for the canvas and the panorama."""
-        canvas = buf.as_strided((H, W, 3), (W * 3, 3, 1))
         if bb[1] < 0:
             y0, y1, x0, x1 = 0, H - 1, 0, W - 1
-            pano = canvas
         else:
             y0 = max(0, bb[0] + margin)
             y1 = min(H - 1, bb[1] - margin)
             x0, x1 = bb[2], bb[3]
-            pano = canvas if (y0 > y1 or x0 > x1) else buf.as_strided(
+        # the two views of the same buffer and geometry are reused from the last call (a
+        # replayed stitch usually has both): creating them costs more than the rest of run()
+        vk = (buf.data_ptr(), H, W, y0, y1, x0, x1)
+        views = self._views
+        if views is None or views[0] != vk:
+            canvas = buf.as_strided((H, W, 3), (W * 3, 3, 1))
+            pano = canvas if (bb[1] < 0 or y0 > y1 or x0 > x1) else buf.as_strided(
                 (y1 + 1 - y0, x1 + 1 - x0, 3), (W * 3, 3, 1), buf.storage_offset() + y0 * W * 3 + x0 * 3)
+            self._views = views = (vk, canvas, pano)
+        canvas, pano = views[1], views[2]
         t["total"] = time.perf_counter() - t0
         return StitchResult(pano, canvas, shifts, best_pairs, recs, (y0, y1, x0, x1), t)
 
