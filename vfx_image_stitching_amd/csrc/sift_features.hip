@@ -1195,6 +1195,9 @@ constexpr float kFix = 4194304.0f;    // 2^22: contributions <= 255 sqrt(2) fit 
 #define PANO_DESC_SW 4                // patch columns per strip: one (SW + 2)-float load per step
 #endif
 constexpr int kDescSW = PANO_DESC_SW;
+#ifndef PANO_DESC_NS_PREFETCH
+#define PANO_DESC_NS_PREFETCH 0       // 1: a strip change's rows loaded a step ahead (12 more VGPRs)
+#endif
 #ifndef PANO_DESC_COPIES
 #define PANO_DESC_COPIES 2            // histogram copies per wave (copy = lane % copies)
 #endif
@@ -1241,17 +1244,15 @@ __device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ coun
     return false;
 }
 
-// OCC: waves per SIMD the register budget is sized for.  Measured (same box): at parrington
-// 3 -> 168 VGPRs, no spills, 250-257 us against 4 -> 128 VGPRs with spills, 260 us (5: 264 us);
-// at 1080p the other way, 3.25 ms at 3 against 3.12 ms at 4.  Both are built and the launch
-// picks by the size of the base octave (desc_occ).
-constexpr long long kDescOcc4Px = 4 << 20;   // base-octave pixels from which OCC 4 is used
-
-// PANO_DESC_OCC=3|4 forces the budget (read per call, for the A/B tests).
-static int desc_occ(long long base_px) {
+// OCC: waves per SIMD the register budget is sized for.  With a strip change's rows loaded
+// when reached (PANO_DESC_NS_PREFETCH=0, 12 VGPRs fewer) the 4-wave budget spills 5 registers
+// instead of 13, and measures best at both sizes (same box, feature-stage timing): parrington
+// 0.222 ms at 4 against 0.238 at 3 and 0.241 at 5; 1080p 2.86 ms against 3.10 and 2.99.  The
+// 3-wave build stays for the A/B (PANO_DESC_OCC=3, read per call).
+static int desc_occ(long long) {
     const char *e = getenv("PANO_DESC_OCC");
-    if (e && (e[0] == '3' || e[0] == '4') && !e[1]) return e[0] - '0';
-    return base_px >= kDescOcc4Px ? 4 : 3;
+    if (e && e[0] == '3' && !e[1]) return 3;
+    return 4;
 }
 
 template <bool OUT_U8, int OCC>
@@ -1501,12 +1502,17 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                         do { ++sn; } while (cpre[sn + 1] == cpre[sn]);
                         yn = clo[sn];
                     }
-                    float N0[WN], N1[WN], N2[WN];
+                    float N2[WN];
+#if PANO_DESC_NS_PREFETCH
+                    float N0[WN], N1[WN];
                     if (newstrip) {
                         win(sn, yn - 1, N0);
                         win(sn, yn, N1);
                     }
                     if (more) win(sn, yn + 1, N2);
+#else
+                    if (more && !newstrip) win(sn, yn + 1, N2);
+#endif
                     const float ysf = (float)ys, ys2 = ysf * ysf;
                     // exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) = exp2(kq (xs^2 + ys^2)): a rotation
                     // keeps the radius (no LDS read on the sample path)
@@ -1518,8 +1524,15 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                         sx = sn;
                         yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
                         strip_consts(sx);
+#if PANO_DESC_NS_PREFETCH
 #pragma unroll
                         for (int i = 0; i < WN; ++i) { Tm[i] = N0[i]; T0[i] = N1[i]; Tp[i] = N2[i]; }
+#else
+                        // a strip change (about once per lane run) loads its three rows here
+                        win(sn, yn - 1, Tm);
+                        win(sn, yn, T0);
+                        win(sn, yn + 1, Tp);
+#endif
                     } else {
 #pragma unroll
                         for (int i = 0; i < WN; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; Tp[i] = N2[i]; }
