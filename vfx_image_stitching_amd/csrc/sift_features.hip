@@ -307,6 +307,9 @@ constexpr int XSR = 32;          // output rows per item (default; PANO_EXTREMA_
 #define PANO_XPD 3
 #endif
 constexpr int XPD = PANO_XPD;    // rows prefetched ahead
+#ifndef PANO_XSTREAM_BLOCKS
+#define PANO_XSTREAM_BLOCKS 1    // waves per SIMD the register budget is sized for (6: 80 VGPRs, within noise; 8: spills, 2.5x slower)
+#endif
 
 struct XArgs {
     const float *dog[PANO_MAX_OCTAVES][PANO_MAX_LEVELS];
@@ -320,7 +323,7 @@ __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf
 __device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
 
 template <int NL, int SR>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, PANO_XSTREAM_BLOCKS)
 extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
                int32_t *__restrict__ raw_cnt, int raw_cap, int item_base, int item_end) {
     constexpr int ni = NL - 2;
@@ -537,9 +540,12 @@ constexpr int kOriCopies = PANO_ORI_COPIES;
 constexpr float kInv360 = 1.0f / 360.0f;   // RN(1 / 360)
 constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
 #ifndef PANO_ORI_STAGE
-#define PANO_ORI_STAGE 12
+#define PANO_ORI_STAGE 8
 #endif
-constexpr int kOriStage = PANO_ORI_STAGE;   // patch loads per lane in flight (37^2 / 64 <= 22: two rounds)
+constexpr int kOriStage = PANO_ORI_STAGE;
+#ifndef PANO_ORI_BLOCKS
+#define PANO_ORI_BLOCKS 6        // waves per SIMD the register budget is sized for (80 VGPRs; measured 1-3 % faster than 88)
+#endif   // patch loads per lane in flight (37^2 / 64 <= 22: two rounds)
 
 struct OriParams {
     double scale_factor, radius_factor, peak_ratio;
@@ -742,7 +748,7 @@ __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H,
 // own counter (as descriptor_wave).  Per candidate: the (side+2)^2 neighbourhood staged in
 // LDS, each lane its run of column-major samples into 2^40 fixed-point u64 LDS atomics,
 // smoothing and peak interpolation in f64 (the reference's), one aggregated append.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, PANO_ORI_BLOCKS)
 orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             const int32_t *__restrict__ cand_cnt, int cand_cap, int n_frames, int32_t *__restrict__ work,
             RawKp *__restrict__ raw, int32_t *__restrict__ raw_cnt, int raw_cap) {
