@@ -585,6 +585,9 @@ row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
 #ifndef PANO_I8_STAGGER
 #define PANO_I8_STAGGER 1                // waves 4-7 run each tile's epilogue one barrier late
 #endif
+#ifndef PANO_I8_PRIO
+#define PANO_I8_PRIO 0                   // 1: waves 4-7 at s_setprio 1 for the whole loop
+#endif
 #ifndef PANO_I8_WAVES
 #define PANO_I8_WAVES 4                  // 4 waves per SIMD (two workgroups per CU): measured 2.87 -> 2.57 ms at 1080p
 #endif
@@ -666,16 +669,26 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
 #else
     const int sr = tid & (BT - 1), sp = tid / BT;
 #endif
+    // fetch only issues the loads (the next tile's, a tile ahead); store, one tile later,
+    // forms C from them, so no wait on a load sits right behind its issue
     uint4 pre[2];
     int pre_c = kPadC;
     auto fetch = [&](int jt) {
         const int row = jt * BT + sr;
         pre[0] = pre[1] = make_uint4(0u, 0u, 0u, 0u);
+        pre_c = kPadC;                                  // past the count: never a best
         if (row < NB) {
             const uint4 *src = (const uint4 *)(dB + (size_t)row * PANO_DESC_DIM + 32 * sp);
             pre[0] = src[0];
             pre[1] = src[1];
+#if PANO_I8_QLDS
+            pre_c = norms[(size_t)fb * cap + row];      // |b|^2; the byte sum is taken in store
+#else
+            if (sp == 0) pre_c = cst[(size_t)fb * cap + row] + (1 << 22);
+#endif
         }
+    };
+    auto store = [&](int buf, int cbuf) {
 #if PANO_I8_QLDS
         unsigned int sum = 0;
         const unsigned int w[8] = {pre[0].x, pre[0].y, pre[0].z, pre[0].w, pre[1].x, pre[1].y, pre[1].z, pre[1].w};
@@ -683,13 +696,8 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
         for (int i = 0; i < 8; ++i) sum = __builtin_amdgcn_udot4(w[i], 0x01010101u, sum, false);
         sum += __shfl_xor(sum, 1);
         sum += __shfl_xor(sum, 2);
-        pre_c = row < NB ? norms[(size_t)fb * cap + row] - 256 * (int)sum + (1 << 22)
-                         : kPadC;                       // past the count: never a best
-#else
-        pre_c = row < NB && sp == 0 ? cst[(size_t)fb * cap + row] + (1 << 22) : kPadC;
+        if (pre_c != kPadC) pre_c = pre_c - 256 * (int)sum + (1 << 22);
 #endif
-    };
-    auto store = [&](int buf, int cbuf) {
         uint4 *d4 = (uint4 *)(Bs2[buf] + sr * BPI + 32 * sp);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
@@ -743,6 +751,9 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
     // epilogue runs beside its partner's MFMAs.  C32 is triple-buffered: a late epilogue of
     // tile t runs while tile t + 2 is staged.
     const bool lag = PANO_I8_STAGGER && wj == 1;
+#if PANO_I8_PRIO
+    if (wj == 1) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two waves per SIMD, item 4
+#endif
     int jt = blockIdx.x, cur = 0, c3 = 0;
     fetch(jt);
     store(0, 0);
