@@ -44,9 +44,14 @@ constexpr int kHuffSub = 16;    // second-level lookup tables per Huffman table
 // k + advance positions without decoding the symbol.  lut entries with bit 15 set hold a
 // second-level offset; codes the table lacks (reached only off sync) read as a 1-bit code.
 // One or two LDS reads per codeword, no search loop.
+// Canonical codes longer than 9 bits have contiguous 9-bit prefixes [first_long, first_long +
+// nsub), assigned second-level tables 0, 1, ... in that order, so a walker computes the
+// second-level index from the bits alone and reads both levels at once (one LDS round trip
+// per codeword, not two dependent ones).
 struct Huff {
     uint16_t lut[512];
     uint16_t sub[kHuffSub * 128];
+    uint32_t first_long;        // 9-bit prefix of the first code longer than 9 bits (512: none)
 };
 
 // Everything a kernel needs about one frame (built on the host by jpeg_plan).
@@ -90,6 +95,15 @@ __host__ __device__ __forceinline__ uint32_t window32(const uint32_t *w, uint32_
 __host__ __device__ __forceinline__ uint32_t huff_entry(const Huff *T, uint32_t x) {
     const uint32_t e1 = T->lut[x >> 23];
     const uint32_t e2 = T->sub[((e1 & 0x7FFF) + ((x >> 16) & 127)) & (kHuffSub * 128 - 1)];
+    return (e1 & 0x8000) ? e2 : e1;
+}
+// The same entry with the second-level index taken from the bits (first_long: the table's
+// Huff::first_long): the two reads are independent.  For a short code the second read lands
+// anywhere inside the table and is discarded.
+__host__ __device__ __forceinline__ uint32_t huff_entry_par(const Huff *T, uint32_t x, uint32_t first_long) {
+    const uint32_t pre = x >> 23;
+    const uint32_t e1 = T->lut[pre];
+    const uint32_t e2 = T->sub[(((pre - first_long) & (kHuffSub - 1)) << 7) | ((x >> 16) & 127)];
     return (e1 & 0x8000) ? e2 : e1;
 }
 
@@ -179,6 +193,10 @@ __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_
     // the MCU layout as 2 bits per block in a register (no memory read per block)
     uint32_t layout = 0;
     for (int i = 0; i < bpm; ++i) layout |= (uint32_t)(mcu_comp[i] & 3) << (2 * i);
+    // each table's first long prefix, 10 bits apiece (tables 0..5: DC of components 0..2,
+    // then their AC tables)
+    uint64_t flpack = 0;
+    for (int i = 0; i < 6; ++i) flpack |= (uint64_t)(T[i].first_long & 1023) << (10 * i);
     int c = (int)(layout >> (2 * b)) & 3;
     // bit buffer: buf holds stream bits [pos, pos + cnt) left-aligned, cnt >= 32 at the top of
     // every iteration; nxt is the next stream word, loaded an iteration before it is needed, so
@@ -203,7 +221,8 @@ __host__ __device__ __forceinline__ uint64_t walk(const uint32_t *words, uint32_
         nxt = rd(wi);
         const uint32_t x = (uint32_t)(buf >> 32);
         const bool isdc = k == 0;
-        const uint32_t e = huff_entry(T + (isdc ? c : 3 + c), x);
+        const int tix = isdc ? c : 3 + c;
+        const uint32_t e = huff_entry_par(T + tix, x, (uint32_t)(flpack >> (10 * tix)) & 1023);
         const int cl = (int)(e & 15) + 1;
         const int s = (int)((e >> 4) & 31);
         const int adv = (int)((e >> 9) & 63) + 1;

@@ -149,6 +149,7 @@ int make_huff(int cls, const uint8_t *bits17, const uint8_t *vals, Huff *T) {
         ++si;
     }
     memset(T, 0, sizeof(*T));
+    T->first_long = 512;
     int nsub = 0;
     for (int i = 0; i < total; ++i) {
         const int l = size[i];
@@ -167,6 +168,9 @@ int make_huff(int cls, const uint8_t *bits17, const uint8_t *vals, Huff *T) {
         if (!(T->lut[pre] & 0x8000)) {
             if (T->lut[pre] != 0) return PANO_E_ARG;    // a shorter code is its prefix
             if (nsub == kHuffSub) return PANO_E_UNSUPPORTED;
+            if (nsub == 0) T->first_long = (uint32_t)pre;
+            // canonical codes: the long prefixes are contiguous and in order (jpeg_core.h Huff)
+            if ((uint32_t)pre != T->first_long + (uint32_t)nsub) return PANO_E_ARG;
             T->lut[pre] = (uint16_t)(0x8000 | nsub * 128);
             ++nsub;
         }
