@@ -267,6 +267,14 @@ class Stitcher:
         self.ctx.check(self.ctx.lib.pano_gray_bbox(self.ctx.h, ptr(img), H, W, thr, ptr(bb)))
         return bb
 
+    def _raw_stream(self):
+        """The caller's current HIP stream handle (torch's raw-stream accessor: the public
+        ``current_stream(device)`` builds a Stream object, a few microseconds per call)."""
+        get = getattr(self.torch._C, "_cuda_getCurrentRawStream", None)
+        if get is not None:
+            return get(self.device.index)
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
     # ------------------------------------------------------------------ hipGraph replay
     def _replay(self, key, fn):
         """fn() through a cached hipGraph: one eager call sizes every scratch buffer, the
@@ -402,7 +410,7 @@ class Stitcher:
             self.ratio, res.data_ptr(), canvas.data_ptr())
         ent = self._graph_entry(key) if self._graph_mode else None
         if ent is not None:       # replay on the caller's stream and wait: one library call
-            cur = T.cuda.current_stream(self.device).cuda_stream
+            cur = self._raw_stream()
             self.ctx.check(lib.pano_graph_launch_sync(c, ent[0], _lib._P(cur)))
             self.last_graphs.append(ent[0])
             cyl, colnz = ent[1]
@@ -468,7 +476,7 @@ class Stitcher:
             fast = self._fast
             if fast is not None and fast[0] == fk and fast[1][7] == self.ctx.generation():
                 g, cyl, colnz, off_bb, off_plan, nhead, canvas, _ = fast[1]
-                cur = self.torch.cuda.current_stream(self.device).cuda_stream
+                cur = self._raw_stream()
                 self.ctx.check(self.ctx.lib.pano_graph_launch_sync(self.ctx.h, g, _lib._P(cur)))
                 self.last_graphs.append(g)
                 head = self._head_np[:nhead]
