@@ -319,6 +319,27 @@ struct XArgs {
     int n_oct;
 };
 
+// Whole-wave lane shifts by one through DPP (wave_shr:1 / wave_shl:1, GFX9 DPP controls):
+// one VALU op instead of a ds_bpermute round trip.  The end lanes get 0 (only halo lanes use
+// them).  PANO_XDPP=0 keeps __shfl_up / __shfl_down.
+#ifndef PANO_XDPP
+#define PANO_XDPP 1
+#endif
+__device__ __forceinline__ float lane_from_below(float v) {     // lane i <- lane i - 1
+#if PANO_XDPP
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+#else
+    return __shfl_up(v, 1);
+#endif
+}
+__device__ __forceinline__ float lane_from_above(float v) {     // lane i <- lane i + 1
+#if PANO_XDPP
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+#else
+    return __shfl_down(v, 1);
+#endif
+}
+
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 __device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
 
@@ -384,7 +405,7 @@ extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
             float hxC[NL], hnC[NL];
 #pragma unroll
             for (int l = 0; l < NL; ++l) {
-                const float lf = __shfl_up(c[l], 1), rt = __shfl_down(c[l], 1);
+                const float lf = lane_from_below(c[l]), rt = lane_from_above(c[l]);
                 hxC[l] = max3f(lf, c[l], rt);
                 hnC[l] = min3f(lf, c[l], rt);
             }
