@@ -1239,6 +1239,9 @@ constexpr int kDescCopies = PANO_DESC_COPIES;
 static_assert(kDescSS <= 64 && (kDescGrp & (kDescGrp - 1)) == 0, "super-strip divides 64");
 
 static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "strip width divides 64");
+#ifndef PANO_DESC_RPI
+#define PANO_DESC_RPI 1               // fixed-point scale folded into the sample weight (fewer VALU)
+#endif
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
                                       // 3: every sample's taps from one cached location)
@@ -1373,7 +1376,15 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             float ob = atan2_oct(gy, gx) - a8;               // (-12, 4]
             ob = ob < 0.0f ? ob + 8.0f : ob;
             ob = ob < 0.0f ? ob + 8.0f : ob;
+#if PANO_DESC_RPI
+            // scaled to the 2^22 fixed point up front (a power of two: every product below is
+            // exactly 2^22 times its unscaled value), so each contribution is one multiply and
+            // one round-half-up conversion, v_cvt_rpi_i32_f32 = floor(x + 0.5): the same integer
+            // as the unscaled form's u32(fma(v, 2^22, 0.5)) for x in [0, 2^31)
+            const float wm = (w * mag) * kFix;
+#else
             const float wm = w * mag;
+#endif
             const float fr = floorf(rbin), fc = floorf(cbin), fo = floorf(ob);
             const float rf = rbin - fr, cf = cbin - fc;
             // (the reference's o0 = floor(ob) % 8, of = ob - o0 gives of = 8 when np.mod rounds a
@@ -1381,12 +1392,25 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             // the ulp level, which no other arithmetic reproduces: here of = ob - floor(ob), the
             // continuous form -- DESIGN.md 4, "descriptor outliers")
             const int o0 = (int)fo & 7, o1 = (o0 + 1) & 7;
+#if PANO_DESC_RPI
+            // (r0 + 1, c0 + 1) bin from the integer-valued floors (exact in f32): one conversion
+            const int base = (int)fmaf(fr, 48.0f, fmaf(fc, 8.0f, 56.0f));
+#else
             const int base = ((int)fr + 1) * 48 + ((int)fc + 1) * 8;   // (r0 + 1, c0 + 1) bin
+#endif
             const float c1 = wm * rf, c0w = wm - c1;
             const float v00 = c0w * (1.0f - cf), v01 = c0w * cf, v10 = c1 * (1.0f - cf), v11 = c1 * cf;
             const float of = ob - fo;
             const float nof = 1.0f - of;
+#if PANO_DESC_RPI
+            auto fix = [](float v) {
+                int r;
+                asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+                return (unsigned long long)(uint32_t)r;
+            };
+#else
             auto fix = [](float v) { return (unsigned long long)(uint32_t)fmaf(v, kFix, 0.5f); };
+#endif
             unsigned long long *hA = h + base + o0, *hB = h + base + o1;
 #if PANO_DESC_ABL == 0
             atomicAdd(hA, fix(v00 * nof));      atomicAdd(hB, fix(v00 * of));
@@ -1481,11 +1505,11 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             int t = (lane / kDescGrp) * Q;
             const int tend = min(t + Q, nsamp);
             if (t < tend) {
-                int sx = 0, s1 = nstrip - 1;               // largest strip with cpre[sx] <= t
-                while (sx < s1) {
-                    const int mid = (sx + s1 + 1) >> 1;
+                int sx = 0, shi = nstrip - 1;              // largest strip with cpre[sx] <= t
+                while (sx < shi) {
+                    const int mid = (sx + shi + 1) >> 1;
                     if (cpre[mid] <= t) sx = mid;
-                    else s1 = mid - 1;
+                    else shi = mid - 1;
                 }
                 int ys = clo[sx] + (t - cpre[sx]);
                 int yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
