@@ -152,6 +152,11 @@ int pano_sift_copy_level(pano_ctx *ctx, int frame, int octave, int level, int do
  *                        level 0 of octave 0; every Gaussian and DoG level stays resident
  *                        (pano_sift_copy_level reads them back).  The kernels are those of
  *                        params (sigma, num_intervals).
+ * pano_sift_pyramid_kernels  the same with the caller's kernel list (any gaussian_kernels, not
+ *                        only generate_gaussian_kernels' : sift_impl.py:89-92 blurs level l - 1
+ *                        by kernels[l]): n_kernels levels per octave (3..8), each kernel
+ *                        cv2.GaussianBlur's float32 one (ksize = round(8 s + 1) | 1, at most 64
+ *                        taps: s < 7.9); outside those limits PANO_E_UNSUPPORTED.
  * pano_sift_reserve_levels + pano_sift_set_level
  *                        lay out a resident pyramid for n frames with octave 0 of H0 x W0 and
  *                        upload caller levels into it (Gaussian: dog = 0, DoG: dog = 1), e.g.
@@ -195,6 +200,8 @@ int pano_sift_base(pano_ctx *ctx, const float *d_gray, int n, int h, int w,
                    const pano_sift_params *params, float *d_base);
 int pano_sift_pyramid_base(pano_ctx *ctx, const float *d_base, int n, int H0, int W0, int n_octaves,
                            const pano_sift_params *params);
+int pano_sift_pyramid_kernels(pano_ctx *ctx, const float *d_base, int n, int H0, int W0, int n_octaves,
+                              const double *h_kernels, int n_kernels);
 int pano_sift_reserve_levels(pano_ctx *ctx, int n, int H0, int W0, int n_octaves, int n_levels);
 int pano_sift_set_level(pano_ctx *ctx, int frame, int octave, int level, int dog, const float *d_in);
 int pano_sift_dog(pano_ctx *ctx);

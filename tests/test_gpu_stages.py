@@ -136,8 +136,31 @@ def test_pyramid_from_any_float_base(gpu, frames00):
     for o in range(4):
         for l in range(6):
             np.testing.assert_array_equal(gauss[o, l], ref[o][l], err_msg=f"{o},{l}")
+
+
+
+@pytest.mark.parametrize("kernels", [[1.6, 1.0, 1.0, 1.0, 1.0, 1.0], [2.0, 1.2, 0.7, 1.5],
+                                     [1.6, 0.5, 2.2, 0.9, 1.7, 1.1, 1.3, 0.8]])
+def test_pyramid_any_kernel_list(gpu, kernels):
+    """generate_gaussian_images with kernel lists generate_gaussian_kernels never makes (the
+    reference blurs with whatever list it is given, sift_impl.py:82-97): 4, 6 and 8 levels,
+    equal to the oracle's cascade bit for bit; DoG from the same levels."""
+    from oracle import sift as osift
+    from vfx_image_stitching_amd import sift_impl
+    rng = np.random.default_rng(7)
+    base = (rng.random((80, 112)) * 255).astype(np.float32)
+    gauss = sift_impl.generate_gaussian_images(base, 3, kernels)
+    ref = osift.gaussian_pyramid(base, 3, np.asarray(kernels))
+    assert gauss.shape == (3, len(kernels))
+    for o in range(3):
+        for l in range(len(kernels)):
+            np.testing.assert_array_equal(gauss[o, l], ref[o][l], err_msg=f"{o},{l}")
+    dogs = sift_impl.generate_DoG_images(gauss)
+    np.testing.assert_array_equal(dogs[1, 0], gauss[1, 1] - gauss[1, 0])
+    with pytest.raises(IndexError):
+        sift_impl.generate_gaussian_images(base, 2, [1.6, 1.0])
     with pytest.raises(NotImplementedError):
-        sift_impl.generate_gaussian_images(base, 2, [1.6, 1.0, 1.0, 1.0, 1.0, 1.0])
+        sift_impl.generate_gaussian_images(base, 2, [1.6, 1.0, 40.0])    # 321 taps
 
 
 def test_float_gray_base_image(gpu, frames00):
@@ -255,3 +278,37 @@ def test_per_candidate_helpers_refuse_bad_input(gpu, frames00):
         sift_impl.compute_keypoints_with_orientations(KeyPoint(10, 10, 1e9), 0, gauss[0][1])
     assert sift_impl.localize_extrema([], 0, 3, dogs[0], 1.6, 0.04, 5) == []
     assert sift_impl.orient_keypoints([], 0, gauss[0][1]) == []
+
+
+def _assert_same_features(kps, desc, okps, odesc):
+    t = _kp_table(kps)
+    assert len(kps) == len(okps) and len(kps) > 10
+    for k in ("x", "y", "size", "octave"):
+        np.testing.assert_array_equal(t[k], okps[k], err_msg=k)
+    d = np.abs(desc - np.asarray(odesc, np.float32))
+    assert desc.dtype == np.float32 and d.max() <= 1 and (d > 0).mean() < 1e-3
+
+
+def test_float_images_take_the_reference_sequence(gpu, frames00):
+    """compute_keypoints_and_descriptors on images whose gray is not an 8-bit one
+    (sift_impl.py:27-29 converts any image: cvtColor, astype(float32)): a non-integer gray
+    image, and a float BGR image (cv2.cvtColor's float formula, not the u8 fixed-point one),
+    through the reference's stage sequence on libpano -- equal to the oracle's chain on the
+    same float gray."""
+    from oracle import sift as osift
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import sift_impl
+    bgr = np.ascontiguousarray(frames00["prtn00"][96:224, 144:304])          # 128 x 160
+    gray = bgr_to_gray_u8(bgr).astype(np.float32) * np.float32(0.73) + np.float32(3.25)
+    kps, desc = sift_impl.compute_keypoints_and_descriptors(gray)
+    okps, odesc = osift.detect_and_describe(gray)
+    _assert_same_features(kps, desc, okps, odesc)
+    f = bgr.astype(np.float32)
+    g = (f[..., 0] * np.float32(0.114) + f[..., 1] * np.float32(0.587)) + f[..., 2] * np.float32(0.299)
+    kps, desc = sift_impl.compute_keypoints_and_descriptors(f)
+    okps, odesc = osift.detect_and_describe(g)
+    _assert_same_features(kps, desc, okps, odesc)
+    # the pair paths keep taking 8-bit frames only
+    from vfx_image_stitching_amd import image_stitching_sift as iss
+    with pytest.raises(NotImplementedError):
+        iss.compute_shift_sift(f, f)

@@ -110,6 +110,7 @@ SIGNATURES = {
     "pano_sift_pyramid": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams)]),
     "pano_sift_base": (_I, [_P, _P, _I, _I, _I, ctypes.POINTER(SiftParams), _P]),
     "pano_sift_pyramid_base": (_I, [_P, _P, _I, _I, _I, _I, ctypes.POINTER(SiftParams)]),
+    "pano_sift_pyramid_kernels": (_I, [_P, _P, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_double), _I]),
     "pano_sift_reserve_levels": (_I, [_P, _I, _I, _I, _I, _I]),
     "pano_sift_set_level": (_I, [_P, _I, _I, _I, _I, _P]),
     "pano_sift_dog": (_I, [_P]),

@@ -287,6 +287,25 @@ int pano_sift_pyramid_base(pano_ctx *ctx, const float *base, int n, int H0, int 
     return launch_sift_pyramid_src(ctx, src, n, H0, W0, &p, false, true);
 }
 
+int pano_sift_pyramid_kernels(pano_ctx *ctx, const float *base, int n, int H0, int W0, int n_octaves,
+                              const double *kernels, int n_kernels) {
+    if (!ctx || !base || !kernels || n <= 0 || H0 <= 0 || W0 <= 0 || n_octaves <= 0)
+        return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_pyramid_kernels") : PANO_E_ARG;
+    if (n_octaves > PANO_MAX_OCTAVES)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_pyramid_kernels: more than PANO_MAX_OCTAVES octaves");
+    for (int l = 1; l < n_kernels; ++l)
+        if (!(kernels[l] >= 0.0))
+            return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_pyramid_kernels: negative or NaN sigma");
+    pano_sift_params p;
+    pano_sift_default_params(&p);
+    PyrSource src;
+    src.base = base;
+    src.max_oct = n_octaves;
+    src.sig = kernels;
+    src.n_sig = n_kernels;
+    return launch_sift_pyramid_src(ctx, src, n, H0, W0, &p, false, true);
+}
+
 int pano_sift_reserve_levels(pano_ctx *ctx, int n, int H0, int W0, int n_octaves, int n_levels) {
     if (!ctx || n <= 0 || H0 <= 0 || W0 <= 0 || n_octaves <= 0 || n_levels < 3 || n_levels > PANO_MAX_LEVELS)
         return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_reserve_levels") : PANO_E_ARG;

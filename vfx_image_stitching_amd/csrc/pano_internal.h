@@ -214,6 +214,8 @@ struct PyrSource {
     const float *base = nullptr;     // [n][h][w] f32 base = octave 0, level 0 (generate_gaussian_images)
     int max_oct = 0;                 // base source: the caller's num_octaves
     bool base_only = false;          // stop after level 0 of octave 0 (generate_base_image)
+    const double *sig = nullptr;     // base source: the caller's kernel list (level l blurs level
+    int n_sig = 0;                   // l - 1 by sig[l]; n_sig levels), else the parameters' list
 };
 int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, int w,
                             const pano_sift_params *p, bool defer_tail, bool full);

@@ -1745,6 +1745,14 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     const int gh = src.base ? std::max(1, h / 2) : h, gw = src.base ? std::max(1, w / 2) : w;
     int rc = sift_plan(p, gh, gw, &no, &nl, &sb, sl);
     if (rc) return pano_fail(ctx, rc, "unsupported SIFT parameters");
+    if (src.base && src.sig) {
+        // generate_gaussian_images(base, n, kernels) with the caller's list (sift_impl.py:82-97:
+        // level l = GaussianBlur(level l - 1, kernels[l]); the next octave from level -3)
+        if (src.n_sig < 3 || src.n_sig > PANO_MAX_LEVELS)
+            return pano_fail(ctx, PANO_E_UNSUPPORTED, "gaussian kernel list: 3 to PANO_MAX_LEVELS entries");
+        nl = src.n_sig;
+        for (int l = 0; l < nl; ++l) sl[l] = src.sig[l];
+    }
     rc = src.base ? sift_reserve_dims(ctx, n, h, w, src.max_oct, nl) : sift_reserve_pyramid(ctx, n, h, w, p);
     if (rc) return rc;
     no = ctx->n_oct;

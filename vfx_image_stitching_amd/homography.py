@@ -114,8 +114,8 @@ def match_homography(img1, img2, ratio=0.7, reproj_thr=5.0, min_match_count=MIN_
     where ``outline`` is the query frame's corners mapped into the train frame (None without
     a homography)."""
     from .keypoint import from_records
-    from .sift_impl import _as_bgr_u8, _stitcher
-    a, b = _as_bgr_u8(img1), _as_bgr_u8(img2)
+    from .sift_impl import _frame_u8, _stitcher
+    a, b = _frame_u8(img1), _frame_u8(img2)
     st = _stitcher(1.6, 3, 0.5, 5)
     feats = st.features_of([a, b])
     res = find_pair_homographies(st, feats, [(0, 1)], ratio, reproj_thr, min_match_count, n_hyp, seed)[0]

@@ -19,11 +19,11 @@ from .stitching import run_panorama as _run
 def compute_shift_sift(imgA, imgB, ransac_thr=3, desc_thresh=25000):
     """Frames may differ in shape: the reference extracts each frame's features on its own
     (image_stitching_sift.py:59-60); so does features_of."""
-    from .sift_impl import _as_bgr_u8, _stitcher
+    from .sift_impl import _frame_u8, _stitcher
     st = _stitcher(1.6, 3, 0.5, 5)
     st.ransac_thr = float(ransac_thr)
     st.desc_thresh = float(desc_thresh)
-    feats = st.features_of([_as_bgr_u8(imgA), _as_bgr_u8(imgB)])
+    feats = st.features_of([_frame_u8(imgA), _frame_u8(imgB)])
     recs, _ = st.pair_records(feats, [(0, 1)])
     r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
     if r["status"] == _lib.PANO_E_OVERFLOW:

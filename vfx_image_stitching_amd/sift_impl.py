@@ -33,24 +33,62 @@ def _stitcher(sigma, num_intervals, assumed_blur, border):
     return st
 
 
-def _as_bgr_u8(image) -> np.ndarray:
+def _as_bgr_u8(image):
+    """The frame as u8 BGR for the batched chain, or None when the reference's arithmetic
+    differs from that chain's: a non-u8 BGR image goes through cv2.cvtColor's float formula
+    (not the u8 fixed-point one), a non-integer gray image through float levels."""
     img = np.asarray(image)
+    if img.ndim == 3 and img.shape[2] == 3:
+        return np.ascontiguousarray(img) if img.dtype == np.uint8 else None
+    if img.ndim != 2:
+        raise ValueError("expected an H x W x 3 BGR or H x W gray image")
     if img.dtype != np.uint8:
         r = np.rint(img)
         if not (np.array_equal(r, img) and img.min() >= 0 and img.max() <= 255):
-            raise NotImplementedError("libpano SIFT takes 8-bit images (the reference's inputs)")
+            return None
         img = r.astype(np.uint8)
+    # (1868 g + 9617 g + 4899 g + 8192) >> 14 == g: gray survives the BGR2GRAY step
+    return np.ascontiguousarray(np.repeat(img[..., None], 3, axis=2))
+
+
+def _frame_u8(image):
+    """_as_bgr_u8 for the batched pair paths (compute_shift_sift, match_homography), whose
+    reference inputs are cv2.imread frames: other images are refused."""
+    bgr = _as_bgr_u8(image)
+    if bgr is None:
+        raise NotImplementedError("the pair paths take 8-bit frames (cv2.imread's); "
+                                  "compute_keypoints_and_descriptors takes float images")
+    return bgr
+
+
+def _gray_f32(image):
+    """sift_impl.py:27-29 for the images the batched chain does not take: cv2.cvtColor
+    BGR2GRAY of a float BGR image (B * 0.114 + G * 0.587 + R * 0.299 in float32, OpenCV's
+    scalar order; its SIMD body may fuse -- parity unpinned for float BGR input, no cv2 here),
+    computed on the device, then astype(float32)."""
+    img = np.asarray(image)
     if img.ndim == 2:
-        # (1868 g + 9617 g + 4899 g + 8192) >> 14 == g: gray survives the BGR2GRAY step
-        img = np.repeat(img[..., None], 3, axis=2)
-    if img.ndim != 3 or img.shape[2] != 3:
-        raise ValueError("expected an H x W x 3 BGR or H x W gray image")
-    return np.ascontiguousarray(img)
+        return np.ascontiguousarray(img, np.float32)
+    ctx, torch, dev = _dev()
+    t = torch.from_numpy(np.ascontiguousarray(img, np.float32)).to(dev)
+    g = (t[..., 0] * 0.114 + t[..., 1] * 0.587) + t[..., 2] * 0.299
+    return g.cpu().numpy()
 
 
 def compute_keypoints_and_descriptors(image, sigma=1.6, num_intervals=3, assumed_blur=0.5,
                                       image_border_width=5):
     bgr = _as_bgr_u8(image)
+    if bgr is None:
+        # the reference's own sequence (sift_impl.py:27-38) through the stage functions below,
+        # every stage a libpano launch: float images whose gray is not an 8-bit one
+        gray = _gray_f32(image)
+        base = generate_base_image(gray, sigma, assumed_blur)
+        gauss = generate_gaussian_images(base, compute_number_of_octaves(base.shape),
+                                         generate_gaussian_kernels(sigma, num_intervals))
+        dogs = generate_DoG_images(gauss)
+        kps = find_scale_space_extrema(gauss, dogs, num_intervals, sigma, image_border_width)
+        kps = convert_keypoints_to_input_image_size(remove_duplicate_keypoints(kps))
+        return kps, generate_descriptors(kps, gauss)
     st = _stitcher(sigma, num_intervals, assumed_blur, image_border_width)
     kps, desc, counts = st.features_fit(st.upload(bgr[None]))
     n = int(counts.cpu()[0])
@@ -219,31 +257,30 @@ def generate_base_image(image, sigma, assumed_blur):
     return out.cpu().numpy()
 
 
-def _kernel_params(gaussian_kernels):
-    """(sigma, num_intervals) of a generate_gaussian_kernels list; libpano derives the level
-    sigmas itself, so other lists are refused rather than silently replaced."""
-    k = np.asarray(gaussian_kernels, np.float64).ravel()
-    ni = len(k) - 3
-    if ni < 1 or not np.array_equal(k, generate_gaussian_kernels(float(k[0]), ni)):
-        raise NotImplementedError("gaussian_kernels must come from generate_gaussian_kernels(sigma, n)")
-    return float(k[0]), ni
-
-
 def generate_gaussian_images(image, num_octaves, gaussian_kernels):
-    """sift_impl.py:82-97 on any f32 base image (pano_sift_pyramid_base): per octave the
-    cascaded blurs of gaussian_kernels[1:], next base = INTER_NEAREST 1/2 of level -3."""
+    """sift_impl.py:82-97 on any f32 base image and any kernel list (pano_sift_pyramid_kernels):
+    per octave level l = GaussianBlur(level l - 1, gaussian_kernels[l]), next base =
+    INTER_NEAREST 1/2 of level -3."""
     import ctypes
-    sigma, ni = _kernel_params(gaussian_kernels)
+    k = np.ascontiguousarray(np.asarray(gaussian_kernels, np.float64).ravel())
+    if len(k) < 3:
+        # the reference indexes level -3 for the next octave's base
+        raise IndexError("generate_gaussian_images needs at least 3 kernels")
     base = _f32_2d(image, "generate_gaussian_images")
     ctx, torch, dev = _dev()
     src = torch.from_numpy(base).to(dev)
     H0, W0 = base.shape
-    p = _params(sigma=sigma, num_intervals=ni)
-    ctx.check(ctx.lib.pano_sift_pyramid_base(ctx.h, _lib.ptr(src), 1, H0, W0, int(num_octaves),
-                                             ctypes.byref(p)))
+    rc = ctx.lib.pano_sift_pyramid_kernels(ctx.h, _lib.ptr(src), 1, H0, W0, int(num_octaves),
+                                           k.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(k))
+    try:
+        ctx.check(rc)
+    except _lib.PanoError as e:
+        if e.code == _lib.PANO_E_UNSUPPORTED:     # a kernel wider than PANO_MAX_TAPS, > max levels
+            raise NotImplementedError(str(e)) from e
+        raise
     no = ctypes.c_int32()
     ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, 0, None, None, ctypes.byref(no)))
-    return _read_levels(ctx, no.value, ni + 3, dog=False)
+    return _read_levels(ctx, no.value, len(k), dog=False)
 
 
 def generate_DoG_images(gaussian_images):
