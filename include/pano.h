@@ -444,6 +444,9 @@ int pano_graph_launch(pano_ctx *ctx, pano_graph *g);
  * stitch's whole per-call GPU work as one call (its last node copies the result header to
  * pinned host memory, pano_copy_async). */
 int pano_graph_launch_sync(pano_ctx *ctx, pano_graph *g, void *hip_stream);
+/* Replay g on `hip_stream` (NULL: the context's stream) without waiting: a caller keeping two
+ * stitches in flight (Stitcher.run_sequence) waits on its own event per replay. */
+int pano_graph_launch_stream(pano_ctx *ctx, pano_graph *g, void *hip_stream);
 /* Copy on the context's stream (device or pinned host pointers; capturable): up to 1 MiB as
  * a copy kernel (the GPU writes pinned host memory directly), larger as hipMemcpyAsync. */
 int pano_copy_async(pano_ctx *ctx, void *dst, const void *src, size_t bytes);

@@ -206,3 +206,28 @@ def test_release_scratch_then_replay_recaptures(gpu, parrington, gold_json):
     for _ in range(2):
         assert digest(st.run(dev, pfo, margin=pm, graph=True).panorama.cpu().numpy()) == want
     st.release_graphs()
+
+
+def test_run_sequence_matches_run(gpu, parrington):
+    """Stitcher.run_sequence (two stitches in flight, alternating output slots) yields the same
+    panoramas and shifts as synchronous run() calls, over a sequence mixing two frame sets (the
+    set changes exercise its drain-and-run fallback); run() works as before afterwards."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = parrington
+    st = Stitcher("sift")
+    devA, devB = st.upload(frames), st.upload(frames[:8])
+    fA, fB = list(focals), list(focals)[:8]
+    want = {}
+    for key, dev, f in (("A", devA, fA), ("B", devB, fB)):
+        r = st.run(dev, f, margin=margin, graph=True)
+        want[key] = (r.panorama.cpu().numpy().copy(), list(r.shifts))
+    seq = ["A", "A", "A", "B", "A", "B", "B", "B", "A", "A", "A", "A"]
+    items = [(devA, fA) if k == "A" else (devB, fB) for k in seq]
+    n = 0
+    for k, r in zip(seq, st.run_sequence(items, margin=margin)):
+        np.testing.assert_array_equal(r.panorama.cpu().numpy(), want[k][0], err_msg=f"item {n} ({k})")
+        assert list(r.shifts) == want[k][1]
+        n += 1
+    assert n == len(seq)
+    r = st.run(devA, fA, margin=margin, graph=True)
+    np.testing.assert_array_equal(r.panorama.cpu().numpy(), want["A"][0])

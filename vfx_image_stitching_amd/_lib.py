@@ -152,6 +152,7 @@ SIGNATURES = {
     "pano_graph_end": (_I, [_P, ctypes.POINTER(_P)]),
     "pano_graph_launch": (_I, [_P, _P]),
     "pano_graph_launch_sync": (_I, [_P, _P, _P]),
+    "pano_graph_launch_stream": (_I, [_P, _P, _P]),
     "pano_copy_async": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "pano_graph_prof": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int), _PD]),
     "pano_graph_destroy": (_I, [_P]),

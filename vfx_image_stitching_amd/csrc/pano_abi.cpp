@@ -628,6 +628,12 @@ int pano_graph_launch(pano_ctx *ctx, pano_graph *g) {
     return PANO_OK;
 }
 
+int pano_graph_launch_stream(pano_ctx *ctx, pano_graph *g, void *stream) {
+    if (!ctx || !g) return PANO_E_ARG;
+    PANO_HIP(ctx, hipGraphLaunch(g->exec, stream ? (hipStream_t)stream : ctx->stream));
+    return PANO_OK;
+}
+
 int pano_graph_launch_sync(pano_ctx *ctx, pano_graph *g, void *stream) {
     if (!ctx || !g) return PANO_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;

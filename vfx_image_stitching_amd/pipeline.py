@@ -99,7 +99,13 @@ class Stitcher:
         self._graph_mode = False
         self._fast = None                # (key, replay state) of run()'s graph fast path
         self._fast_key = None
-        self._views = None               # (key, canvas view, panorama view) of _crop_planned
+        self._views = {}                 # key -> (canvas view, panorama view) of _crop_planned
+        # output slots of the device-planned stitch (run_sequence keeps two stitches in flight):
+        # slot s has its own result / canvas / pinned head buffers, hence its own graph and
+        # fast-path state; run() uses slot 0
+        self._slot = 0
+        self._slot_state = {}            # slot -> (fast, fast_key, head_np) while not current
+        self._head_np = None
 
     # ------------------------------------------------------------------ buffers
     def _get(self, name, shape, dtype):
@@ -335,10 +341,14 @@ class Stitcher:
         g = self._graphs.pop(key)[0]
         if self._fast is not None and self._fast[1][0] is g:
             self._fast = None
+        for sl, st in list(self._slot_state.items()):
+            if st[0] is not None and st[0][1][0] is g:
+                self._slot_state[sl] = (None, None, st[2])
         self.ctx.graph_destroy(g)
 
     def release_graphs(self):
         self._fast = None
+        self._slot_state = {sl: (None, None, st[2]) for sl, st in self._slot_state.items()}
         for ent in self._graphs.values():
             self.ctx.graph_destroy(ent[0])
         self._graphs.clear()
@@ -376,19 +386,20 @@ class Stitcher:
         lib, c = self.ctx.lib, self.ctx.h
         off_bb = P * 64
         off_plan = (off_bb + 4 * BBOX_SLOTS * 4 + 255) // 256 * 256
-        res = self._get("result", (off_plan + int(lib.pano_plan_device_bytes()),), T.uint8)
+        sfx = f"@{self._slot}" if self._slot else ""
+        res = self._get("result" + sfx, (off_plan + int(lib.pano_plan_device_bytes()),), T.uint8)
         # canvas capacity: every step pads by at most one frame width (|dx| <= w for real
         # overlaps) and the drift-corrected rows stay within one frame height; a plan above
         # it reports PANO_E_OVERFLOW and run() composites with the host plan instead
         Hcap, Wcap = self.canvas_cap or (2 * h, (n + 2) * w)
-        canvas = self._get("canvas_cap", (Hcap * Wcap * 3,), T.uint8)
+        canvas = self._get("canvas_cap" + sfx, (Hcap * Wcap * 3,), T.uint8)
 
         nhead = off_plan + 32
-        pin = self._buf.get("head_pin")
+        pin = self._buf.get("head_pin" + sfx)
         if pin is None or pin.numel() < nhead:
             pin = T.empty(max(nhead, 4096), dtype=T.uint8, pin_memory=True)
-            self._buf["head_pin"] = pin
-            self._head_np = pin.numpy()
+            self._buf["head_pin" + sfx] = pin
+        self._head_np = pin.numpy()
 
         def seg():
             cyl, colnz = self.cylindrical(frames_dev, focals)
@@ -460,6 +471,100 @@ class Stitcher:
             return None
         return 1 << int(np.ceil(np.log2(int(c.max()))))
 
+    def _use_slot(self, sl):
+        """Make output slot sl current: its buffers, graph fast path and pinned head."""
+        if sl == self._slot:
+            return
+        self._slot_state[self._slot] = (self._fast, self._fast_key, self._head_np)
+        self._fast, self._fast_key, self._head_np = self._slot_state.pop(sl, (None, None, None))
+        self._slot = sl
+
+    def run_sequence(self, items, margin: int = 15):
+        """Generator: run(..., graph=True) over a sequence of stitches -- items: (frames_dev,
+        focals) pairs, e.g. consecutive frame sets of a video or one set re-stitched -- with two
+        in flight: stitch i + 1 is launched before the host reads stitch i's head and builds its
+        result, so the GPU does not idle while the host finishes a stitch (the host gap between
+        synchronous run() calls).  Stitches alternate between two output slots; a
+        yielded result stays valid until the generator is resumed (run()'s rule: until the next
+        call).  A stitch the replay cannot finish (first use of a slot, a capacity or plan
+        overflow, a missing match) drains the pipeline and goes through run()."""
+        items = list(items)
+        T = self.torch
+        inflight = None                  # (index, slot, event, replay state)
+
+        def launch(i):
+            sl = i % 2
+            self._use_slot(sl)
+            frames_dev, focals = items[i]
+            fast = self._fast
+            if (fast is None or fast[0] != self._fast_key_of(frames_dev, focals)
+                    or fast[1][7] != self.ctx.generation()):
+                return None
+            g = fast[1][0]
+            self.ctx.check(self.ctx.lib.pano_graph_launch_stream(self.ctx.h, g, _lib._P(self._raw_stream())))
+            ev = T.cuda.Event()
+            ev.record()
+            return (i, sl, ev, fast[1])
+
+        def finish(job):
+            i, sl, ev, state = job
+            _, cyl, colnz, off_bb, off_plan, nhead, canvas, _ = state
+            t0 = time.perf_counter()
+            ev.synchronize()
+            head = self._slot_head(sl)[:nhead]
+            hdr = int(head[off_plan:off_plan + 4].view(np.int32)[0])
+            if hdr != _lib.PANO_OK or head[:off_bb].view(np.int32).reshape(-1, 16)[:, 15].any():
+                return None
+            self._use_slot(sl)
+            return self._from_head(head, off_bb, off_plan, canvas, cyl, colnz, margin, True, {}, t0)
+
+        try:
+            i = 0
+            while i < len(items) or inflight is not None:
+                nxt = launch(i) if i < len(items) else None
+                if i < len(items) and nxt is None:
+                    # not replayable yet: drain, then the synchronous path (captures the graph)
+                    if inflight is not None:
+                        job, inflight = inflight, None
+                        r = finish(job)
+                        yield r if r is not None else self._rerun(items, job[0], margin)
+                    yield self._rerun(items, i, margin)
+                    i += 1
+                    continue
+                if inflight is not None:
+                    job, inflight = inflight, None
+                    r = finish(job)
+                    if r is None:
+                        # drain the launched successor, redo this stitch synchronously, then
+                        # re-issue the successor
+                        if nxt is not None:
+                            nxt[2].synchronize()
+                        yield self._rerun(items, job[0], margin)
+                        if nxt is not None:
+                            i = nxt[0]
+                            continue
+                    else:
+                        yield r
+                inflight = nxt
+                i += 1
+        finally:
+            if inflight is not None:
+                inflight[2].synchronize()
+            self._use_slot(0)
+
+    def _rerun(self, items, i, margin):
+        self._use_slot(i % 2)
+        return self.run(items[i][0], items[i][1], margin=margin, graph=True)
+
+    def _slot_head(self, sl):
+        return self._head_np if sl == self._slot else self._slot_state[sl][2]
+
+    def _fast_key_of(self, frames_dev, focals):
+        return (frames_dev.data_ptr(), tuple(frames_dev.shape),
+                np.asarray(focals, np.float64).tobytes(), self.canvas_cap, self.method, self.match,
+                self.ratio, self.desc_thresh, self.ransac_thr, bytes(self.params), self.cap,
+                self.max_points)
+
     def _run(self, frames_dev, focals, margin, graph, device_plan):
         t = {}
         tick = time.perf_counter
@@ -469,10 +574,7 @@ class Stitcher:
         if device_plan and 2 <= n <= 256:
             self._graph_mode = graph
             # replay fast path: same frames buffer, focals and settings as the last replay
-            fk = (frames_dev.data_ptr(), tuple(frames_dev.shape),
-                  np.asarray(focals, np.float64).tobytes(), self.canvas_cap, self.method, self.match,
-                  self.ratio, self.desc_thresh, self.ransac_thr, bytes(self.params), self.cap,
-                  self.max_points) if graph else None
+            fk = self._fast_key_of(frames_dev, focals) if graph else None
             fast = self._fast
             if fast is not None and fast[0] == fk and fast[1][7] == self.ctx.generation():
                 g, cyl, colnz, off_bb, off_plan, nhead, canvas, _ = fast[1]
@@ -483,36 +585,42 @@ class Stitcher:
             else:
                 self._fast_key = fk
                 cyl, colnz, head, off_bb, off_plan, canvas = self._planned(frames_dev, focals)
-            head = head.copy()          # ONE read of the pinned head; the next run() reuses it
-            recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1)
-            hdr = head[off_plan:off_plan + 32].view(np.int32)
-            t["features_match_ransac"] = tick() - t0
-            status = head[:off_bb].view(np.int32).reshape(-1, 16)[:, 15]     # PAIR_NP.status
-            if status.any():
-                self._check_records(recs)
-            if hdr[0] == _lib.PANO_E_NOMATCH:
-                raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
-            if hdr[0] == _lib.PANO_OK:
-                if self.method == "sift" and not status.any():
-                    # the records' six doubles (dx dy xA yA xB yB) in one conversion
-                    rows = head[:off_bb].view(np.float64).reshape(-1, 8)[:, :6].tolist()
-                    shifts = [(r[0], r[1]) for r in rows]
-                    best_pairs = [((r[2], r[3]), (r[4], r[5])) for r in rows]
-                else:
-                    shifts, best_pairs = self._shifts(recs)
-                H, W = int(hdr[1]), int(hdr[2])
-                # crop box: min of ymin / xmin and max of ymax / xmax over the partial boxes,
-                # as one min over the sign-flipped columns
-                slots = head[off_bb:off_bb + 16 * BBOX_SLOTS].view(np.int32).reshape(BBOX_SLOTS, 4)
-                m = (slots * _BOX_SIGN).min(axis=0).tolist()
-                bb = (m[0], -m[1], m[2], -m[3])
-                return self._crop_planned(canvas, H, W, bb, margin, shifts, best_pairs, recs, t, t0)
-            # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
-            return self._finish(cyl, colnz, recs, margin, graph, t, t0)
+            return self._from_head(head, off_bb, off_plan, canvas, cyl, colnz, margin, graph, t, t0)
         cyl, colnz, recs_dev = self.records(frames_dev, focals, graph)
         recs = recs_dev.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)   # sync point 1
         t["features_match_ransac"] = tick() - t0
         self._check_records(recs)
+        return self._finish(cyl, colnz, recs, margin, graph, t, t0)
+
+    def _from_head(self, head, off_bb, off_plan, canvas, cyl, colnz, margin, graph, t, t0):
+        """The StitchResult of a device-planned stitch from its pinned head (records, crop box,
+        plan header)."""
+        tick = time.perf_counter
+        head = head.copy()          # ONE read of the pinned head; the next run() reuses it
+        recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1)
+        hdr = head[off_plan:off_plan + 32].view(np.int32)
+        t["features_match_ransac"] = tick() - t0
+        status = head[:off_bb].view(np.int32).reshape(-1, 16)[:, 15]     # PAIR_NP.status
+        if status.any():
+            self._check_records(recs)
+        if hdr[0] == _lib.PANO_E_NOMATCH:
+            raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+        if hdr[0] == _lib.PANO_OK:
+            if self.method == "sift" and not status.any():
+                # the records' six doubles (dx dy xA yA xB yB) in one conversion
+                rows = head[:off_bb].view(np.float64).reshape(-1, 8)[:, :6].tolist()
+                shifts = [(r[0], r[1]) for r in rows]
+                best_pairs = [((r[2], r[3]), (r[4], r[5])) for r in rows]
+            else:
+                shifts, best_pairs = self._shifts(recs)
+            H, W = int(hdr[1]), int(hdr[2])
+            # crop box: min of ymin / xmin and max of ymax / xmax over the partial boxes,
+            # as one min over the sign-flipped columns
+            slots = head[off_bb:off_bb + 16 * BBOX_SLOTS].view(np.int32).reshape(BBOX_SLOTS, 4)
+            m = (slots * _BOX_SIGN).min(axis=0).tolist()
+            bb = (m[0], -m[1], m[2], -m[3])
+            return self._crop_planned(canvas, H, W, bb, margin, shifts, best_pairs, recs, t, t0)
+        # PANO_E_OVERFLOW: composite with the host plan below, reusing the records
         return self._finish(cyl, colnz, recs, margin, graph, t, t0)
 
     @staticmethod
@@ -557,13 +665,15 @@ class Stitcher:
         # the two views of the same buffer and geometry are reused from the last call (a
         # replayed stitch usually has both): creating them costs more than the rest of run()
         vk = (buf.data_ptr(), H, W, y0, y1, x0, x1)
-        views = self._views
-        if views is None or views[0] != vk:
+        views = self._views.get(vk)
+        if views is None:
             canvas = buf.as_strided((H, W, 3), (W * 3, 3, 1))
             pano = canvas if (bb[1] < 0 or y0 > y1 or x0 > x1) else buf.as_strided(
                 (y1 + 1 - y0, x1 + 1 - x0, 3), (W * 3, 3, 1), buf.storage_offset() + y0 * W * 3 + x0 * 3)
-            self._views = views = (vk, canvas, pano)
-        canvas, pano = views[1], views[2]
+            if len(self._views) >= 8:
+                self._views.clear()
+            self._views[vk] = views = (canvas, pano)
+        canvas, pano = views
         t["total"] = time.perf_counter() - t0
         return StitchResult(pano, canvas, shifts, best_pairs, recs, (y0, y1, x0, x1), t)
 
