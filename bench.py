@@ -117,7 +117,7 @@ def parse():
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch eagerly instead of replaying captured hipGraphs")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="N=1 graph mode: one synchronous run() per step instead of "
+                    help="N=1 graph mode: time one synchronous run() per step instead of "
                          "Stitcher.run_sequence (two stitches in flight)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: a fixed sequence per rank (default); strong: ONE fixed sequence "
@@ -271,11 +271,14 @@ def main():
     # ROCm rejects timing events recorded inside graphs (hipErrorInvalidHandle), so the
     # dominant kernel is timed with the same events over K eager steps run right after.
     # N = 1 with graphs: the K stitches go through Stitcher.run_sequence, which launches stitch
-    # k + 1 before the host finishes stitch k (every stitch still completes and is read back)
+    # k + 1 before the host finishes stitch k (every stitch still completes and is read back);
+    # the same K stitches as synchronous run() calls are timed beside it (--no-pipeline: the
+    # other way round).
     pipelined = world == 1 and args.graph and args.pipeline
+    seq_beside = world == 1 and args.graph and not args.pipeline
     if args.graph:
         step(graph=True)
-        if pipelined:
+        if pipelined or seq_beside:
             for _ in st.run_sequence([(dev, focals)] * 3, margin=margin):   # both output slots
                 pass
         torch.cuda.synchronize()
@@ -296,15 +299,19 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    ms_sync = None
-    if pipelined:
-        # the same K stitches as synchronous run() calls, for the record (not `value`)
+    ms_other = None
+    if pipelined or seq_beside:
+        # the same K stitches in the other form, for the record (not `value`)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        for _ in range(args.steps):
-            step(graph=True)
+        if pipelined:
+            for _ in range(args.steps):
+                step(graph=True)
+        else:
+            for _ in st.run_sequence([(dev, focals)] * args.steps, margin=margin):
+                pass
         torch.cuda.synchronize()
-        ms_sync = (time.perf_counter() - t1) / args.steps * 1e3
+        ms_other = (time.perf_counter() - t1) / args.steps * 1e3
     if args.graph:
         ctx.prof_enable(rk)
         ctx.prof_read(rk)
@@ -422,10 +429,9 @@ def main():
         else f"Mpixels/s stitched ({args.workload}, {args.method})",
         "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-        "pipelined": {"two_in_flight": True, "ms_per_step_sync_run": round(ms_sync, 4),
-                      "note": "Stitcher.run_sequence: stitch k + 1 launched before the host reads "
-                              "stitch k's head; ms_per_step_sync_run = the same stitches as "
-                              "synchronous run() calls"} if ms_sync is not None else None,
+        "timed_form": "run_sequence" if pipelined else "run",
+        "run_sequence_ms_per_step" if seq_beside else "run_ms_per_step":
+            round(ms_other, 4) if ms_other is not None else None,
         "higher_is_better": True,
         "scaling": args.scaling, "vs_baseline": None,
         "dtype": ("u8 frames; f32 pyramid (OpenCV's float32 FMA blur order); match " +
