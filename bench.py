@@ -52,11 +52,16 @@ MFMA_F32_PEAK_TFLOPS = 157.3    # dense f32 MFMA
 F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X f32 vector peak (v_pk_fma_f32), the blur's arithmetic
 
 
-def pmc_traffic(kernel, workload, method):
+PMC_PROFILE_FRAMES = {"parrington": 18, "synthetic": 19}   # frames of the profiled step
+
+
+def pmc_traffic(kernel, workload, method, n_frames):
     """HBM bytes per launch of a kernel class from the newest committed PMC traffic profile
     (tools/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over the same
     SIFT step -- parrington, or the 19-frame synthetic 1080p one -- corrected per
-    profiles/r01_fetch_calibration.txt)."""
+    profiles/r01_fetch_calibration.txt).  A step of another frame count (the strong-scaling
+    batch: 144 frames on one GPU) gets the profile's bytes scaled per frame -- every class
+    here moves bytes in proportion to its frames -- and the source says so."""
     import glob
     if workload not in ("parrington", "synthetic") or method != "sift":
         return None, None
@@ -67,7 +72,13 @@ def pmc_traffic(kernel, workload, method):
     c = d.get("classes", {}).get(kernel)
     if not c or not c.get("launches_per_step"):
         return None, None
-    return c["hbm_bytes_per_step"] / c["launches_per_step"], os.path.relpath(files[-1], ROOT)
+    per_launch = c["hbm_bytes_per_step"] / c["launches_per_step"]
+    src = os.path.relpath(files[-1], ROOT)
+    prof_frames = d.get("frames", PMC_PROFILE_FRAMES[workload])
+    if n_frames != prof_frames:
+        per_launch *= n_frames / prof_frames
+        src += f" (a {prof_frames}-frame step, scaled per frame to {n_frames} frames)"
+    return per_launch, src
 
 
 def blur_f32_flops(st, n_frames):
@@ -346,7 +357,7 @@ def main():
         if byts is not None:
             per_launch_bytes = byts / launches_per_step
             ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
-            traffic, tsrc = pmc_traffic(rk, args.workload, args.method)
+            traffic, tsrc = pmc_traffic(rk, args.workload, args.method, n_local)
             roof = {"bound": "hbm", "kernel": rk, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                     "timing": ("HIP events on the library stream, %d eager steps right after the "
                                "graph-replayed timed region" % args.steps) if args.graph

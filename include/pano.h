@@ -196,6 +196,11 @@ int pano_sift_localize(pano_ctx *ctx, const pano_sift_params *params, const floa
 int pano_sift_orient(pano_ctx *ctx, const pano_sift_params *params, const float *d_gauss, int h, int w,
                      int octave, const pano_kp *d_kps, int n, pano_kp *d_out, int32_t *d_counts);
 
+/* cv2.cvtColor(image, COLOR_BGR2GRAY) on a float32 BGR image (sift_impl.py:27-28, the drop-in's
+ * float path): d_bgr [n][h][w][3] f32 -> d_gray [n][h][w] f32, OpenCV's scalar RGB2Gray<float>
+ * order b * 0.114f + g * 0.587f + r * 0.299f (parity with its SIMD body unpinned). */
+int pano_gray_bgr_f32(pano_ctx *ctx, const float *d_bgr, int n, int h, int w, float *d_gray);
+
 int pano_sift_base(pano_ctx *ctx, const float *d_gray, int n, int h, int w,
                    const pano_sift_params *params, float *d_base);
 int pano_sift_pyramid_base(pano_ctx *ctx, const float *d_base, int n, int H0, int W0, int n_octaves,
@@ -244,6 +249,11 @@ int pano_match(pano_ctx *ctx, const float *d_desc, const int32_t *d_counts, int 
 int pano_match_u8(pano_ctx *ctx, const uint8_t *d_desc_u8, const int32_t *d_norms,
                   const int32_t *d_counts, int cap, const int32_t *h_pairs, int n_pairs,
                   int32_t *d_best, float *d_d1, float *d_d2);
+
+/* The exact squared norms pano_match_u8 reads, for byte descriptors that did not come from
+ * pano_sift_u8 (which writes them itself): d_norms[r] = sum of d_desc_u8[r][0..127]^2, rows
+ * 16-byte aligned (the `np.dot(d, d)` of image_stitching_sift.py:71 on integer rows). */
+int pano_desc_norms_u8(pano_ctx *ctx, const uint8_t *d_desc_u8, int rows, int32_t *d_norms);
 
 /* ---------------------------------------------------------------- R1
  * Match filter (distance < desc_thresh, optional Lowe ratio d1 < ratio*d2 when ratio > 0;

@@ -231,3 +231,28 @@ def test_run_sequence_matches_run(gpu, parrington):
     assert n == len(seq)
     r = st.run(devA, fA, margin=margin, graph=True)
     np.testing.assert_array_equal(r.panorama.cpu().numpy(), want["A"][0])
+
+
+def test_run_sequence_distinct_buffers(gpu, parrington):
+    """The video case: every item a distinct device buffer of the same shape.
+    Items go through the slots' staging buffers, so each slot's graph is captured once and
+    replayed for every later buffer (graph count bounded), with the same panoramas as run()."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    names, frames, focals, margin = parrington
+    st = Stitcher("sift")
+    sets = [np.roll(frames, k, axis=0) for k in (0, 3, 7)]
+    fsets = [list(np.roll(np.asarray(focals), k)) for k in (0, 3, 7)]
+    want = []
+    for fr, fo in zip(sets, fsets):
+        r = st.run(st.upload(fr), fo, margin=margin)
+        want.append(r.panorama.cpu().numpy().copy())
+    st.release_graphs()
+    order = [0, 1, 2, 1, 0, 2, 2, 0, 1, 0]
+    items = [(st.upload(sets[k]), fsets[k]) for k in order]      # ten distinct buffers
+    n = 0
+    for k, r in zip(order, st.run_sequence(items, margin=margin)):
+        np.testing.assert_array_equal(r.panorama.cpu().numpy(), want[k], err_msg=f"item {n}")
+        n += 1
+    assert n == len(order)
+    # staged: one captured stitch graph per (slot, focal set), not one per buffer
+    assert len(st._graphs) <= 2 * len(sets), len(st._graphs)

@@ -161,6 +161,25 @@ def test_pyramid_any_kernel_list(gpu, kernels):
         sift_impl.generate_gaussian_images(base, 2, [1.6, 1.0])
     with pytest.raises(NotImplementedError):
         sift_impl.generate_gaussian_images(base, 2, [1.6, 1.0, 40.0])    # 321 taps
+    for bad in ([1.6, 1.0, float("inf")], [1.6, float("nan"), 1.0], [1.6, 1.0, 7.9], [1.6, -1.0, 1.0]):
+        with pytest.raises(NotImplementedError):
+            sift_impl.generate_gaussian_images(base, 2, bad)
+
+
+def test_pyramid_kernels_abi_refuses_bad_counts(gpu):
+    """pano_sift_pyramid_kernels checks n_kernels (3 .. PANO_MAX_LEVELS) before it reads the
+    list: a short list with a huge count, and 2 or 9 levels, are refused, not read past."""
+    import ctypes
+
+    from vfx_image_stitching_amd import _lib
+    from vfx_image_stitching_amd import sift_impl
+    ctx, torch, dev = sift_impl._dev()
+    base = torch.zeros((32, 32), dtype=torch.float32, device=dev)
+    k = np.array([1.6, 1.2], np.float64)
+    kp = k.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    for n in (2, 9, 1 << 30, -1):
+        rc = ctx.lib.pano_sift_pyramid_kernels(ctx.h, _lib.ptr(base), 1, 32, 32, 2, kp, n)
+        assert rc == _lib.PANO_E_UNSUPPORTED, (n, rc)
 
 
 def test_float_gray_base_image(gpu, frames00):
@@ -308,7 +327,40 @@ def test_float_images_take_the_reference_sequence(gpu, frames00):
     kps, desc = sift_impl.compute_keypoints_and_descriptors(f)
     okps, odesc = osift.detect_and_describe(g)
     _assert_same_features(kps, desc, okps, odesc)
+    # the float gray itself (pano_gray_bgr_f32) equals the scalar formula bit for bit
+    np.testing.assert_array_equal(sift_impl._gray_f32(f), g)
     # the pair paths keep taking 8-bit frames only
     from vfx_image_stitching_amd import image_stitching_sift as iss
     with pytest.raises(NotImplementedError):
         iss.compute_shift_sift(f, f)
+
+
+def test_bgr_depths_cv2_refuses(gpu):
+    """cv2.cvtColor(BGR2GRAY) takes uint8, uint16 and float32 BGR only (sift_impl.py:27-28):
+    float64 BGR is refused with ValueError (cv2's "Unsupported depth"), uint16 with
+    NotImplementedError (cv2's 16-bit path is not restated); neither is silently converted."""
+    from vfx_image_stitching_amd import sift_impl
+    img = np.zeros((64, 64, 3))
+    with pytest.raises(ValueError):
+        sift_impl.compute_keypoints_and_descriptors(img.astype(np.float64))
+    with pytest.raises(ValueError):
+        sift_impl.compute_keypoints_and_descriptors(img.astype(np.int32))
+    with pytest.raises(NotImplementedError):
+        sift_impl.compute_keypoints_and_descriptors(img.astype(np.uint16))
+
+
+def test_desc_norms_kernel(gpu):
+    """pano_desc_norms_u8 equals the integer sum of squares per row (random bytes, 0 and 255
+    rows, a row count that is not a multiple of the wave's 8 rows)."""
+    import torch
+
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    st = Stitcher("sift")
+    rng = np.random.default_rng(3)
+    d = rng.integers(0, 256, size=(3, 37, 128), dtype=np.uint8)
+    d[0, 0] = 255
+    d[1, 5] = 0
+    dev = torch.from_numpy(d).cuda()
+    got = st.desc_norms(dev).cpu().numpy()
+    want = (d.astype(np.int64) ** 2).sum(-1)
+    np.testing.assert_array_equal(got, want)

@@ -141,6 +141,8 @@ SIGNATURES = {
     "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),
     "pano_blend_two": (_I, [_P, _P, _I, _I, _P, _I, _I, _PI32, _D, _P]),
     "pano_gray_bbox": (_I, [_P, _P, _I, _I, _I, _P]),
+    "pano_gray_bgr_f32": (_I, [_P, _P, _I, _I, _I, _P]),
+    "pano_desc_norms_u8": (_I, [_P, _P, _I, _P]),
     "pano_jpeg_info": (_I, [_P, ctypes.c_size_t, _PI32, _PI32, _PI32]),
     "pano_jpeg_decode": (_I, [_P, _I, _P, _P, _P, _I, _I, _P]),
     "pano_jpeg_stats": (_I, [_P, _PI32, _I]),

@@ -1,4 +1,4 @@
-// fill.hip -- stream-ordered byte fill used instead of hipMemsetAsync on every path that may
+// fill.hip -- small utility kernels.  Stream-ordered byte fill used instead of hipMemsetAsync on every path that may
 // be captured into a hipGraph: the fill is an ordinary kernel whose arguments (pointer,
 // byte, size) are captured by value, so replays never depend on the runtime's internal
 // memset implementation.  16 bytes per thread where alignment allows, bytes at the edges.
@@ -54,5 +54,59 @@ int launch_copy(pano_ctx *ctx, void *dst, const void *src, size_t bytes) {
     const unsigned blocks = (unsigned)std::min<size_t>((items + 255) / 256, 1024);
     copy_bytes<<<blocks, 256, 0, ctx->stream>>>((const uint8_t *)src, (uint8_t *)dst, bytes);
     PANO_LAUNCH_CHECK(ctx, "copy_bytes");
+    return PANO_OK;
+}
+
+// S0's float-BGR gray (sift_impl.py:27-28 on a float32 image): cv2.cvtColor(COLOR_BGR2GRAY),
+// OpenCV's RGB2Gray<float> scalar body dst = src[0] * 0.114f + src[1] * 0.587f + src[2] *
+// 0.299f, left to right, no contraction (the Makefile builds with -ffp-contract=off).  One
+// thread per pixel; [n][h][w][3] -> [n][h][w].
+__global__ void __launch_bounds__(256)
+gray_bgr_f32(const float *__restrict__ bgr, float *__restrict__ gray, size_t px) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= px) return;
+    const float *q = bgr + 3 * i;
+    gray[i] = (q[0] * 0.114f + q[1] * 0.587f) + q[2] * 0.299f;
+}
+
+int pano_gray_bgr_f32(pano_ctx *ctx, const float *bgr, int n, int h, int w, float *gray) {
+    if (!ctx || !bgr || !gray || n <= 0 || h <= 0 || w <= 0)
+        return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_gray_bgr_f32") : PANO_E_ARG;
+    const size_t px = (size_t)n * h * w;
+    gray_bgr_f32<<<(unsigned)((px + 255) / 256), 256, 0, ctx->stream>>>(bgr, gray, px);
+    PANO_LAUNCH_CHECK(ctx, "gray_bgr_f32");
+    return PANO_OK;
+}
+
+// Exact squared norms of byte descriptor rows (what pano_match_u8 reads beside the bytes):
+// one wave per 8 rows, 8 lanes per row, each lane 16 bytes (v_dot4_u32_u8 on its 4 words),
+// then a 3-step shuffle reduction inside the row's lane group.
+__global__ void __launch_bounds__(256)
+desc_norms_u8(const uint8_t *__restrict__ desc, int32_t *__restrict__ norms, int rows) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int r = t >> 3, part = t & 7;
+    uint32_t s = 0;
+    if (r < rows) {
+        const uint4 v = ((const uint4 *)(desc + (size_t)r * 128))[part];
+        s = __builtin_amdgcn_udot4(v.x, v.x, 0u, false);
+        s = __builtin_amdgcn_udot4(v.y, v.y, s, false);
+        s = __builtin_amdgcn_udot4(v.z, v.z, s, false);
+        s = __builtin_amdgcn_udot4(v.w, v.w, s, false);
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    if (r < rows && part == 0) norms[r] = (int32_t)s;
+}
+
+int pano_desc_norms_u8(pano_ctx *ctx, const uint8_t *desc, int rows, int32_t *norms) {
+    if (!ctx || rows < 0 || (rows && (!desc || !norms)))
+        return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_desc_norms_u8") : PANO_E_ARG;
+    if ((uintptr_t)desc & 15)
+        return pano_fail(ctx, PANO_E_ARG, "pano_desc_norms_u8: rows must be 16-byte aligned");
+    if (!rows) return PANO_OK;
+    const size_t threads = (size_t)rows * 8;
+    desc_norms_u8<<<(unsigned)((threads + 255) / 256), 256, 0, ctx->stream>>>(desc, norms, rows);
+    PANO_LAUNCH_CHECK(ctx, "desc_norms_u8");
     return PANO_OK;
 }

@@ -116,6 +116,35 @@ __global__ void __launch_bounds__(kEncThreads) jpeg_enc_blocks(EncDev D) {
     }
 }
 
+// In-place exclusive scan of v[0 .. n) by one 1024-thread workgroup, 1024 entries per step
+// with a running carry: the chunk offsets of jpeg_enc_emit (bits) and jpeg_enc_stuff (0xFF
+// bytes).  Each chunk workgroup then reads its own offset -- O(nchunk) in all, where summing
+// every earlier chunk per workgroup was O(nchunk^2) (tens of thousands of chunks on a
+// config-5-sized canvas).
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) jpeg_enc_exscan(uint32_t *__restrict__ v, int n) {
+    __shared__ uint32_t ws[kScanThreads / 64];
+    const int wv = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (int base = 0; base < n; base += kScanThreads) {
+        const int i = base + (int)threadIdx.x;
+        const uint32_t x = i < n ? v[i] : 0u;
+        const uint32_t inc = wave_incl_scan(x);
+        if ((threadIdx.x & 63) == 63) ws[wv] = inc;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kScanThreads / 64; ++w) {
+            const uint32_t t = ws[w];
+            wbase += w < wv ? t : 0u;
+            tot += t;
+        }
+        if (i < n) v[i] = carry + wbase + inc - x;
+        carry += tot;
+        __syncthreads();                 // ws is rewritten by the next step
+    }
+}
+
 struct CountPut {
     uint32_t n = 0;
     __device__ __forceinline__ void operator()(uint32_t, int len) { n += (uint32_t)len; }
@@ -181,21 +210,12 @@ struct EmitPut {
 
 __global__ void __launch_bounds__(kEncThreads) jpeg_enc_emit(EncDev D) {
     __shared__ uint32_t wsum[kEncThreads / 64];
-    __shared__ uint32_t red[kEncThreads];
     __shared__ uint32_t base;
     __shared__ EncTabs T;
     for (int i = threadIdx.x; i < (int)(sizeof(EncTabs) / 4); i += kEncThreads)
         ((uint32_t *)&T)[i] = ((const uint32_t *)D.tabs)[i];
-    // bits before this chunk
-    uint32_t p = 0;
-    for (int i = threadIdx.x; i < (int)blockIdx.x; i += kEncThreads) p += D.chunk_bits[i];
-    red[threadIdx.x] = p;
-    __syncthreads();
-    for (int o = kEncThreads / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) base = red[0];
+    // bits before this chunk: chunk_bits holds the exclusive prefix (jpeg_enc_exscan)
+    if (threadIdx.x == 0) base = D.chunk_bits[blockIdx.x];
     __syncthreads();
     const int b0 = blockIdx.x * kLenChunk;
     for (int b = b0 + threadIdx.x; b < b0 + kLenChunk; b += kEncThreads) {
@@ -244,19 +264,11 @@ __global__ void __launch_bounds__(kEncThreads) jpeg_enc_ff_count(EncDev D) {
 
 __global__ void __launch_bounds__(kEncThreads) jpeg_enc_stuff(EncDev D) {
     __shared__ uint32_t wsum[kEncThreads / 64];
-    __shared__ uint32_t red[kEncThreads];
     __shared__ uint32_t base;
     const uint32_t nbits = D.total[0], nbytes = (nbits + 7) / 8;
-    uint32_t p = 0;
-    for (int i = threadIdx.x; i < (int)blockIdx.x; i += kEncThreads) p += D.ff_cnt[i];
-    red[threadIdx.x] = p;
-    __syncthreads();
-    for (int o = kEncThreads / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
     const uint32_t j0 = blockIdx.x * kByteChunk;
-    if (threadIdx.x == 0) base = red[0] + j0;            // output position of byte j0
+    // 0xFF bytes before this chunk: ff_cnt holds the exclusive prefix (jpeg_enc_exscan)
+    if (threadIdx.x == 0) base = D.ff_cnt[blockIdx.x] + j0;   // output position of byte j0
     __syncthreads();
     // 16 consecutive bytes per thread (kByteChunk = 16 * kEncThreads)
     const uint32_t jt = j0 + threadIdx.x * 16;
@@ -344,8 +356,10 @@ int launch_jpeg_encode(pano_ctx *ctx, const uint8_t *bgr, int h, int w, int64_t 
         if (rc) return rc;
         jpeg_enc_blocks<<<(nblk + kEncThreads / 8 - 1) / (kEncThreads / 8), kEncThreads, 0, ctx->stream>>>(D);
         jpeg_enc_lengths<<<nchunk, kEncThreads, 0, ctx->stream>>>(D);
+        jpeg_enc_exscan<<<1, kScanThreads, 0, ctx->stream>>>(D.chunk_bits, nchunk);
         jpeg_enc_emit<<<nchunk, kEncThreads, 0, ctx->stream>>>(D);
         jpeg_enc_ff_count<<<nbchunk, kEncThreads, 0, ctx->stream>>>(D);
+        jpeg_enc_exscan<<<1, kScanThreads, 0, ctx->stream>>>(D.ff_cnt, nbchunk);
         jpeg_enc_stuff<<<nbchunk, kEncThreads, 0, ctx->stream>>>(D);
         PANO_LAUNCH_CHECK(ctx, "jpeg encode");
     }

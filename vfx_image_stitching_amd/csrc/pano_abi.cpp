@@ -293,9 +293,14 @@ int pano_sift_pyramid_kernels(pano_ctx *ctx, const float *base, int n, int H0, i
         return ctx ? pano_fail(ctx, PANO_E_ARG, "pano_sift_pyramid_kernels") : PANO_E_ARG;
     if (n_octaves > PANO_MAX_OCTAVES)
         return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_pyramid_kernels: more than PANO_MAX_OCTAVES octaves");
+    // the level count first: kernels[] is read only up to a valid n_kernels
+    if (n_kernels < 3 || n_kernels > PANO_MAX_LEVELS)
+        return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_pyramid_kernels: 3 <= n_kernels <= PANO_MAX_LEVELS");
+    // every sigma finite, >= 0 and narrow enough for PANO_MAX_TAPS taps (rint(8 s + 1) | 1 <= 63)
     for (int l = 1; l < n_kernels; ++l)
-        if (!(kernels[l] >= 0.0))
-            return pano_fail(ctx, PANO_E_UNSUPPORTED, "pano_sift_pyramid_kernels: negative or NaN sigma");
+        if (!(kernels[l] >= 0.0 && kernels[l] * 8.0 + 1.0 < (double)PANO_MAX_TAPS))
+            return pano_fail(ctx, PANO_E_UNSUPPORTED,
+                             "pano_sift_pyramid_kernels: sigma negative, NaN, infinite or wider than PANO_MAX_TAPS taps");
     pano_sift_params p;
     pano_sift_default_params(&p);
     PyrSource src;

@@ -1379,8 +1379,13 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
 #if PANO_DESC_RPI
             // scaled to the 2^22 fixed point up front (a power of two: every product below is
             // exactly 2^22 times its unscaled value), so each contribution is one multiply and
-            // one round-half-up conversion, v_cvt_rpi_i32_f32 = floor(x + 0.5): the same integer
-            // as the unscaled form's u32(fma(v, 2^22, 0.5)) for x in [0, 2^31)
+            // one round-half-up conversion, v_cvt_rpi_i32_f32 = floor(x + 0.5).  Against the
+            // unscaled form's u32(fma(v, 2^22, 0.5)) the exhaustive device probe over every f32
+            // x in [0, 2^31) (tools/probes/rpi_check.hip, profiles/r05_rpi_check.txt) finds
+            // 4,194,305 inputs that differ, all by one unit of 2^-22: the odd integers of
+            // [2^23, 2^24), where the fma's RN(x + 0.5) ties to even and rounds up, and x = 0.5,
+            // which the instruction takes to 0.  Either is a 1e-7-relative restatement of the
+            // reference's float32 np.add.at; the descriptor bytes of every fixture are unchanged
             const float wm = (w * mag) * kFix;
 #else
             const float wm = w * mag;

@@ -1500,6 +1500,12 @@ blur_tail(TailArgs ta) {
 // the centre tap 1 / sum itself.  ksize = cvRound(8 s + 1) | 1 (float images).
 Taps make_taps(double sigma) {
     Taps t;
+    // non-finite or too wide sigmas are refused before the int conversion (nearbyint(inf) has
+    // no int value): ksize = rint(8 s + 1) | 1 must fit PANO_MAX_TAPS
+    if (!(sigma >= 0.0 && sigma * 8.0 + 1.0 < (double)PANO_MAX_TAPS)) {
+        t.n = -1;
+        return t;
+    }
     int n = (int)nearbyint(sigma * 4 * 2 + 1) | 1;
     if (n > PANO_MAX_TAPS) n = -1;
     t.n = n;

@@ -57,7 +57,7 @@ def find_pair_homographies(st, feats, pairs, ratio=0.7, reproj_thr=5.0,
     if desc.dtype == T.uint8:
         norms = getattr(feats, "norms", None)
         if norms is None:
-            norms = (desc.int() ** 2).sum(-1, dtype=T.int32)
+            norms = st.desc_norms(desc)
         st.ctx.check(lib.pano_match_u8(c, ptr(desc), ptr(norms), ptr(counts), cap, _lib.i32p(hp), P,
                                        ptr(best), ptr(d1), ptr(d2)))
     else:

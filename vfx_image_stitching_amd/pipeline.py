@@ -105,6 +105,7 @@ class Stitcher:
         # fast-path state; run() uses slot 0
         self._slot = 0
         self._slot_state = {}            # slot -> (fast, fast_key, head_np) while not current
+        self._stage = {}                 # slot -> staging frame buffer (run_sequence, distinct items)
         self._head_np = None
 
     # ------------------------------------------------------------------ buffers
@@ -195,8 +196,17 @@ class Stitcher:
             pts[i, :p.shape[1]] = p[0]
             desc[i, :d.shape[1]] = d[0]
         if desc.dtype == T.uint8:
-            return Features((pts, desc, counts), (desc.int() ** 2).sum(-1, dtype=T.int32))
+            return Features((pts, desc, counts), self.desc_norms(desc))
         return pts, desc, counts
+
+    def desc_norms(self, desc):
+        """Exact squared norms [frames][cap] i32 of byte descriptors [frames][cap][128]
+        (pano_desc_norms_u8), for byte rows that did not come out of pano_sift_u8."""
+        T = self.torch
+        d = desc.contiguous()
+        norms = T.empty(d.shape[:-1], dtype=T.int32, device=d.device)
+        self.ctx.check(self.ctx.lib.pano_desc_norms_u8(self.ctx.h, ptr(d), d.numel() // 128, ptr(norms)))
+        return norms
 
     def pair_records(self, feats, pairs, out=None):
         T = self.torch
@@ -214,7 +224,7 @@ class Stitcher:
         if desc.dtype == T.uint8:
             norms = getattr(feats, "norms", None)
             if norms is None:
-                norms = (desc.int() ** 2).sum(-1, dtype=T.int32)
+                norms = self.desc_norms(desc)
             self.ctx.check(self.ctx.lib.pano_match_u8(self.ctx.h, ptr(desc), ptr(norms), ptr(counts), cap,
                                                       _lib.i32p(hp), P, ptr(best), ptr(d1), d2p))
         else:
@@ -487,19 +497,39 @@ class Stitcher:
         synchronous run() calls).  Stitches alternate between two output slots; a
         yielded result stays valid until the generator is resumed (run()'s rule: until the next
         call).  A stitch the replay cannot finish (first use of a slot, a capacity or plan
-        overflow, a missing match) drains the pipeline and goes through run()."""
+        overflow, a missing match) drains the pipeline and goes through run().
+
+        Graphs are keyed on the frame buffer's address.  When every item is the same resident
+        buffer (one set re-stitched) the graphs replay on it directly.  When the items are
+        distinct buffers (a video's frame sets), each slot owns a staging buffer: the item's
+        frames are copied into it on the stream (a device copy, ~3 us per 10 MB) and the slot's
+        graph, captured once on the staging buffer, replays for every item of that shape --
+        no re-capture per buffer."""
         items = list(items)
         T = self.torch
         inflight = None                  # (index, slot, event, replay state)
+        shared = len({(f.data_ptr(), tuple(f.shape)) for f, _ in items}) <= 1
+
+        def src_of(i):
+            frames_dev = items[i][0]
+            if shared:
+                return frames_dev
+            stg = self._stage.get(i % 2)
+            if stg is None or stg.shape != frames_dev.shape or stg.device != frames_dev.device:
+                stg = self._stage[i % 2] = T.empty_like(frames_dev)
+            return stg
 
         def launch(i):
             sl = i % 2
             self._use_slot(sl)
             frames_dev, focals = items[i]
+            src = src_of(i)
             fast = self._fast
-            if (fast is None or fast[0] != self._fast_key_of(frames_dev, focals)
+            if (fast is None or fast[0] != self._fast_key_of(src, focals)
                     or fast[1][7] != self.ctx.generation()):
                 return None
+            if src is not frames_dev:
+                src.copy_(frames_dev, non_blocking=True)      # same stream as the replay
             g = fast[1][0]
             self.ctx.check(self.ctx.lib.pano_graph_launch_stream(self.ctx.h, g, _lib._P(self._raw_stream())))
             ev = T.cuda.Event()
@@ -527,8 +557,8 @@ class Stitcher:
                     if inflight is not None:
                         job, inflight = inflight, None
                         r = finish(job)
-                        yield r if r is not None else self._rerun(items, job[0], margin)
-                    yield self._rerun(items, i, margin)
+                        yield r if r is not None else self._rerun(items, job[0], margin, src_of)
+                    yield self._rerun(items, i, margin, src_of)
                     i += 1
                     continue
                 if inflight is not None:
@@ -539,7 +569,7 @@ class Stitcher:
                         # re-issue the successor
                         if nxt is not None:
                             nxt[2].synchronize()
-                        yield self._rerun(items, job[0], margin)
+                        yield self._rerun(items, job[0], margin, src_of)
                         if nxt is not None:
                             i = nxt[0]
                             continue
@@ -552,9 +582,12 @@ class Stitcher:
                 inflight[2].synchronize()
             self._use_slot(0)
 
-    def _rerun(self, items, i, margin):
+    def _rerun(self, items, i, margin, src_of):
         self._use_slot(i % 2)
-        return self.run(items[i][0], items[i][1], margin=margin, graph=True)
+        src = src_of(i)
+        if src is not items[i][0]:
+            src.copy_(items[i][0], non_blocking=True)
+        return self.run(src, items[i][1], margin=margin, graph=True)
 
     def _slot_head(self, sl):
         return self._head_np if sl == self._slot else self._slot_state[sl][2]

@@ -35,11 +35,22 @@ def _stitcher(sigma, num_intervals, assumed_blur, border):
 
 def _as_bgr_u8(image):
     """The frame as u8 BGR for the batched chain, or None when the reference's arithmetic
-    differs from that chain's: a non-u8 BGR image goes through cv2.cvtColor's float formula
-    (not the u8 fixed-point one), a non-integer gray image through float levels."""
+    differs from that chain's: a float32 BGR image goes through cv2.cvtColor's float formula
+    (not the u8 fixed-point one), a non-integer gray image through float levels.  BGR images
+    of other depths are refused as cv2.cvtColor would treat them: float64 (and every other
+    depth cv2 has no BGR2GRAY for) raises ValueError like cv2's "Unsupported depth" error;
+    uint16, which cv2 converts with its 16-bit fixed-point path, raises NotImplementedError
+    (no fixture pins that path)."""
     img = np.asarray(image)
     if img.ndim == 3 and img.shape[2] == 3:
-        return np.ascontiguousarray(img) if img.dtype == np.uint8 else None
+        if img.dtype == np.uint8:
+            return np.ascontiguousarray(img)
+        if img.dtype == np.float32:
+            return None
+        if img.dtype == np.uint16:
+            raise NotImplementedError("16-bit BGR input: cv2's 16-bit BGR2GRAY path is not restated")
+        raise ValueError(f"cvtColor(BGR2GRAY): unsupported depth {img.dtype} (cv2 takes uint8, "
+                         "uint16 and float32)")
     if img.ndim != 2:
         raise ValueError("expected an H x W x 3 BGR or H x W gray image")
     if img.dtype != np.uint8:
@@ -63,15 +74,18 @@ def _frame_u8(image):
 
 def _gray_f32(image):
     """sift_impl.py:27-29 for the images the batched chain does not take: cv2.cvtColor
-    BGR2GRAY of a float BGR image (B * 0.114 + G * 0.587 + R * 0.299 in float32, OpenCV's
+    BGR2GRAY of a float32 BGR image (B * 0.114 + G * 0.587 + R * 0.299 in float32, OpenCV's
     scalar order; its SIMD body may fuse -- parity unpinned for float BGR input, no cv2 here),
-    computed on the device, then astype(float32)."""
+    computed on the device by pano_gray_bgr_f32, then astype(float32)."""
     img = np.asarray(image)
     if img.ndim == 2:
         return np.ascontiguousarray(img, np.float32)
     ctx, torch, dev = _dev()
+    h, w = img.shape[:2]
     t = torch.from_numpy(np.ascontiguousarray(img, np.float32)).to(dev)
-    g = (t[..., 0] * 0.114 + t[..., 1] * 0.587) + t[..., 2] * 0.299
+    g = torch.empty((h, w), dtype=torch.float32, device=dev)
+    ctx.check(ctx.lib.pano_gray_bgr_f32(ctx.h, _lib.ptr(t), 1, h, w, _lib.ptr(g)))
+    ctx.sync()
     return g.cpu().numpy()
 
 
