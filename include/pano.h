@@ -348,6 +348,13 @@ int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *d_recs, int n, int h, i
 int pano_composite_planned(pano_ctx *ctx, const uint8_t *d_frames, const uint8_t *d_colnz, int n,
                            int h, int w, const void *d_plan, uint8_t *d_canvas, int Hcap,
                            int Wcap, int black_threshold, int32_t *d_bbox);
+/* pano_plan_device followed by pano_composite_planned in two launches instead of three (the
+ * composite's column tables are built by the plan launch, one workgroup per frame): the same
+ * plan, canvas and crop-box partials, byte for byte. */
+int pano_plan_composite_device(pano_ctx *ctx, const pano_pair_rec *d_recs, const uint8_t *d_frames,
+                               const uint8_t *d_colnz, int n, int h, int w, int int_shifts,
+                               void *d_plan, uint8_t *d_canvas, int Hcap, int Wcap,
+                               int black_threshold, int32_t *d_bbox);
 
 /* One rank's band of a sharded stitch from the GLOBAL plan of pano_plan_device
  * (built from every rank's gathered records): the rank holds frames f0 .. f0 + n_local - 1

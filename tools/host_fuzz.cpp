@@ -9,6 +9,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <vector>
 
@@ -44,7 +45,7 @@ constexpr int kMaxN = 400;
 int main(int argc, char **argv) {
     const long iters = argc > 1 ? atol(argv[1]) : 20000;
     if (argc > 2) g_state = strtoull(argv[2], nullptr, 10);
-    long ok = 0, refused = 0, bad = 0;
+    long ok = 0, refused = 0, bad = 0, fast_diff = 0;
     std::vector<double> shifts, pairs;
     std::vector<pano_step> steps;
     std::vector<int32_t> tmp;
@@ -67,6 +68,23 @@ int main(int argc, char **argv) {
         const int rc = plan_core([&](int k, double *d) { d[0] = shifts[2 * k]; d[1] = shifts[2 * k + 1]; },
                                  [&](int k, double *d) { for (int q = 0; q < 4; ++q) d[q] = pairs[4 * k + q]; },
                                  n, h, w, steps.data(), first, hw, tmp.data());
+        // plan_device's form (per-step constants + the short chain) must be the same plan
+        {
+            std::vector<pano_step> steps2((size_t)n, pano_step{});
+            std::vector<int32_t> tmp2(5 * (size_t)n, 0);
+            int32_t first2[2] = {0, 0}, hw2[2] = {0, 0};
+            const int rc2 = plan_fast([&](int k, double *d) { d[0] = shifts[2 * k]; d[1] = shifts[2 * k + 1]; },
+                                      [&](int k, double *d) { for (int q = 0; q < 4; ++q) d[q] = pairs[4 * k + q]; },
+                                      n, h, w, steps2.data(), first2, hw2, tmp2.data());
+            bool same = rc2 == rc;
+            if (same && rc == PANO_OK)
+                same = memcmp(steps2.data(), steps.data(), sizeof(pano_step) * (size_t)(n - 1 > 0 ? n - 1 : 0)) == 0 &&
+                       first2[0] == first[0] && first2[1] == first[1] && hw2[0] == hw[0] && hw2[1] == hw[1];
+            if (!same) {
+                ++fast_diff;
+                if (fast_diff <= 5) fprintf(stderr, "plan_fast differs: iteration %ld n %d rc %d / %d\n", it, n, rc, rc2);
+            }
+        }
         if (rc != PANO_OK) { ++refused; continue; }
         ++ok;
         // consistency of an accepted plan
@@ -82,6 +100,7 @@ int main(int argc, char **argv) {
             if (++bad <= 5) fprintf(stderr, "inconsistent plan: iteration %ld n %d h %d w %d\n", it, n, h, w);
         }
     }
-    printf("{\"iterations\": %ld, \"ok\": %ld, \"refused\": %ld, \"inconsistent\": %ld}\n", iters, ok, refused, bad);
-    return bad ? 1 : 0;
+    printf("{\"iterations\": %ld, \"ok\": %ld, \"refused\": %ld, \"inconsistent\": %ld, \"plan_fast_differs\": %ld}\n",
+           iters, ok, refused, bad, fast_diff);
+    return (bad || fast_diff) ? 1 : 0;
 }

@@ -136,6 +136,7 @@ SIGNATURES = {
     "pano_plan_device": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "pano_band_plan": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "pano_composite_planned": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
+    "pano_plan_composite_device": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
     "pano_composite_sequential": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P,
                                        _I, _I]),
     "pano_blend_geometry": (_I, [_D, _D, _PD, _I, _I, _I, _I, _PI32, _PD]),

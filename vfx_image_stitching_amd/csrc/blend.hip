@@ -155,12 +155,24 @@ struct SeqArg {
 // Device-planned stitch (pano_plan_device): the plan kernel writes the sequence table and
 // the canvas size to HBM, so the composite launches read them there and the whole stitch is
 // one launch chain (one hipGraph, one device->host read at the end).
+#ifndef PANO_PLAN_CLOCK
+#define PANO_PLAN_CLOCK 0        // 1: s_memtime stamps of plan_device's phases in DevPlan::clk
+#endif
 struct DevPlan {
     int32_t status, H, W, n;            // status: PANO_OK, PANO_E_NOMATCH, or PANO_E_OVERFLOW
     int32_t first_x, first_y, pad0, pad1;   //   (-> the host plan path)
     SeqArg sa;
     pano_step steps[kMaxSeq];
+    long long clk[8];                   // PANO_PLAN_CLOCK timing builds (tools/plan_clock.py); last
 };
+#ifndef PANO_PLAN_FAST
+#define PANO_PLAN_FAST 1         // 0: plan_core over LDS state by one thread (the A/B reference)
+#endif
+#if PANO_PLAN_CLOCK
+#define PLAN_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) dp->clk[k] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PLAN_STAMP(k) do { } while (0)
+#endif
 
 template <bool DEV>
 __global__ void __launch_bounds__(256)
@@ -516,16 +528,26 @@ namespace {
 // arithmetic.  The plan is a sequential scalar chain: the records are staged in LDS and ONE
 // thread runs it over LDS state (a global-memory chain would pay an HBM round trip per
 // dependent access); the parallel-composite check and the write-out use every thread.
+// TABLES (plan_tables): grid = n workgroups; every workgroup replays the (cheap, serial) plan
+// itself, workgroup 0 publishes it (and initialises the crop-box slots), and workgroup i then
+// builds composite_tables' mode / weight row of frame i from its own copy -- the plan and the
+// tables in one launch, no cross-workgroup hand-off.
+template <bool TABLES>
 __global__ void __launch_bounds__(256)
 plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int_shifts, int Hcap,
-            int Wcap, DevPlan *__restrict__ dp) {
+            int Wcap, DevPlan *__restrict__ dp, const uint8_t *__restrict__ colnz = nullptr,
+            uint8_t *__restrict__ mode = nullptr, float2 *__restrict__ wgt = nullptr,
+            int32_t *__restrict__ bbox = nullptr) {
     __shared__ double rv[6][kMaxSeq];           // dx dy xA yA xB yB per pair (converted)
     __shared__ pano_step st[kMaxSeq];
-    __shared__ int32_t tmp[5 * kMaxSeq];
+    __shared__ int32_t tmp[8 * kMaxSeq];           // plan scratch (plan_core: 5 n; the fast path: 8 rows)
     __shared__ int32_t fx[kMaxSeq];
     __shared__ int32_t hdr[6];                  // status H W first_x first_y, bands flag
     __shared__ int bad;
     const int tid = threadIdx.x, P = n - 1;
+    const bool lead = blockIdx.x == 0;          // the workgroup that publishes the plan
+    PLAN_STAMP(0);
+    if (TABLES && lead && bbox && tid < PANO_BBOX_SLOTS) box_init_slot(bbox + 4 * tid);
     auto conv = [&](double v) { return int_shifts ? (double)(long long)v : v; };   // int() truncates
     if (tid == 0) bad = 0;
     __syncthreads();
@@ -536,6 +558,115 @@ plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int
         rv[2][k] = conv(r.xA); rv[3][k] = conv(r.yA); rv[4][k] = conv(r.xB); rv[5][k] = conv(r.yB);
     }
     __syncthreads();
+    PLAN_STAMP(1);
+#if PANO_PLAN_FAST
+    // Wave 0: the per-step constants (plan_step_const) one step per lane; the serial part --
+    // the drift sum in pair order and the mosaic-size chain (plan_chain_hw) -- with each
+    // step's constants broadcast by readlane; then every lane finishes its own step
+    // (plan_chain_step from the sizes the chain handed it) and the origins are suffix sums
+    // across the lanes.  Same numbers as plan_core (plan_fast, tools/host_fuzz.cpp).  Per step
+    // the chain costs ~490 cycles (PANO_PLAN_CLOCK): plan_core over LDS state by one thread
+    // ~1,200; the same chain on LDS broadcast reads ~650.
+    if (tid < 64) {
+        const int lane = tid;
+        auto rl = [](int v, int j) { return __builtin_amdgcn_readlane(v, j); };
+        auto rld = [](double v, int j) {
+            const long long b = __double_as_longlong(v);
+            const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
+            const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+            return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+        };
+        int rc = bad ? PANO_E_NOMATCH : PANO_OK;
+        int Hm = h, Wm = w, oy = 0, ox = 0;
+        if (rc == PANO_OK) {
+            // drift correction: the sum in pair order, as Python's
+            double tot = 0.0;
+            long long itot = 0;
+            for (int k = 0; k < P; ++k) {
+                if (int_shifts) itot += (long long)rv[1][k];
+                else tot = tot + rv[1][k];
+            }
+            const double avg = int_shifts ? (double)itot / (double)P : tot / (double)P;
+            PLAN_STAMP(2);
+            if (h <= 0 || w <= 0 || h > kPlanMaxSide / 2 || w > kPlanMaxSide / 2) rc = PANO_E_ARG;
+            int32_t *yM = tmp, *xM = tmp + kMaxSeq, *yF = tmp + 2 * kMaxSeq, *xF = tmp + 3 * kMaxSeq,
+                    *ptop = tmp + 4 * kMaxSeq;          // by step k = i - 1
+            for (int c0 = 0; c0 < P && rc == PANO_OK; c0 += 64) {
+                const int k = c0 + lane;
+                PlanStepConst c{};
+                if (k < P) {
+                    const double pd[4] = {rv[2][k], rv[3][k], rv[4][k], rv[5][k]};
+                    c = plan_step_const(rv[0][k], rv[1][k] - avg, pd);
+                }
+                // the serial part: only the mosaic size; lane j keeps the size its step starts
+                // from and computes the rest of its step afterwards
+                int Hin = Hm, Win = Wm;
+                const int m = min(64, P - c0);
+                for (int j = 0; j < m; ++j) {
+                    PlanStepConst cj;
+                    cj.bad = rl(c.bad, j);
+                    if (cj.bad) { rc = PANO_E_ARG; break; }
+                    cj.r00 = rld(c.r00, j);
+                    cj.r10 = rld(c.r10, j);
+                    cj.swapped = rl(c.swapped, j);
+                    cj.myA = rl(c.myA, j);
+                    cj.myB = rl(c.myB, j);
+                    cj.mxB = rl(c.mxB, j);
+                    int H1, W1;
+                    plan_chain_hw(cj, Hm, Wm, h, w, H1, W1);
+                    if (H1 > kPlanMaxSide || W1 > kPlanMaxSide) { rc = PANO_E_OVERFLOW; break; }
+                    if (lane == j) { Hin = Hm; Win = Wm; }
+                    Hm = H1;
+                    Wm = W1;
+                }
+                const PlanStepOut mine = plan_chain_step(c, Hin, Win, h, w);
+                if (k < P && rc == PANO_OK) {
+                    pano_step &q = st[k];
+                    q.canvas_h = mine.H;
+                    q.canvas_w = mine.W;
+                    q.frame_is_a = c.swapped;
+                    q.pad = 0;
+                    q.overlap_range = mine.ov;
+                    yM[k] = mine.yM; xM[k] = mine.xM; yF[k] = mine.yF; xF[k] = mine.xF; ptop[k] = mine.ptop;
+                }
+            }
+            PLAN_STAMP(7);
+            if (rc == PANO_OK) {
+                // origins: step k's mosaic sits at the sum of yM / xM over the later steps
+                for (int c0 = (P - 1) / 64 * 64; c0 >= 0; c0 -= 64) {
+                    const int k = c0 + lane;
+                    const int vy = k < P ? yM[k] : 0, vx = k < P ? xM[k] : 0;
+                    int iy = vy, ix = vx;            // inclusive prefix over the lanes
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const int ty = __shfl_up(iy, d), tx = __shfl_up(ix, d);
+                        if (lane >= d) { iy += ty; ix += tx; }
+                    }
+                    const int ty = __shfl(iy, 63), tx = __shfl(ix, 63);
+                    if (k < P) {
+                        pano_step &q = st[k];
+                        q.canvas_y = oy + ty - iy;   // later steps of this chunk + later chunks
+                        q.canvas_x = ox + tx - ix;
+                        q.frame_y = q.canvas_y + yF[k] + ptop[k];
+                        q.frame_x = q.canvas_x + xF[k];
+                    }
+                    oy += ty;
+                    ox += tx;
+                }
+            }
+        }
+        if (lane == 0) {
+            hdr[0] = rc;
+            hdr[1] = rc == PANO_OK ? Hm : 0;
+            hdr[2] = rc == PANO_OK ? Wm : 0;
+            hdr[3] = ox;
+            hdr[4] = oy;
+            if (rc == PANO_OK && !(ox >= 0 && oy >= 0 && ox + w <= Wm && oy + h <= Hm && Hm <= Hcap && Wm <= Wcap))
+                hdr[0] = PANO_E_OVERFLOW;
+        }
+        PLAN_STAMP(3);
+    }
+#else
     if (tid == 0) {
         hdr[0] = PANO_OK;
         if (bad) {
@@ -552,9 +683,11 @@ plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int
                 avg = tot / (double)P;
             }
             int32_t first[2], hw[2];
+            PLAN_STAMP(2);
             const int rc = plan_core([&](int k, double *d) { d[0] = rv[0][k]; d[1] = rv[1][k] - avg; },
                                      [&](int k, double *d) { for (int q = 0; q < 4; ++q) d[q] = rv[2 + q][k]; },
                                      n, h, w, st, first, hw, tmp);
+            PLAN_STAMP(3);
             hdr[0] = rc ? rc : PANO_OK;
             hdr[1] = hw[0];
             hdr[2] = hw[1];
@@ -565,12 +698,54 @@ plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int
                 hdr[0] = PANO_E_OVERFLOW;
         }
     }
+#endif
     __syncthreads();
     const int status = hdr[0];
+    PLAN_STAMP(4);
     if (status == PANO_OK) {
         const int H = hdr[1], W = hdr[2];
         for (int i = tid; i < n; i += blockDim.x) fx[i] = i ? st[i - 1].frame_x : hdr[3];
         __syncthreads();
+        if (TABLES) {
+            // composite_tables' row of frame i = blockIdx.x from this workgroup's plan copy
+            const int i = blockIdx.x;
+            const double ov = i ? st[i - 1].overlap_range : 0.0;
+            int carry = 0;
+            int *sh = tmp;                       // the plan's scratch, free now
+            for (int base = 0; base < w; base += 256) {
+                const int c = base + tid;
+                int fF = 0, fM = 0;
+                if (c < w) {
+                    fF = colnz[(size_t)i * w + c] != 0;
+                    if (i > 0) {
+                        const int xm = fx[i] + c - fx[i - 1];
+                        fM = (xm >= 0 && xm < w) ? colnz[(size_t)(i - 1) * w + xm] != 0 : 0;
+                    }
+                }
+                const int both = fF && fM;
+                // exclusive rank of `both` (ballot per wave, wave totals through LDS)
+                const unsigned long long m = __ballot(both);
+                const int lane = tid & 63, wv = tid >> 6;
+                if (lane == 0) sh[wv] = __popcll(m);
+                __syncthreads();
+                int wbase = 0, tot = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    wbase += q < wv ? sh[q] : 0;
+                    tot += sh[q];
+                }
+                if (c < w) {
+                    const int rank = carry + wbase + __popcll(m & ((1ull << lane) - 1ull));
+                    mode[(size_t)i * w + c] = (uint8_t)(fF ? (both ? 2 : 1) : 0);
+                    const double alpha = ov != 0.0 ? (double)rank / ov : 0.0;
+                    wgt[(size_t)i * w + c] = make_float2((float)(1.0 - alpha), (float)alpha);
+                }
+                carry += tot;
+                __syncthreads();
+            }
+            PLAN_STAMP(5);
+            if (!lead) return;
+        }
         for (int i = tid; i < n; i += blockDim.x) {
             bool ok = true;
             if (i) {
@@ -578,8 +753,9 @@ plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int
                 ok = q.frame_x >= 0 && q.frame_x + w <= W && q.frame_y >= 0 && q.frame_y + h <= H &&
                      q.canvas_y >= 0 && q.canvas_y + q.canvas_h <= H;
             }
-            for (int j = 0; ok && j <= i - 2; ++j)      // frame i never meets a frame j <= i - 2
-                ok = fx[i] + w <= fx[j] || fx[j] + w <= fx[i];
+            const int xi = fx[i];
+            for (int j = 0; j <= i - 2; ++j)            // frame i never meets a frame j <= i - 2
+                ok &= xi + w <= fx[j] || fx[j] + w <= xi;
             if (!ok) atomicOr(&bad, 2);
             dp->sa.fx[i] = fx[i];
             dp->sa.fy[i] = i ? st[i - 1].frame_y : hdr[4];
@@ -589,6 +765,8 @@ plan_device(const pano_pair_rec *__restrict__ recs, int n, int h, int w, int int
         }
         __syncthreads();
     }
+    if (TABLES && !lead) return;
+    PLAN_STAMP(6);
     if (tid == 0) {
         dp->status = (status == PANO_OK && (bad & 2)) ? PANO_E_OVERFLOW : status;
         dp->n = n;
@@ -690,7 +868,7 @@ int launch_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, i
         return pano_fail(ctx, PANO_E_ARG, "pano_plan_device: bad arguments");
     {
         PanoProf prof_(ctx, PK_COMPOSITE);
-        plan_device<<<1, 256, 0, ctx->stream>>>(recs, n, h, w, int_shifts, Hcap, Wcap, (DevPlan *)plan);
+        plan_device<false><<<1, 256, 0, ctx->stream>>>(recs, n, h, w, int_shifts, Hcap, Wcap, (DevPlan *)plan);
     }
     PANO_LAUNCH_CHECK(ctx, "plan_device");
     return PANO_OK;
@@ -716,6 +894,37 @@ int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t
     }
     PANO_LAUNCH_CHECK(ctx, "composite_tables");
     (void)info;                                  // the owner records: computed per column in composite_pixels
+    {
+        dim3 grid((Wcap + 63) / 64, (Hcap + 4 * kCompRows - 1) / (4 * kCompRows));
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        composite_pixels<true><<<grid, 256, 0, ctx->stream>>>(frames, h, w, nullptr, canvas, Hcap, Wcap, thr,
+                                                              bbox, dp, mode, wgt);
+    }
+    PANO_LAUNCH_CHECK(ctx, "composite_pixels");
+    return PANO_OK;
+}
+
+// pano_plan_device + pano_composite_planned as two launches: plan_device<true> (the plan in
+// every workgroup, the composite tables of frame i in workgroup i, the crop-box slots) and
+// composite_pixels.  Same bytes as the three-launch form (the tables are the same arithmetic).
+int launch_plan_composite_device(pano_ctx *ctx, const pano_pair_rec *recs, const uint8_t *frames,
+                                 const uint8_t *colnz, int n, int h, int w, int int_shifts, void *plan,
+                                 uint8_t *canvas, int Hcap, int Wcap, int thr, int32_t *bbox) {
+    if (n < 2 || n > kMaxSeq || h <= 0 || w <= 0 || !recs || !plan || !frames || !colnz || !canvas)
+        return pano_fail(ctx, PANO_E_ARG, "pano_plan_composite_device: bad arguments");
+    const DevPlan *dp = (const DevPlan *)plan;
+    const size_t o_w = ((size_t)n * w + 255) & ~size_t(255);
+    const size_t o_own = o_w + (((size_t)n * w * sizeof(float2) + 255) & ~size_t(255));
+    int rc = pano_grow(ctx, (void **)&ctx->flags, &ctx->flags_bytes, o_own + (size_t)Wcap * sizeof(ColInfo));
+    if (rc) return rc;
+    uint8_t *mode = ctx->flags;
+    float2 *wgt = (float2 *)(ctx->flags + o_w);
+    {
+        PanoProf prof_(ctx, PK_COMPOSITE);
+        plan_device<true><<<n, 256, 0, ctx->stream>>>(recs, n, h, w, int_shifts, Hcap, Wcap, (DevPlan *)plan,
+                                                      colnz, mode, wgt, bbox);
+    }
+    PANO_LAUNCH_CHECK(ctx, "plan_device");
     {
         dim3 grid((Wcap + 63) / 64, (Hcap + 4 * kCompRows - 1) / (4 * kCompRows));
         PanoProf prof_(ctx, PK_COMPOSITE);

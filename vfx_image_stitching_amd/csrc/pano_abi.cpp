@@ -488,6 +488,14 @@ int pano_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *
                                     black_threshold, bbox);
 }
 
+int pano_plan_composite_device(pano_ctx *ctx, const pano_pair_rec *recs, const uint8_t *frames,
+                               const uint8_t *colnz, int n, int h, int w, int int_shifts, void *plan,
+                               uint8_t *canvas, int Hcap, int Wcap, int black_threshold, int32_t *bbox) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_plan_composite_device(ctx, recs, frames, colnz, n, h, w, int_shifts, plan, canvas, Hcap,
+                                        Wcap, black_threshold, bbox);
+}
+
 int pano_composite_sequential(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
                               int h, int w, const pano_step *steps, const int32_t *first_xy,
                               uint8_t *canvas, int H, int W) {

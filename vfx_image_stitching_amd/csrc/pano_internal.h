@@ -271,6 +271,9 @@ int launch_band_plan(pano_ctx *ctx, const void *plan, int f0, int n_local, int w
 int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,
                              int w, const void *plan, uint8_t *canvas, int Hcap, int Wcap, int thr,
                              int32_t *bbox);
+int launch_plan_composite_device(pano_ctx *ctx, const pano_pair_rec *recs, const uint8_t *frames,
+                                 const uint8_t *colnz, int n, int h, int w, int int_shifts, void *plan,
+                                 uint8_t *canvas, int Hcap, int Wcap, int thr, int32_t *bbox);
 int launch_composite_bbox(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n,
                           int h, int w, const pano_step *steps, const int32_t *first_xy,
                           uint8_t *canvas, int H, int W, int thr, int32_t *bbox);

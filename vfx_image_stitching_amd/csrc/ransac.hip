@@ -34,6 +34,27 @@ __device__ int block_excl_scan(int v, int *sh, int &total) {
     return r;
 }
 
+// Exclusive scan of one flag per thread over the RB-thread block: a wave ballot gives the
+// in-wave prefix (popcount of the lanes below), one barrier publishes the wave totals.  The
+// Hillis-Steele scan above takes 2 log2(RB) = 20 barriers per RB rows: pair_compact 10.4 us.
+__device__ __forceinline__ int block_flag_scan(bool flag, int *wsum, int &total) {
+    const unsigned long long m = __ballot(flag);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < RB / 64; ++w) {
+        const int t = wsum[w];
+        base += w < wv ? t : 0;
+        tot += t;
+    }
+    total = tot;
+    __syncthreads();                     // wsum is rewritten by the next call
+    return base + below;
+}
+
 // votes for every move of `mv[0..k)`, then first-max; results in *best_m, *best_v
 __device__ void vote_argmax(const double2 *mv, int k, double thr, double2 *tile, int *ish,
                             int *best_m, int *best_v) {
@@ -92,7 +113,7 @@ pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
              const float *__restrict__ d2, float desc_thresh, double ratio,
              double2 *__restrict__ moves, int32_t *__restrict__ midx, int32_t *__restrict__ kcount,
              int32_t *__restrict__ votes) {
-    __shared__ int ish[2 * RB];
+    __shared__ int wsum[RB / 64];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int fa = pairs.a[p], fb = pairs.b[p];
     const int NA = min(max(counts[fa], 0), cap);
@@ -111,7 +132,7 @@ pair_compact(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
             // distance (correctly rounded), compared in Python doubles
             acc = ratio > 0.0 ? ((double)sqrtf(p1[i]) < ratio * (double)sqrtf(p2[i])) : 1;
         int tot;
-        const int pos = block_excl_scan(acc, ish, tot);
+        const int pos = block_flag_scan(acc != 0, wsum, tot);
         if (acc) {
             const int j = bp[i];
             double xa, ya, xb, yb;

@@ -415,11 +415,11 @@ class Stitcher:
             cyl, colnz = self.cylindrical(frames_dev, focals)
             feats = self.features(cyl)
             recs_dev, _ = self.pair_records(feats, [(i, i + 1) for i in range(P)], out=res[:off_bb])
-            self.ctx.check(lib.pano_plan_device(c, ptr(recs_dev), n, h, w, int(self.method != "sift"),
-                                                Hcap, Wcap, ptr(res[off_plan:])))
-            self.ctx.check(lib.pano_composite_planned(c, ptr(cyl), ptr(colnz), n, h, w,
-                                                      ptr(res[off_plan:]), ptr(canvas), Hcap, Wcap, 0,
-                                                      ptr(res[off_bb:off_plan])))
+            # the plan (drift + geometry) and the composite tables in one launch, then the pixels
+            self.ctx.check(lib.pano_plan_composite_device(c, ptr(recs_dev), ptr(cyl), ptr(colnz), n, h, w,
+                                                          int(self.method != "sift"), ptr(res[off_plan:]),
+                                                          ptr(canvas), Hcap, Wcap, 0,
+                                                          ptr(res[off_bb:off_plan])))
             # the records, crop box and plan header to pinned host memory: the one host read
             self.ctx.check(lib.pano_copy_async(c, _lib._P(pin.data_ptr()), ptr(res), nhead))
             return cyl, colnz
