@@ -367,6 +367,13 @@ int pano_plan_composite_device(pano_ctx *ctx, const pano_pair_rec *d_recs, const
  * graph-capturable. */
 int pano_band_plan(pano_ctx *ctx, const void *d_plan, int f0, int n_local, int w, int Wcap,
                    void *d_local_plan, int32_t *d_band);
+/* The rank's row of the N > 1 layout exchange (distributed.py), on the device: from the global
+ * plan, pano_band_plan's d_band and the band's PANO_BBOX_SLOTS crop-box partials, d_row[8]
+ * int64 = {ymin, ymax, xmin, xmax} in global columns ({2^30, -1, 2^30, -1} when no pixel
+ * passed or the band was refused), own_lo, own_hi, fallback (1: the global or the band plan
+ * refused), the global plan's status.  Device-only, graph-capturable. */
+int pano_band_layout_row(pano_ctx *ctx, const void *d_plan, const int32_t *d_band,
+                         const int32_t *d_bbox, int64_t *d_row);
 
 /* blend_two_images(shift_vec, ref_match, imgA, imgB) for arbitrary inputs
  * image_stitching_sift.py:156-202.  Geometry comes from pano_blend_geometry. */

@@ -135,6 +135,7 @@ SIGNATURES = {
     "pano_plan_device_bytes": (ctypes.c_size_t, []),
     "pano_plan_device": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "pano_band_plan": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "pano_band_layout_row": (_I, [_P, _P, _P, _P, _P]),
     "pano_composite_planned": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
     "pano_plan_composite_device": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
     "pano_composite_sequential": (_I, [_P, _P, _P, _I, _I, _I, ctypes.POINTER(Step), _PI32, _P,

@@ -845,7 +845,44 @@ __global__ void band_plan(const DevPlan *__restrict__ g, int f0, int n_local, in
     }
 }
 
+// The rank's row of the N > 1 layout exchange, on the device (so the all_gather of the rows
+// needs no host round trip): {ymin, ymax, xmin, xmax} of the band's crop-box partials in
+// GLOBAL columns (NO_BOX when no pixel passed), own_lo, own_hi, fallback (the global plan or
+// the band plan refused), the global plan's status.
+__global__ void band_layout_row(const DevPlan *__restrict__ g, const int32_t *__restrict__ band,
+                                const int32_t *__restrict__ slots, long long *__restrict__ row) {
+    const int t = threadIdx.x;                   // one wave
+    int a = 0x7fffffff, b = -1, c = 0x7fffffff, d = -1;
+    if (t < PANO_BBOX_SLOTS) { a = slots[4 * t]; b = slots[4 * t + 1]; c = slots[4 * t + 2]; d = slots[4 * t + 3]; }
+    for (int o = 32; o > 0; o >>= 1) {
+        a = min(a, __shfl_xor(a, o)); b = max(b, __shfl_xor(b, o));
+        c = min(c, __shfl_xor(c, o)); d = max(d, __shfl_xor(d, o));
+    }
+    if (t == 0) {
+        const int gst = g->status, bst = band[0];
+        const bool ok = gst == PANO_OK && bst == PANO_OK;
+        const long long lo = ok ? band[1] : 0, hi = ok ? band[2] : 0;
+        const bool box = ok && b >= 0;
+        row[0] = box ? a : (1ll << 30);
+        row[1] = box ? b : -1;
+        row[2] = box ? c + lo : (1ll << 30);
+        row[3] = box ? d + lo : -1;
+        row[4] = lo;
+        row[5] = hi;
+        row[6] = ok ? 0 : 1;
+        row[7] = gst;
+    }
+}
+
 }  // namespace
+
+int launch_band_layout_row(pano_ctx *ctx, const void *plan, const int32_t *band, const int32_t *slots,
+                           long long *row) {
+    if (!plan || !band || !slots || !row) return pano_fail(ctx, PANO_E_ARG, "pano_band_layout_row: bad arguments");
+    band_layout_row<<<1, 64, 0, ctx->stream>>>((const DevPlan *)plan, band, slots, row);
+    PANO_LAUNCH_CHECK(ctx, "band_layout_row");
+    return PANO_OK;
+}
 
 int launch_band_plan(pano_ctx *ctx, const void *plan, int f0, int n_local, int w, int Wcap,
                      void *local_plan, int32_t *band) {

@@ -474,6 +474,12 @@ int pano_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, int
     return launch_plan_device(ctx, recs, n, h, w, int_shifts, Hcap, Wcap, plan);
 }
 
+int pano_band_layout_row(pano_ctx *ctx, const void *plan, const int32_t *band, const int32_t *bbox,
+                         int64_t *row) {
+    if (!ctx) return PANO_E_ARG;
+    return launch_band_layout_row(ctx, plan, band, bbox, (long long *)row);
+}
+
 int pano_band_plan(pano_ctx *ctx, const void *plan, int f0, int n_local, int w, int Wcap,
                    void *local_plan, int32_t *band) {
     if (!ctx) return PANO_E_ARG;

@@ -266,6 +266,8 @@ int launch_composite(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz,
 size_t plan_device_bytes();
 int launch_plan_device(pano_ctx *ctx, const pano_pair_rec *recs, int n, int h, int w, int int_shifts,
                        int Hcap, int Wcap, void *plan);
+int launch_band_layout_row(pano_ctx *ctx, const void *plan, const int32_t *band, const int32_t *slots,
+                           long long *row);
 int launch_band_plan(pano_ctx *ctx, const void *plan, int f0, int n_local, int w, int Wcap,
                      void *local_plan, int32_t *band);
 int launch_composite_planned(pano_ctx *ctx, const uint8_t *frames, const uint8_t *colnz, int n, int h,

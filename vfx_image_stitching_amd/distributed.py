@@ -256,6 +256,45 @@ def rank_records(stitcher, frames_dev, focals, pmax, graph=False):
     return block, cyl, colnz
 
 
+def _staged(t, group):
+    """gloo moves host memory only: a device tensor in a gloo group (the multi-process tests on
+    one GPU) is exchanged through a host copy.  RCCL ("nccl") moves device memory directly."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_gather_dev(out, inp, group=None):
+    """all_gather_into_tensor(out, inp): device to device over RCCL; staged through host
+    memory for a gloo group on device tensors."""
+    import torch.distributed as dist
+    if _staged(inp, group):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+        return out
+    dist.all_gather_into_tensor(out, inp, group=group)
+    return out
+
+
+def _p2p(ops_spec, group=None):
+    """batch_isend_irecv of (op, tensor, peer) triples; gloo on device tensors goes through
+    host copies (receives copied back after the wait)."""
+    import torch.distributed as dist
+    ops, back = [], []
+    for op, t, peer in ops_spec:
+        if _staged(t, group):
+            h = t.cpu() if op is dist.isend else t.new_empty(t.shape, device="cpu")
+            if op is dist.irecv:
+                back.append((t, h))
+            t = h
+        ops.append(dist.P2POp(op, t, peer, group))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    for t, h in back:
+        t.copy_(h)
+
+
 def gather_blocks(block, group=None):
     """THE collective of a sharded stitch: all_gather_into_tensor of every rank's [pmax, 64]
     record block, device to device (RCCL over xGMI for backend "nccl"; gloo on CPU tensors)."""
@@ -265,8 +304,7 @@ def gather_blocks(block, group=None):
     if world == 1:
         return block
     out = torch.empty((world * block.shape[0], 64), dtype=torch.uint8, device=block.device)
-    dist.all_gather_into_tensor(out, block, group=group)
-    return out
+    return all_gather_dev(out, block, group)
 
 
 def block_layout(pair_counts):
@@ -293,6 +331,16 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
     Returns (records PAIR_NP, band view [H, own_hi - own_lo, 3] on device, own_lo, (H, W),
     local crop box (ymin, ymax, xmin, xmax) in global columns or NO_BOX)."""
     import torch
+    S = rank_band_launch(stitcher, cyl, colnz, gathered, pair_counts, f0, graph)
+    torch.cuda.current_stream(stitcher.device).synchronize()      # the one host read
+    return rank_band_finish(S, S["pin"].numpy()[:S["nhead"]])
+
+
+def rank_band_launch(stitcher, cyl, colnz, gathered, pair_counts, f0, graph=False):
+    """rank_band's launches, nothing read back: the global plan, this rank's band plan and
+    composite, the band's layout row (pano_band_layout_row, 8 int64 at S["row"]) and the
+    pinned copy of the head.  Returns the state rank_band_finish parses."""
+    import torch
     from .pipeline import BBOX_SLOTS
     st = stitcher
     lib, c = st.ctx.lib, st.ctx.h
@@ -302,15 +350,18 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
     plan_bytes = int(lib.pano_plan_device_bytes())
     off_bb = P * 64
     off_band = off_bb + 16 * BBOX_SLOTS
-    off_gp = (off_band + 16 + 255) // 256 * 256
+    off_row = off_band + 16                      # the layout row: 8 int64 (8-byte aligned)
+    off_gp = (off_row + 64 + 255) // 256 * 256
     off_lp = off_gp + (plan_bytes + 255) // 256 * 256
     res = st._get("band_result", (off_lp + plan_bytes,), torch.uint8)
     Hcap, Wcap = st.canvas_cap or (2 * h, (n_local + 2) * w)
     canvas = st._get("band_canvas", (Hcap * Wcap * 3,), torch.uint8)
     nhead = off_gp + 32
+    world = len(pair_counts)
+    npin = nhead + 64 * world                    # + the gathered layout table (run_rank)
     pin = st._buf.get("band_pin")
-    if pin is None or pin.numel() < nhead:
-        pin = torch.empty(max(nhead, 4096), dtype=torch.uint8, pin_memory=True)
+    if pin is None or pin.numel() < npin:
+        pin = torch.empty(max(npin, 4096), dtype=torch.uint8, pin_memory=True)
         st._buf["band_pin"] = pin
 
     def seg():
@@ -326,6 +377,8 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
         st.ctx.check(lib.pano_composite_planned(c, _lib.ptr(cyl), _lib.ptr(colnz), n_local, h, w,
                                                 _lib.ptr(res[off_lp:]), _lib.ptr(canvas), Hcap, Wcap, 0,
                                                 _lib.ptr(res[off_bb:off_band])))
+        st.ctx.check(lib.pano_band_layout_row(c, _lib.ptr(res[off_gp:off_lp]), _lib.ptr(res[off_band:off_row]),
+                                              _lib.ptr(res[off_bb:off_band]), _lib.ptr(res[off_row:off_row + 64])))
         st.ctx.check(lib.pano_copy_async(c, _lib._P(pin.data_ptr()), _lib.ptr(res), nhead))
 
     if graph:
@@ -334,8 +387,17 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
         st._replay(key, seg)
     else:
         seg()
-    torch.cuda.current_stream(st.device).synchronize()           # the one host read
-    head = pin.numpy()[:nhead]
+    return {"st": st, "pin": pin, "nhead": nhead, "off_bb": off_bb, "off_band": off_band,
+            "off_gp": off_gp, "row": res[off_row:off_row + 64].view(torch.int64).view(1, LAYOUT_INTS),
+            "canvas": canvas, "f0": f0, "n_local": n_local, "Hcap": Hcap, "Wcap": Wcap}
+
+
+def rank_band_finish(S, head):
+    """rank_band's result from the pinned head (records, crop-box partials, band info, the
+    global plan header); raises BandError when the plan or the band plan refused."""
+    from .pipeline import BBOX_SLOTS
+    st, off_bb, off_band, off_gp = S["st"], S["off_bb"], S["off_band"], S["off_gp"]
+    f0, n_local, Hcap, Wcap, canvas = S["f0"], S["n_local"], S["Hcap"], S["Wcap"], S["canvas"]
     recs = head[:off_bb].view(_lib.PAIR_NP).reshape(-1).copy()
     st._check_records(recs)
     band = head[off_band:off_band + 16].view(np.int32)
@@ -359,7 +421,7 @@ def rank_band(stitcher, cyl, colnz, gathered, pair_counts, f0, margin=15, graph=
     return recs, view, own_lo, (H, W), box
 
 
-LAYOUT_INTS = 8                # per rank: ymin ymax xmin xmax own_lo own_hi fallback 0
+LAYOUT_INTS = 8                # per rank: ymin ymax xmin xmax own_lo own_hi fallback plan-status
 
 
 def _root(group):
@@ -401,8 +463,7 @@ def assemble_bands(owned, layout, canvas_hw, group=None, out=None):
     root = _root(group) if world > 1 else 0
     if rank != 0:
         if owned.numel():
-            for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, owned.contiguous(), root, group)]):
-                q.wait()
+            _p2p([(dist.isend, owned.contiguous(), root)], group)
         return None
     canvas = out if out is not None else torch.empty((H, W, 3), dtype=torch.uint8, device=owned.device)
     lo0, hi0 = int(layout[0, 4]), int(layout[0, 5])
@@ -414,11 +475,9 @@ def assemble_bands(owned, layout, canvas_hw, group=None, out=None):
             continue
         t = torch.empty((H, hi - lo, 3), dtype=torch.uint8, device=owned.device)
         src = dist.get_global_rank(group, r) if group is not None else r
-        ops.append(dist.P2POp(dist.irecv, t, src, group))
+        ops.append((dist.irecv, t, src))
         tmps.append((lo, hi, t))
-    if ops:
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
+    _p2p(ops, group)
     for lo, hi, t in tmps:
         canvas[:, lo:hi].copy_(t)
     return canvas
@@ -444,10 +503,8 @@ def fold_on_root(stitcher, cyl, colnz, recs, pair_counts, margin=15, group=None)
     rank = dist.get_rank(group)
     if rank != 0:
         if cyl.shape[0] > 1:
-            ops = [dist.P2POp(dist.isend, cyl[1:].contiguous(), _root(group), group),
-                   dist.P2POp(dist.isend, colnz[1:].contiguous(), _root(group), group)]
-            for q in dist.batch_isend_irecv(ops):
-                q.wait()
+            _p2p([(dist.isend, cyl[1:].contiguous(), _root(group)),
+                  (dist.isend, colnz[1:].contiguous(), _root(group))], group)
         return None
     parts_c, parts_z, ops = [cyl], [colnz], []
     for r in range(1, world):
@@ -457,12 +514,10 @@ def fold_on_root(stitcher, cyl, colnz, recs, pair_counts, margin=15, group=None)
         tc = torch.empty((c,) + tuple(cyl.shape[1:]), dtype=cyl.dtype, device=cyl.device)
         tz = torch.empty((c,) + tuple(colnz.shape[1:]), dtype=colnz.dtype, device=colnz.device)
         src = dist.get_global_rank(group, r) if group is not None else r
-        ops += [dist.P2POp(dist.irecv, tc, src, group), dist.P2POp(dist.irecv, tz, src, group)]
+        ops += [(dist.irecv, tc, src), (dist.irecv, tz, src)]
         parts_c.append(tc)
         parts_z.append(tz)
-    if ops:
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
+    _p2p(ops, group)
     cyl_all = torch.cat(parts_c).contiguous()
     colnz_all = torch.cat(parts_z).contiguous()
     return st._finish(cyl_all, colnz_all, recs, margin, False, {}, time.perf_counter())
@@ -488,6 +543,8 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
     block, cyl, colnz = rank_records(st, frames_dev, focals, pmax, graph)
     gathered = gather_blocks(block, group)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world > 1:
+        return _run_rank_sharded(st, cyl, colnz, gathered, pair_start, pair_counts, group, margin, graph)
     try:
         recs, owned, own_lo, (H, W), box = rank_band(st, cyl, colnz, gathered, pair_counts,
                                                      pair_start, margin, graph)
@@ -526,3 +583,47 @@ def run_rank(stitcher, frames_dev, focals, pair_start, pair_counts, group=None, 
         pano = canvas if (y0 > y1 or x0 > x1) else canvas[y0:y1 + 1, x0:x1 + 1]
     return {"records": recs, "band": owned, "x_offset": own_lo, "canvas_hw": (H, W),
             "bbox": (y0, y1, x0, x1), "panorama": pano, "canvas": canvas}
+
+
+def _run_rank_sharded(st, cyl, colnz, gathered, pair_start, pair_counts, group, margin, graph):
+    """run_rank at world > 1 with ONE host read per rank: the band segment is launched, its
+    layout row (pano_band_layout_row: crop box, owned columns, refusal, plan status) goes
+    through an all_gather on the device, and a single pinned read brings back the head
+    (records, band, plan header) together with every rank's layout row.  Then the owned bands
+    go to rank 0 (P2P), which places and crops them; a refused band anywhere sends every rank
+    to the fold on rank 0 instead."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    S = rank_band_launch(st, cyl, colnz, gathered, pair_counts, pair_start, graph)
+    lay = torch.empty((world, LAYOUT_INTS), dtype=torch.int64, device=cyl.device)
+    all_gather_dev(lay, S["row"], group)
+    pin, nhead = S["pin"], S["nhead"]
+    st.ctx.check(st.ctx.lib.pano_copy_async(st.ctx.h, _lib._P(pin.data_ptr() + nhead), _lib.ptr(lay),
+                                            64 * world))
+    torch.cuda.current_stream(st.device).synchronize()            # the one host read
+    raw = pin.numpy()
+    layout = raw[nhead:nhead + 64 * world].view(np.int64).reshape(world, LAYOUT_INTS).copy()
+    if (layout[:, 7] == _lib.PANO_E_NOMATCH).any():
+        raise PanoError(_lib.PANO_E_NOMATCH, "a pair has no descriptor match")
+    if layout[:, 6].any():
+        # some band was refused: every rank sees it in the gathered layout, all take the fallback
+        recs = raw[:S["off_bb"]].view(_lib.PAIR_NP).reshape(-1).copy()
+        st._check_records(recs)
+        res = fold_on_root(st, cyl, colnz, recs, pair_counts, margin, group)
+        if res is None:
+            return {"records": recs, "band": None, "x_offset": 0, "canvas_hw": None, "bbox": None,
+                    "panorama": None, "canvas": None}
+        return {"records": res.records, "band": res.canvas, "x_offset": 0,
+                "canvas_hw": tuple(res.canvas.shape[:2]), "bbox": res.bbox, "panorama": res.panorama,
+                "canvas": res.canvas}
+    recs, owned, own_lo, (H, W), _ = rank_band_finish(S, raw[:nhead])
+    y0, y1, x0, x1 = crop_box(layout_box(layout), H, W, margin)
+    canvas = assemble_bands(owned, layout, (H, W), group, out=st._get("full_canvas", (H, W, 3), torch.uint8)
+                            if dist.get_rank(group) == 0 else None)
+    pano = None
+    if canvas is not None:
+        pano = canvas if (y0 > y1 or x0 > x1) else canvas[y0:y1 + 1, x0:x1 + 1]
+    return {"records": recs, "band": owned, "x_offset": own_lo, "canvas_hw": (H, W),
+            "bbox": (y0, y1, x0, x1), "panorama": pano, "canvas": canvas}
+
