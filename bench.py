@@ -7,11 +7,16 @@
 A step = one whole stitch of one rank's sequence, inputs resident in HBM:
 cylindrical projection -> SIFT features of every frame -> NN match (exact i8 MFMA) -> RANSAC
 -> [N>1: all_gather of per-pair records] -> drift correction + composite plan -> composite
-(band) -> crop bounding box [N>1: one 8-int-per-rank layout all_gather, every band sent to
-rank 0 (RCCL P2P over xGMI), which assembles the canvas and crops the panorama -- inside the
-timed step].  Rank r stitches the parrington loop
-starting at frame 17 r (18 frames, 17 pairs): per-GPU work is fixed ("weak" scaling) and the
-job is one panorama of N laps, N*17 + 1 distinct frames.
+(band) -> crop bounding box [N>1: the band's 8-int layout row all_gathered on the device and
+read back with the band head (one host read per rank), every band sent to rank 0 (RCCL P2P
+over xGMI), which assembles the canvas and crops the panorama -- inside the timed step].
+
+N = 1 (default): one stitch of the 18 parrington frames (BASELINE config 3, the headline).
+N > 1 (default): the north_star's scaling target, the synthetic 144-frame / 143-pair 1080p
+batch with its pairs sharded over the ranks (strong scaling; the line
+carries the committed N = 1 time of the same batch as `strong_n1_reference`), plus the weak
+form as `weak_laps`: rank r stitches the parrington loop from frame 17 r, one panorama of N
+laps.  --workload / --scaling choose either form explicitly.
 
 value  = distinct input Mpx of the job / max-over-ranks seconds per step.
 roofline: the dominant kernel, timed live with HIP events on the library's stream over the
@@ -118,7 +123,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="parrington", choices=["parrington", "grail", "synthetic"])
+    ap.add_argument("--workload", default=None, choices=["parrington", "grail", "synthetic"],
+                    help="default: parrington at N = 1 (the headline config); at N > 1 the "
+                         "north_star's scaling config, the synthetic 144-frame / 143-pair batch")
     ap.add_argument("--method", default="sift", choices=["sift", "harris"])
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -130,11 +137,25 @@ def parse():
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N=1 graph mode: time one synchronous run() per step instead of "
                          "Stitcher.run_sequence (two stitches in flight)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: a fixed sequence per rank (default); strong: ONE fixed sequence "
-                         "(the set's 18 frames, or the synthetic 144-frame / 143-pair batch) "
-                         "whose pairs are sharded over the ranks")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="weak: a fixed sequence per rank; strong: ONE fixed sequence (the set's "
+                         "18 frames, or the synthetic 144-frame / 143-pair batch) whose pairs are "
+                         "sharded over the ranks.  Default: weak at N = 1 (one parrington stitch), "
+                         "strong at N > 1 (with --workload defaulting to synthetic: SURVEY 8(e))")
+    ap.add_argument("--no-weak-laps", dest="weak_laps", action="store_false",
+                    help="N > 1: skip the secondary weak-scaling parrington-laps measurement")
     return ap.parse_args()
+
+
+def resolve_defaults(args, world):
+    """N = 1: the headline (parrington, one stitch per step).  N > 1: the north_star's scaling
+    target, >= 6x at 8 GPUs on the 144-pair synthetic batch -- the 143 pairs of config 5 sharded
+    over the ranks, the panorama assembled on rank 0 inside every step (strong scaling)."""
+    if args.workload is None:
+        args.workload = "parrington" if world == 1 else "synthetic"
+    if args.scaling is None:
+        args.scaling = "strong" if (world > 1 and args.workload == "synthetic") else "weak"
+    return args
 
 
 SYNTH_PAIRS_PER_RANK = 18      # config 5: 8 ranks x 18 pairs ~ the 143-pair 144-frame loop
@@ -237,10 +258,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world == 1 and args.gpus > 1:
         raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local)
+    # rehearsal of the N > 1 path on a one-GPU box (tests only, never a reported line): every
+    # rank on cuda:0 over gloo (PANO_BENCH_REHEARSE=1); the real run is one rank per GPU, RCCL
+    rehearse = os.environ.get("PANO_BENCH_REHEARSE") == "1"
+    torch.cuda.set_device(0 if rehearse else local)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    args = resolve_defaults(args, world)
 
     from vfx_image_stitching_amd import distributed as D
     from vfx_image_stitching_amd.pipeline import Stitcher
@@ -435,6 +463,15 @@ def main():
         elif len(frames) == 18:
             cpu = cpu_baseline(frames, focals, args.cpu_frames, args.method, h, w)
 
+    # N > 1 strong: the same batch's N = 1 time from the committed single-GPU line (a different
+    # box and run; the driver computes efficiency from its own per-N values), and the weak
+    # parrington laps as a secondary measurement
+    strong_ref = weak = None
+    if world > 1 and args.scaling == "strong":
+        strong_ref = strong_n1_reference(args.workload, args.method, ms_step)
+    if world > 1 and args.weak_laps and args.method == "sift" and args.scaling == "strong":
+        weak = weak_laps_secondary(args, rank, world)
+
     line = {
         "metric": "Mpixels/s stitched (18-img parrington, SIFT path)" if args.workload == "parrington"
         else f"Mpixels/s stitched ({args.workload}, {args.method})",
@@ -465,13 +502,76 @@ def main():
         "pcie_inclusive": pcie,
         "jpeg_inclusive": jpg,
         "cpu_baseline": cpu,
+        "strong_n1_reference": strong_ref,
+        "weak_laps": weak,
         "parity": parity,
         "kernels_ms_per_step": {k: round(v["total_ms"], 4) for k, v in per_kernel.items()},
     }
+    if rehearse:
+        line["rehearsal"] = ("PANO_BENCH_REHEARSE: every rank on cuda:0 over gloo (host-staged "
+                             "exchanges) -- a path check, not a scaling measurement")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def strong_n1_reference(workload, method, ms_step):
+    """The committed N = 1 line of the same strong-scaling batch (profiles/r*_bench_<workload>
+    _strong_n1.json, newest round): its ms_per_step and the speedup of this run over it."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_bench_{workload}_strong_n1.json")))
+    if not files or method != "sift":
+        return None
+    try:
+        ref = json.loads(open(files[-1]).read().strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return None
+    n1 = ref.get("ms_per_step")
+    if not n1:
+        return None
+    return {"ms_per_step_n1": n1, "source": os.path.relpath(files[-1], ROOT),
+            "speedup": round(n1 / ms_step, 3),
+            "note": "N = 1 time of the same batch from a committed single-GPU run (another box); "
+                    "the driver computes scaling efficiency from its own per-N values"}
+
+
+def weak_laps_secondary(args, rank, world):
+    """N > 1: the weak-scaling form as a secondary number -- rank r stitches the parrington
+    loop starting at frame 17 r, the job is one panorama of N laps assembled on rank 0; K steps,
+    max over ranks (the same timing rules as the main line)."""
+    import torch
+    import torch.distributed as dist
+
+    from vfx_image_stitching_amd import distributed as D
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    frames, focals, margin, (h, w), distinct, counts = workload("parrington", rank, world, "weak")
+    st = Stitcher("sift", cap=4096)
+    dev = st.upload(frames)
+    pair_start = sum(counts[:rank])
+
+    def step(graph):
+        return D.run_rank(st, dev, focals, pair_start, counts, margin=margin, graph=graph)
+    for _ in range(max(1, args.warmup)):
+        step(False)
+    step(True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    mpx = distinct * h * w / 1e6
+    return {"metric": "Mpixels/s stitched (parrington laps, weak scaling)", "unit": "Mpx/s",
+            "value": round(mpx / (el / args.steps), 3), "ms_per_step": round(el / args.steps * 1e3, 4),
+            "frames": distinct, "steps": args.steps, "scaling": "weak",
+            "note": "rank r stitches the parrington loop from frame 17 r; one panorama of N laps "
+                    "assembled on rank 0 per step"}
 
 
 def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx):

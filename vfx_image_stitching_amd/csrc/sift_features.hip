@@ -1209,7 +1209,13 @@ __device__ __forceinline__ float atan2_oct(float y, float x) {
 constexpr int kDescWaves = 4;         // waves (keypoints in flight) per workgroup
 constexpr int kDescCols = 128;        // patch sides up to this use the dense index (default
                                       // parameters: side <= 73)
-constexpr int kHist = 6 * 6 * 8;      // padded histogram (reference: tensor of (ww+2, ww+2, nb))
+#ifndef PANO_DESC_CELL
+#define PANO_DESC_CELL 8              // u64 slots per spatial cell (8 orientation bins [+ padding])
+#endif
+// cell stride: with 8 slots a cell's bin b sits in LDS bank pair (16 cell + 2 b) mod 32, so only
+// the cell's parity separates two lanes' cells; a stride of 9 shifts every cell by 18 banks
+constexpr int kCell = PANO_DESC_CELL, kRowC = 6 * kCell;
+constexpr int kHist = 6 * kRowC;      // padded histogram (reference: tensor of (ww+2, ww+2, nb))
 #ifndef PANO_DESC_SKEW
 #define PANO_DESC_SKEW 2              // u64 slots between histogram copies beyond kHist
 #endif
@@ -1242,6 +1248,10 @@ static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "str
 #ifndef PANO_DESC_RPI
 #define PANO_DESC_RPI 1               // fixed-point scale folded into the sample weight (fewer VALU)
 #endif
+#ifndef PANO_DESC_RING
+#define PANO_DESC_RING 0              // > 0: tap rows prefetched this many steps ahead via LDS-DMA
+#endif
+constexpr int kRing = PANO_DESC_RING > 0 ? PANO_DESC_RING : 1;
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
                                       // 3: every sample's taps from one cached location)
@@ -1294,6 +1304,9 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHistStride];
     __shared__ int col_lo[kDescWaves][kDescCols / kDescSS], col_pre[kDescWaves][kDescCols / kDescSS + 1];   // per super-strip
     __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
+#if PANO_DESC_RING
+    __shared__ __attribute__((aligned(16))) float ring[kDescWaves][PANO_DESC_RING][2][64 * 4];   // LDS-DMA tap rows, per wave
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     unsigned long long *h0 = hist[wv];
     unsigned long long *h = h0 + (lane & (kDescCopies - 1)) * kHistStride;   // this lane's copy
@@ -1399,9 +1412,9 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const int o0 = (int)fo & 7, o1 = (o0 + 1) & 7;
 #if PANO_DESC_RPI
             // (r0 + 1, c0 + 1) bin from the integer-valued floors (exact in f32): one conversion
-            const int base = (int)fmaf(fr, 48.0f, fmaf(fc, 8.0f, 56.0f));
+            const int base = (int)fmaf(fr, (float)kRowC, fmaf(fc, (float)kCell, (float)(kRowC + kCell)));
 #else
-            const int base = ((int)fr + 1) * 48 + ((int)fc + 1) * 8;   // (r0 + 1, c0 + 1) bin
+            const int base = ((int)fr + 1) * kRowC + ((int)fc + 1) * kCell;   // (r0 + 1, c0 + 1) bin
 #endif
             const float c1 = wm * rf, c0w = wm - c1;
             const float v00 = c0w * (1.0f - cf), v01 = c0w * cf, v10 = c1 * (1.0f - cf), v11 = c1 * cf;
@@ -1419,14 +1432,14 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             unsigned long long *hA = h + base + o0, *hB = h + base + o1;
 #if PANO_DESC_ABL == 0
             atomicAdd(hA, fix(v00 * nof));      atomicAdd(hB, fix(v00 * of));
-            atomicAdd(hA + 8, fix(v01 * nof));  atomicAdd(hB + 8, fix(v01 * of));
-            atomicAdd(hA + 48, fix(v10 * nof)); atomicAdd(hB + 48, fix(v10 * of));
-            atomicAdd(hA + 56, fix(v11 * nof)); atomicAdd(hB + 56, fix(v11 * of));
+            atomicAdd(hA + kCell, fix(v01 * nof));  atomicAdd(hB + kCell, fix(v01 * of));
+            atomicAdd(hA + kRowC, fix(v10 * nof)); atomicAdd(hB + kRowC, fix(v10 * of));
+            atomicAdd(hA + kRowC + kCell, fix(v11 * nof)); atomicAdd(hB + kRowC + kCell, fix(v11 * of));
 #elif PANO_DESC_ABL == 1
             hA[0] = fix(v00 * nof);  hB[0] = fix(v00 * of);
-            hA[8] = fix(v01 * nof);  hB[8] = fix(v01 * of);
-            hA[48] = fix(v10 * nof); hB[48] = fix(v10 * of);
-            hA[56] = fix(v11 * nof); hB[56] = fix(v11 * of);
+            hA[kCell] = fix(v01 * nof);  hB[kCell] = fix(v01 * of);
+            hA[kRowC] = fix(v10 * nof); hB[kRowC] = fix(v10 * of);
+            hA[kRowC + kCell] = fix(v11 * nof); hB[kRowC + kCell] = fix(v11 * of);
 #else
             abl_sink += fix(v00 * nof) + fix(v00 * of) + fix(v01 * nof) + fix(v01 * of) + fix(v10 * nof) +
                         fix(v10 * of) + fix(v11 * nof) + fix(v11 * of) + (unsigned long long)(base + o0 + o1);
@@ -1509,6 +1522,142 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const int sub = lane & (kDescGrp - 1);
             int t = (lane / kDescGrp) * Q;
             const int tend = min(t + Q, nsamp);
+#if PANO_DESC_RING
+            // Tap rows prefetched kRing steps ahead through an LDS ring by LDS-DMA loads
+            // (global_load_lds, 2 x 12 bytes per lane and step, no VGPRs): more of each wave's
+            // scattered row loads in flight than the one-step register prefetch allows (its
+            // misses, not the VALU or the histogram, bound the kernel: PANO_DESC_ABL ablations).
+            // The walk runs a uniform iteration count Q; a lane past its run issues its ring
+            // loads from a fixed in-image address and bins nothing.  A strip change loads the
+            // new strip's upper two rows directly (about once per lane run).
+            {
+                const int nst = tend > t ? tend - t : 0;     // this lane's steps
+                int sx = 0, ys = 0, yend = 0;
+                if (nst > 0) {
+                    int shi = nstrip - 1;                    // largest strip with cpre[sx] <= t
+                    while (sx < shi) {
+                        const int mid = (sx + shi + 1) >> 1;
+                        if (cpre[mid] <= t) sx = mid;
+                        else shi = mid - 1;
+                    }
+                    ys = clo[sx] + (t - cpre[sx]);
+                    yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                }
+                constexpr int WN = kDescSW + 2;
+                static_assert(WN == 6, "the ring moves 2 x 3 floats per lane and step");
+                auto rowp = [&](int sxx, int y) {
+                    return img + (size_t)(py + y) * cols + (px + sxx * kDescSS + sub * kDescSW - half) - 1;
+                };
+                const float *dummy = img + (size_t)py * cols + px - 1;
+                float *rw = &ring[wv][0][0][0];
+                // 16-byte LDS-DMA loads land at base + 16 lane (a 12-byte one too: measured,
+                // tools/probes/glds_layout.hip), so a lane's 6 floats are two 16-byte loads,
+                // floats 0-3 and 2-5 of its window
+                // M0 written and read in one statement with the s_nop the M0 -> LDS-DMA hazard
+                // needs (cdna_hip_programming.md, LDS-DMA recipe)
+                const unsigned rw_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float *)rw;
+                auto issue = [&](int slot, const float *q) {
+                    const unsigned d0 = __builtin_amdgcn_readfirstlane(rw_lds + slot * 2048);
+                    const unsigned d1 = d0 + 1024;
+                    unsigned keep;
+                    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                                 : "=&s"(keep) : "v"(q), "s"(d0) : "memory");
+                    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                                 : "=&s"(keep) : "v"(q + 2), "s"(d1) : "memory");
+                };
+                // the prefetch cursor: position of step ip (ip < nst), advanced like the walk
+                int psx = sx, pys = ys, pyend = yend;
+                auto pf_next = [&]() {
+                    ++pys;
+                    if (pys >= pyend) {
+                        do { ++psx; } while (psx < nstrip && cpre[psx + 1] == cpre[psx]);
+                        if (psx < nstrip) {
+                            pys = clo[psx];
+                            pyend = clo[psx] + (cpre[psx + 1] - cpre[psx]);
+                        }
+                    }
+                };
+#pragma unroll
+                for (int k = 0; k < kRing; ++k) {
+                    issue(k, k < nst ? rowp(psx, pys + 1) : dummy);
+                    if (k + 1 < kRing && k + 1 < nst) pf_next();     // the cursor ends on step kRing - 1
+                }
+                float br[kDescSW], bc[kDescSW], xs2[kDescSW];
+                auto strip_consts = [&](int sxx) {
+#pragma unroll
+                    for (int i = 0; i < kDescSW; ++i) {
+                        const int c = sxx * kDescSS + sub * kDescSW + i;
+                        br[i] = cbr[c];
+                        bc[i] = cbc[c];
+                        xs2[i] = (float)((c - half) * (c - half));
+                    }
+                };
+                float Tm[WN], T0[WN];
+                if (nst > 0) {
+                    strip_consts(sx);
+                    const float *q0 = rowp(sx, ys - 1), *q1 = rowp(sx, ys);
+#pragma unroll
+                    for (int i = 0; i < WN; ++i) { Tm[i] = q0[i]; T0[i] = q1[i]; }
+                }
+                for (int it = 0; it < Q; ++it) {
+                    const int slot = it % kRing;
+#ifdef PANO_DESC_RING_VM0
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+                    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * (kRing - 1)) : "memory");
+#endif
+                    const bool live = it < nst;
+                    float Tp[WN];
+                    {
+                        const float4 a = *(const float4 *)(rw + slot * 512 + lane * 4);
+                        const float2 b = *(const float2 *)(rw + slot * 512 + 256 + lane * 4 + 2);
+                        Tp[0] = a.x; Tp[1] = a.y; Tp[2] = a.z; Tp[3] = a.w; Tp[4] = b.x; Tp[5] = b.y;
+                    }
+#ifdef PANO_DESC_RING_DEBUG
+                    if (live) {
+                        const float *qq = rowp(sx, ys + 1);
+                        bool bad = false;
+                        for (int i = 0; i < WN; ++i) bad |= qq[i] != Tp[i];
+                        if (bad && (it == 2 || it == 3) && blockIdx.x < 2) {
+                            const float *qa = rowp(sx, ys), *qb = rowp(sx, ys + 2), *qc = rowp(sx, ys - 1);
+                            printf("ring mismatch blk %d lane %d it %d nst %d sx %d ys %d: ring %g %g | row+1 %g %g | row %g %g | row+2 %g %g | row-1 %g %g\n",
+                                   (int)blockIdx.x, lane, it, nst, sx, ys, Tp[0], Tp[1], qq[0], qq[1], qa[0], qa[1], qb[0], qb[1], qc[0], qc[1]);
+                        }
+                    }
+#endif
+                    if (live) {
+                        const float ysf = (float)ys, ys2 = ysf * ysf;
+#pragma unroll
+                        for (int i = 0; i < kDescSW; ++i)
+                            sample(T0[i + 2] - T0[i], Tm[i + 1] - Tp[i + 1], fmaf(ysf, ar, br[i]),
+                                   fmaf(ysf, ac, bc[i]), __builtin_amdgcn_exp2f(kq * (ys2 + xs2[i])));
+                    }
+                    // the slot is re-filled with step it + kRing once its reads have returned
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    const int ip = it + kRing;
+                    if (ip < nst) pf_next();
+                    issue(slot, ip < nst ? rowp(psx, pys + 1) : dummy);
+                    if (live && it + 1 < nst) {
+                        int yn = ys + 1;
+                        if (yn >= yend) {
+                            do { ++sx; } while (cpre[sx + 1] == cpre[sx]);
+                            yn = clo[sx];
+                            yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                            strip_consts(sx);
+                            const float *q0 = rowp(sx, yn - 1), *q1 = rowp(sx, yn);
+#pragma unroll
+                            for (int i = 0; i < WN; ++i) { Tm[i] = q0[i]; T0[i] = q1[i]; }
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < WN; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; }
+                        }
+                        ys = yn;
+                    }
+                }
+                // drain: the ring's last loads land before the next keypoint reuses it
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+#else
             if (t < tend) {
                 int sx = 0, shi = nstrip - 1;              // largest strip with cpre[sx] <= t
                 while (sx < shi) {
@@ -1596,6 +1745,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                     ys = yn;
                 }
             }
+#endif
         } else {
             // very large patches (non-default parameters): every sample of the square
             const int S = side * side;
@@ -1617,7 +1767,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // crop the padding: element i = (r, c, o) of the 4 x 4 x 8 block
         auto interior = [&](int i) {
-            const int e = ((i >> 5) + 1) * 48 + (((i >> 3) & 3) + 1) * 8 + (i & 7);
+            const int e = ((i >> 5) + 1) * kRowC + (((i >> 3) & 3) + 1) * kCell + (i & 7);
             unsigned long long v = 0;
 #pragma unroll
             for (int c = 0; c < kDescCopies; ++c) v += h0[c * kHistStride + e];
