@@ -89,6 +89,7 @@ struct pano_ctx {
     float *taps = nullptr;               // device Gaussian taps (f32), per level [L][PANO_MAX_TAPS]
     float taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];    // what *taps holds
     bool taps_valid = false;
+    int32_t *octs_sync = nullptr; size_t octs_sync_bytes = 0;   // blur_octs row counters (zeroed)
     uint8_t *gray = nullptr; size_t gray_bytes = 0;   // u8 gray frames (base blur input)
     int32_t *boxslots = nullptr; size_t boxslots_bytes = 0;   // crop-box partials (kBoxSlots x 4)
     // ---- match / ransac scratch
