@@ -595,11 +595,27 @@ row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
 // (candidate rows) are formed while the rows are staged: the lanes staging one row sum its
 // bytes with v_dot4_u32_u8 and a shuffle reduction (no separate row_consts launch; with
 // PANO_I8_QLDS=0 the query rows stay in registers and row_consts still runs).
+typedef __attribute__((address_space(1))) int g_i32;
+typedef __attribute__((address_space(1))) float g_f32;
+
+// reduce_parts folded into dist_i8 (fold != null): each workgroup stores its partial rows
+// write-through (sc1), drains them (s_waitcnt vmcnt(0), barrier) and counts itself in on its
+// (pair, query tile) with one device-scope add; the last of the tile's live splits reads every
+// split's partials back with sc1 loads (MI355X guide, visibility, R1: no fence), merges them in
+// split order -- reduce_parts' arithmetic -- writes best / d1 / d2 and re-zeroes the counter.
+// Query tiles with no live split (past the count, or no candidates) get reduce_parts' "no
+// candidate" rows from their split-0 workgroup.
+struct MatchFold {
+    int32_t *cnt;                        // [pair][query tile] arrivals (zero between launches)
+    int32_t *best;
+    float *d1, *d2;
+};
+
 template <bool SECOND>
 __global__ void __launch_bounds__(512, PANO_I8_WAVES)
 dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, const int32_t *__restrict__ cst,
         const int32_t *__restrict__ counts, int cap, PairArg pairs, Part *__restrict__ parts,
-        int n_split) {
+        int n_split, MatchFold fold) {
     __shared__ __attribute__((aligned(16))) unsigned char Bs2[2][BT * BPI];
     __shared__ __attribute__((aligned(16))) int Cs2[3][BT];   // C32 of tile t in Cs2[t % 3] (a lagging epilogue reads t - 1)
 #if PANO_I8_QLDS
@@ -620,7 +636,17 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
     NB = min(max(NB, 0), cap);
     const int i0 = blockIdx.z * QT;
     const int n_jt = (NB + BT - 1) / BT;
-    if (i0 >= NA || (int)blockIdx.x >= n_jt) return;
+    if (i0 >= NA || (int)blockIdx.x >= n_jt) {
+        if (fold.cnt && blockIdx.x == 0 && (i0 >= NA || n_jt == 0)) {
+            for (int t = threadIdx.x; t < QT && i0 + t < cap; t += 512) {
+                const size_t o = (size_t)p * cap + i0 + t;
+                fold.best[o] = -1;
+                fold.d1[o] = INFINITY;
+                if (fold.d2) fold.d2[o] = INFINITY;
+            }
+        }
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wi = wv & 3, wj = wv >> 2;
     const int lr = lane & 31, lh = lane >> 5;
@@ -815,9 +841,47 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
 #endif
             const float db = x.best >= kNone ? INFINITY : (float)(ra + x.best);
             const float ds = x.second >= kNone ? INFINITY : (float)(ra + x.second);
-            parts[((size_t)p * n_split + blockIdx.x) * cap + gi] = Part{db, x.idx, ds};
+            Part *q = parts + ((size_t)p * n_split + blockIdx.x) * cap + gi;
+            if (fold.cnt) {
+                __hip_atomic_store((g_f32 *)&q->best, db, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((g_i32 *)&q->idx, x.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((g_f32 *)&q->second, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                *q = Part{db, x.idx, ds};
+            }
         }
     }
+    if (!fold.cnt) return;
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every wave: its partials landed
+    __syncthreads();
+    int32_t *cnt = fold.cnt + (size_t)p * gridDim.z + blockIdx.z;
+    if (tid == 0)
+        last = __hip_atomic_fetch_add((g_i32 *)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               min(n_split, n_jt) - 1;
+    __syncthreads();
+    if (!last) return;
+    if (tid < QT && i0 + tid < cap) {
+        const int gi = i0 + tid;
+        float b = INFINITY, s = INFINITY;
+        int j = -1;
+        if (gi < NA) {                           // reduce_parts, reading the partials sc1
+            j = 0x7fffffff;
+            const int nt = min(n_jt, n_split);
+            for (int t = 0; t < nt; ++t) {
+                Part *q = parts + ((size_t)p * n_split + t) * cap + gi;
+                merge(b, j, s, __hip_atomic_load((g_f32 *)&q->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load((g_i32 *)&q->idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load((g_f32 *)&q->second, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+            if (s >= kPadNorm) s = INFINITY;
+        }
+        const size_t o = (size_t)p * cap + gi;
+        fold.best[o] = j;
+        fold.d1[o] = b;
+        if (fold.d2) fold.d2[o] = s;
+    }
+    if (tid == 0) __hip_atomic_store((g_i32 *)cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void reduce_parts(const Part *__restrict__ parts, const int32_t *__restrict__ counts,
@@ -932,7 +996,11 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
         }
         // query tiles x candidate splits x pairs: at least ~2 workgroups per CU even when
         // each pair is small (parrington); large pairs walk their candidate tiles in-kernel
-        const int n_split = std::max(1, std::min(n_bt, (1024 + n_qt * np - 1) / (n_qt * np)));
+        static const int target_wgs = [] {
+            const char *e = getenv("PANO_MATCH_WGS");   // fewest workgroups the splits aim at
+            return e ? std::max(1, atoi(e)) : 1024;
+        }();
+        const int n_split = std::max(1, std::min(n_bt, (target_wgs + n_qt * np - 1) / (n_qt * np)));
         const size_t part_bytes = ((size_t)np * n_split * cap * sizeof(Part) + 255) & ~size_t(255);
         int rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes, part_bytes);
         if (rc) return rc;
@@ -963,14 +1031,42 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
                 }
                 PANO_LAUNCH_CHECK(ctx, "row_consts");
             }
+            // reduce_parts folded in (PANO_MATCH_FOLD, default 1; 0: the separate launch)
+            static const bool fold_on = [] {
+                const char *e = getenv("PANO_MATCH_FOLD");
+                return e ? atoi(e) != 0 : true;
+            }();
+            MatchFold mf{};
+            if (fold_on) {
+                const size_t need = (size_t)256 * n_qt * sizeof(int32_t);
+                if (need > ctx->match_sync_bytes) {
+                    if (ctx->capturing)
+                        return pano_fail(ctx, PANO_E_UNSUPPORTED, "match counters grown inside a graph capture");
+                    if (ctx->match_sync) {
+                        PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+                        (void)hipFree(ctx->match_sync);
+                        ctx->match_sync = nullptr;
+                        ctx->match_sync_bytes = 0;
+                        ++ctx->generation;
+                    }
+                    PANO_HIP(ctx, hipMalloc((void **)&ctx->match_sync, need));
+                    PANO_HIP(ctx, hipMemset(ctx->match_sync, 0, need));   // each launch re-zeroes
+                    ctx->match_sync_bytes = need;
+                }
+                mf.cnt = ctx->match_sync;
+                mf.best = bp;
+                mf.d1 = p1;
+                mf.d2 = p2;
+            }
             {
                 PanoProf prof_(ctx, PK_DIST_MFMA);
                 if (p2)
-                    dist_i8<true><<<grid, 512, 0, ctx->stream>>>(desc, norms, cst, counts, cap, pa, parts, n_split);
+                    dist_i8<true><<<grid, 512, 0, ctx->stream>>>(desc, norms, cst, counts, cap, pa, parts, n_split, mf);
                 else
-                    dist_i8<false><<<grid, 512, 0, ctx->stream>>>(desc, norms, cst, counts, cap, pa, parts, n_split);
+                    dist_i8<false><<<grid, 512, 0, ctx->stream>>>(desc, norms, cst, counts, cap, pa, parts, n_split, mf);
             }
             PANO_LAUNCH_CHECK(ctx, "dist_i8");
+            if (fold_on) continue;
         } else {
             {
                 PanoProf prof_(ctx, PK_DIST_MFMA);

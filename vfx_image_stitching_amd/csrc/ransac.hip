@@ -162,19 +162,116 @@ constexpr int VJS = 8;    // splits of the match range per hypothesis chunk (gri
 // left ~1.4 waves per SIMD and exposed the chain and LDS latency (1080p: 0.63 ms per step).
 // Splitting the match range VJS ways gives VJS x the waves; four matches per iteration are
 // four independent chains.  Partial counts are integer atomics into zeroed votes: exact.
+// pair_select's work for pair p with NT threads: the record of an overflowed or match-less
+// pair, else the first maximum of the votes (strict '>' in match order,
+// image_stitching_sift.py:107) and its record.  vote(m) reads hypothesis m's count.
+template <int NT, typename VOTE>
+__device__ __forceinline__ void select_pair(int *ish, const pano_kp *__restrict__ kps,
+                                            const int32_t *__restrict__ xy, const int32_t *__restrict__ counts,
+                                            int cap, int fa, int fb, const int32_t *__restrict__ bp,
+                                            const double2 *__restrict__ mv, const int32_t *__restrict__ mi, int K,
+                                            VOTE vote, pano_pair_rec *__restrict__ rec) {
+    const int tid = threadIdx.x;
+    pano_pair_rec r{};
+    r.n_matches = K;
+    // a frame with more keypoints than the capacity (count > cap) or whose keypoint stages
+    // overflowed (count -1) was matched on a truncated set: the pair's result is not the
+    // reference's, so the record says so instead of carrying a silently different shift
+    const int ca = counts[fa], cb = counts[fb];
+    if (ca < 0 || cb < 0 || ca > cap || cb > cap) {
+        if (tid == 0) {
+            r.best = -1;
+            r.status = PANO_E_OVERFLOW;
+            *rec = r;
+        }
+        return;
+    }
+    if (K == 0) {
+        if (tid == 0) {
+            r.best = -1;
+            r.status = PANO_E_NOMATCH;
+            *rec = r;
+        }
+        return;
+    }
+    int my_v = -1, my_m = 0x7fffffff;
+    for (int m = tid; m < K; m += NT) {
+        const int v = vote(m);
+        if (v > my_v) { my_v = v; my_m = m; }
+    }
+    ish[tid] = my_v;
+    ish[NT + tid] = my_m;
+    __syncthreads();
+    for (int off = NT / 2; off > 0; off >>= 1) {
+        if (tid < off) {
+            const int v2 = ish[tid + off], m2 = ish[NT + tid + off];
+            const int v1 = ish[tid], m1 = ish[NT + tid];
+            if (v2 > v1 || (v2 == v1 && m2 < m1)) {
+                ish[tid] = v2;
+                ish[NT + tid] = m2;
+            }
+        }
+        __syncthreads();
+    }
+    const int bm = ish[NT], bv = ish[0];
+    if (tid == 0) {
+        const int i = mi[bm];
+        const int j = bp[i];
+        if (kps) {
+            const pano_kp ka = kps[(size_t)fa * cap + i], kb = kps[(size_t)fb * cap + j];
+            r.xA = ka.x; r.yA = ka.y; r.xB = kb.x; r.yB = kb.y;
+        } else {
+            r.xA = xy[((size_t)fa * cap + i) * 2];
+            r.yA = xy[((size_t)fa * cap + i) * 2 + 1];
+            r.xB = xy[((size_t)fb * cap + j) * 2];
+            r.yB = xy[((size_t)fb * cap + j) * 2 + 1];
+        }
+        r.dx = mv[bm].x;
+        r.dy = mv[bm].y;
+        r.votes = bv;
+        r.best = bm;
+        r.status = PANO_OK;
+        *rec = r;
+    }
+}
+
+typedef __attribute__((address_space(1))) int g_i32;
+
+// pair_select folded into pair_votes (SEL, PANO_RANSAC_FOLD): each live workgroup drains its
+// vote atomics (s_waitcnt vmcnt(0), barrier) and counts itself in on its pair with one
+// device-scope add; the pair's last live workgroup reads the votes back with sc1 loads (device-
+// scope atomics and sc1 loads meet at the device-coherent level: MI355X guide, visibility),
+// runs pair_select's work and re-zeroes the counter.  A pair with no live vote workgroup (no
+// match) gets its record from workgroup (0, p, 0).
+struct SelArgs {
+    const pano_kp *kps;
+    const int32_t *xy, *counts, *best, *midx;
+    PairArg pairs;
+    pano_pair_rec *recs;
+    int32_t *cnt;                        // [pair] arrivals (zero between launches)
+};
+
+template <bool SEL>
 __global__ void __launch_bounds__(VB)
 pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount, int cap,
-           double thr, int32_t *__restrict__ votes) {
+           double thr, int32_t *__restrict__ votes, SelArgs sa) {
     __shared__ double2 tile[VB];
+    __shared__ int ish[2 * VB];
+    __shared__ int last;
     // grid (split, pair, hypothesis chunk): the chunks are sized by the capacity, and with
     // the chunk index outermost every live chunk 0 is dispatched before the empty ones
     const int p = blockIdx.y, tid = threadIdx.x;
     const int K = kcount[p];
     const int m0 = blockIdx.z * VB;
-    if (m0 >= K) return;                              // whole workgroup
     const int jlo = (int)((long long)K * blockIdx.x / VJS), jhi = (int)((long long)K * (blockIdx.x + 1) / VJS);
-    if (jlo >= jhi) return;
     const double2 *mv = moves + (size_t)p * cap;
+    if (m0 >= K || jlo >= jhi) {                      // whole workgroup
+        if (SEL && K == 0 && blockIdx.x == 0 && blockIdx.z == 0)
+            select_pair<VB>(ish, sa.kps, sa.xy, sa.counts, cap, sa.pairs.a[p], sa.pairs.b[p],
+                            sa.best + (size_t)p * cap, mv, sa.midx + (size_t)p * cap, 0, [](int) { return 0; },
+                            sa.recs + p);
+        return;
+    }
     const int m = m0 + tid;
     const double2 me = m < K ? mv[m] : make_double2(0.0, 0.0);
     int v = 0;
@@ -201,6 +298,28 @@ pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount
         }
     }
     if (m < K && v) atomicAdd(&votes[(size_t)p * cap + m], v);
+    if constexpr (SEL) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its adds performed
+        __syncthreads();
+        if (tid == 0) {
+            int splits = 0;                                   // live match-range splits of K
+            for (int x = 0; x < VJS; ++x)
+                splits += (int)((long long)K * x / VJS) < (int)((long long)K * (x + 1) / VJS);
+            const int n_live = ((K + VB - 1) / VB) * splits;
+            last = __hip_atomic_fetch_add((g_i32 *)(sa.cnt + p), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   n_live - 1;
+        }
+        __syncthreads();
+        if (!last) return;
+        int32_t *vp = votes + (size_t)p * cap;
+        select_pair<VB>(ish, sa.kps, sa.xy, sa.counts, cap, sa.pairs.a[p], sa.pairs.b[p],
+                        sa.best + (size_t)p * cap, mv, sa.midx + (size_t)p * cap, K,
+                        [&](int mm) {
+                            return __hip_atomic_load((g_i32 *)(vp + mm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        },
+                        sa.recs + p);
+        if (tid == 0) __hip_atomic_store((g_i32 *)(sa.cnt + p), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __global__ void __launch_bounds__(RB)
@@ -210,74 +329,11 @@ pair_select(const pano_kp *__restrict__ kps, const int32_t *__restrict__ xy,
             const int32_t *__restrict__ midx, const int32_t *__restrict__ kcount,
             const int32_t *__restrict__ votes, pano_pair_rec *__restrict__ recs) {
     __shared__ int ish[2 * RB];
-    const int p = blockIdx.x, tid = threadIdx.x;
-    const int fa = pairs.a[p], fb = pairs.b[p];
-    const int K = kcount[p];
-    const int32_t *bp = best + (size_t)p * cap;
-    const double2 *mv = moves + (size_t)p * cap;
-    const int32_t *mi = midx + (size_t)p * cap;
-    pano_pair_rec r{};
-    r.n_matches = K;
-    // a frame with more keypoints than the capacity (count > cap) or whose keypoint stages
-    // overflowed (count -1) was matched on a truncated set: the pair's result is not the
-    // reference's, so the record says so instead of carrying a silently different shift
-    const int ca = counts[fa], cb = counts[fb];
-    if (ca < 0 || cb < 0 || ca > cap || cb > cap) {
-        if (tid == 0) {
-            r.best = -1;
-            r.status = PANO_E_OVERFLOW;
-            recs[p] = r;
-        }
-        return;
-    }
-    if (K == 0) {
-        if (tid == 0) {
-            r.best = -1;
-            r.status = PANO_E_NOMATCH;
-            recs[p] = r;
-        }
-        return;
-    }
-    // first maximum (strict '>' in match order, image_stitching_sift.py:107)
-    int my_v = -1, my_m = 0x7fffffff;
-    for (int m = tid; m < K; m += RB) {
-        const int v = votes[(size_t)p * cap + m];
-        if (v > my_v) { my_v = v; my_m = m; }
-    }
-    ish[tid] = my_v;
-    ish[RB + tid] = my_m;
-    __syncthreads();
-    for (int off = RB / 2; off > 0; off >>= 1) {
-        if (tid < off) {
-            const int v2 = ish[tid + off], m2 = ish[RB + tid + off];
-            const int v1 = ish[tid], m1 = ish[RB + tid];
-            if (v2 > v1 || (v2 == v1 && m2 < m1)) {
-                ish[tid] = v2;
-                ish[RB + tid] = m2;
-            }
-        }
-        __syncthreads();
-    }
-    const int bm = ish[RB], bv = ish[0];
-    if (tid == 0) {
-        const int i = mi[bm];
-        const int j = bp[i];
-        if (kps) {
-            const pano_kp ka = kps[(size_t)fa * cap + i], kb = kps[(size_t)fb * cap + j];
-            r.xA = ka.x; r.yA = ka.y; r.xB = kb.x; r.yB = kb.y;
-        } else {
-            r.xA = xy[((size_t)fa * cap + i) * 2];
-            r.yA = xy[((size_t)fa * cap + i) * 2 + 1];
-            r.xB = xy[((size_t)fb * cap + j) * 2];
-            r.yB = xy[((size_t)fb * cap + j) * 2 + 1];
-        }
-        r.dx = mv[bm].x;
-        r.dy = mv[bm].y;
-        r.votes = bv;
-        r.best = bm;
-        r.status = PANO_OK;
-        recs[p] = r;
-    }
+    const int p = blockIdx.x;
+    const int32_t *vp = votes + (size_t)p * cap;
+    select_pair<RB>(ish, kps, xy, counts, cap, pairs.a[p], pairs.b[p], best + (size_t)p * cap,
+                    moves + (size_t)p * cap, midx + (size_t)p * cap, kcount[p], [&](int m) { return vp[m]; },
+                    recs + p);
 }
 
 __global__ void __launch_bounds__(RB)
@@ -325,12 +381,39 @@ int launch_pair_shifts(pano_ctx *ctx, const pano_kp *kps, const int32_t *xy_i32,
                 (float)desc_thresh, ratio > 0 ? ratio : 0.0, moves + o, midx + o, kcount + p0, votes + o);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_compact");
+        static const bool fold_on = [] {              // pair_select folded into pair_votes
+            const char *e = getenv("PANO_RANSAC_FOLD");
+            return e ? atoi(e) != 0 : true;
+        }();
+        SelArgs sa{};
+        if (fold_on) {
+            const size_t need_c = 256 * sizeof(int32_t);
+            if (need_c > ctx->sel_sync_bytes) {
+                if (ctx->capturing) return pano_fail(ctx, PANO_E_UNSUPPORTED, "select counters inside a graph capture");
+                PANO_HIP(ctx, hipMalloc((void **)&ctx->sel_sync, need_c));
+                PANO_HIP(ctx, hipMemset(ctx->sel_sync, 0, need_c));     // each launch re-zeroes
+                ctx->sel_sync_bytes = need_c;
+            }
+            sa.kps = kps;
+            sa.xy = xy_i32;
+            sa.counts = counts;
+            sa.best = best + o;
+            sa.midx = midx + o;
+            sa.pairs = pa;
+            sa.recs = recs + p0;
+            sa.cnt = ctx->sel_sync;
+        }
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
-            pair_votes<<<dim3(VJS, np, (cap + VB - 1) / VB), VB, 0, ctx->stream>>>(moves + o, kcount + p0, cap,
-                                                                                  thr, votes + o);
+            if (fold_on)
+                pair_votes<true><<<dim3(VJS, np, (cap + VB - 1) / VB), VB, 0, ctx->stream>>>(moves + o, kcount + p0,
+                                                                                            cap, thr, votes + o, sa);
+            else
+                pair_votes<false><<<dim3(VJS, np, (cap + VB - 1) / VB), VB, 0, ctx->stream>>>(moves + o, kcount + p0,
+                                                                                             cap, thr, votes + o, sa);
         }
         PANO_LAUNCH_CHECK(ctx, "pair_votes");
+        if (fold_on) continue;
         {
             PanoProf prof_(ctx, PK_PAIR_SHIFTS);
             pair_select<<<np, RB, 0, ctx->stream>>>(kps, xy_i32, counts, cap, pa, best + o, moves + o, midx + o,
