@@ -582,6 +582,9 @@ row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
 #ifndef PANO_I8_QLDS
 #define PANO_I8_QLDS 1                   // query tile in LDS (0: in registers)
 #endif
+#ifndef PANO_I8_ABL
+#define PANO_I8_ABL 0                    // timing ablations of the epilogue (wrong results): 1, 2
+#endif
 #ifndef PANO_I8_STAGGER
 #define PANO_I8_STAGGER 1                // waves 4-7 run each tile's epilogue one barrier late
 #endif
@@ -753,6 +756,13 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
             for (int b = 0; b < 2; ++b)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
+#if PANO_I8_ABL == 1                                       // timing ablation: 1 VALU op per distance
+                    tb[b] = min(tb[b], acc[a][b][r]);
+                    continue;
+#elif PANO_I8_ABL == 2                                     // timing ablation: no epilogue VALU
+                    if (r == 0) tb[b] = min(tb[b], acc[a][b][0] + cj[0]);
+                    continue;
+#endif
                     const int key = mad_i24(acc[a][b][r], -64, cj[r]);
                     if (SECOND) ts[b] = med3_i32(tb[b], key, ts[b]);
                     tb[b] = min(tb[b], key);

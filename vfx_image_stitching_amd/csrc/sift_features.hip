@@ -1251,7 +1251,9 @@ static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "str
 #ifndef PANO_DESC_RING
 #define PANO_DESC_RING 0              // > 0: tap rows prefetched this many steps ahead via LDS-DMA
 #endif
-constexpr int kRing = PANO_DESC_RING > 0 ? PANO_DESC_RING : 1;
+#if PANO_DESC_RING
+constexpr int kRing = PANO_DESC_RING;
+#endif
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
                                       // 3: every sample's taps from one cached location)
