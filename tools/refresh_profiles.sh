@@ -7,7 +7,7 @@
 #   gpurun_out/refresh/; copy what is judged into profiles/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-R=${R:-r04}
+R=${R:-r05}
 O=gpurun_out/refresh
 rm -rf $O && mkdir -p $O
 for w in parrington synthetic; do

@@ -585,6 +585,9 @@ row_consts(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms,
 #ifndef PANO_I8_ABL
 #define PANO_I8_ABL 0                    // timing ablations of the epilogue (wrong results): 1, 2
 #endif
+#ifndef PANO_I8_DBL
+#define PANO_I8_DBL 0                    // 1: two accumulator sets per wave (epilogue beside the next MFMAs)
+#endif
 #ifndef PANO_I8_STAGGER
 #define PANO_I8_STAGGER 1                // waves 4-7 run each tile's epilogue one barrier late
 #endif
@@ -732,7 +735,8 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
         for (int q = 0; q < 2; ++q)
             d4[q] = make_uint4(pre[q].x ^ 0x80808080u, pre[q].y ^ 0x80808080u, pre[q].z ^ 0x80808080u,
                                pre[q].w ^ 0x80808080u);
-        if (sp == 0) Cs2[cbuf][sr] = pre_c * 32 + key_idx(sr);     // C32: the key's base
+        if (sp == 0) Cs2[cbuf][sr] = PANO_I8_DBL ? -(pre_c * 32 + key_idx(sr))   // -C32: max form
+                                                 : pre_c * 32 + key_idx(sr);     // C32: the key's base
     };
     int best[2] = {kBig, kBig}, second[2] = {kBig, kBig};
     int bj[2] = {0x7fffffff, 0x7fffffff};
@@ -740,9 +744,15 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
     // the epilogue of one tile: its least / second-least key per query row folded into the
     // running state (keys are unique per lane; tiles come in increasing j, so strict < keeps
     // the first index on a tie)
-    auto epilogue = [&](const int *Cs, int jt_e) {
+    auto epilogue = [&](const i32x16 (&acc)[2][2], const int *Cs, int jt_e) {
         const int jb = jt_e * BT + wj * 64 + 4 * lh;
+#if PANO_I8_DBL
+        // negated keys -key = 64 a'.b' - C32 = (acc << 6) + (-C32): ONE v_lshl_add_u32 (a plain
+        // op the scheduler can place between MFMAs), folded with max / med3
+        int tb[2] = {(int)0x80000000, (int)0x80000000}, ts[2] = {(int)0x80000000, (int)0x80000000};
+#else
         int tb[2] = {0x7fffffff, 0x7fffffff}, ts[2] = {0x7fffffff, 0x7fffffff};
+#endif
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             // C32 of this lane's 16 candidate rows: rows (r & 3) + 8 (r >> 2) + 4 lh of block a
@@ -763,11 +773,24 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
                     if (r == 0) tb[b] = min(tb[b], acc[a][b][0] + cj[0]);
                     continue;
 #endif
+#if PANO_I8_DBL
+                    const int nkey = (int)(((unsigned)acc[a][b][r] << 6) + (unsigned)cj[r]);
+                    if (SECOND) ts[b] = med3_i32(tb[b], nkey, ts[b]);
+                    tb[b] = max(tb[b], nkey);
+#else
                     const int key = mad_i24(acc[a][b][r], -64, cj[r]);
                     if (SECOND) ts[b] = med3_i32(tb[b], key, ts[b]);
                     tb[b] = min(tb[b], key);
+#endif
                 }
         }
+#if PANO_I8_DBL
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            tb[b] = -tb[b];
+            ts[b] = -ts[b];
+        }
+#endif
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             const int d1 = tb[b] >> 5, idx = tb[b] & 31;   // arithmetic shift: floor(key / 32)
@@ -786,17 +809,8 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
     // after it (the same number of barriers; the accumulators wait across it), so one wave's
     // epilogue runs beside its partner's MFMAs.  C32 is triple-buffered: a late epilogue of
     // tile t runs while tile t + 2 is staged.
-    const bool lag = PANO_I8_STAGGER && wj == 1;
-#if PANO_I8_PRIO
-    if (wj == 1) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two waves per SIMD, item 4
-#endif
-    int jt = blockIdx.x, cur = 0, c3 = 0;
-    fetch(jt);
-    store(0, 0);
-    if (jt + n_split < n_jt) fetch(jt + n_split);
-    __syncthreads();                // tile jt complete in buffer cur
-    for (; jt < n_jt; jt += n_split, cur ^= 1, c3 = c3 == 2 ? 0 : c3 + 1) {
-        const unsigned char *Bs = Bs2[cur];
+    // the 16 MFMAs of one candidate tile (buffer Bs) into the accumulator set A
+    auto mma = [&](i32x16 (&A)[2][2], const unsigned char *Bs) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             i32x4 fj[2], fq[2];
@@ -809,18 +823,72 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fj[a], fq[b],
-                                                                      k == 0 ? i32x16{} : acc[a][b], 0, 0, 0);
+                    A[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fj[a], fq[b], k == 0 ? i32x16{} : A[a][b], 0, 0, 0);
         }
+    };
+#if PANO_I8_DBL
+    // Two accumulator sets per wave: tile i's epilogue (VALU) is scheduled between the MFMAs
+    // of tile i + 1 in the same wave (sched_group_barrier: 1 MFMA, 6 VALU), instead of after
+    // them behind a dependency on the last MFMA.  Tile i of this workgroup sits in Bs2[i & 1]
+    // and its C32 in Cs2[i % 3]; tile i + 2 is stored into tile i's buffer during step i (every
+    // wave read tile i before the previous step's barrier) and fetched a step before that.
+    i32x16 acc2[2][2];
+    int jt = blockIdx.x, ti = 0;
+    fetch(jt);
+    store(0, 0);
+    if (jt + n_split < n_jt) {
+        fetch(jt + n_split);
+        store(1, 1);
+        if (jt + 2 * n_split < n_jt) fetch(jt + 2 * n_split);
+    }
+    __syncthreads();
+    mma(acc, Bs2[0]);
+    auto step = [&](i32x16 (&X)[2][2], i32x16 (&Y)[2][2]) -> bool {
+        const bool more = jt + n_split < n_jt;
+        // tile i + 1's MFMAs (past the last tile: the stale buffer, results unused) with tile
+        // i's epilogue interleaved
+        mma(Y, Bs2[(ti + 1) & 1]);
+        epilogue(X, Cs2[ti % 3], jt);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        }
+        if (jt + 2 * n_split < n_jt) {
+            store(ti & 1, (ti + 2) % 3);
+            if (jt + 3 * n_split < n_jt) fetch(jt + 3 * n_split);
+        }
+        __syncthreads();
+        jt += n_split;
+        ++ti;
+        return more;
+    };
+    for (;;) {
+        if (!step(acc, acc2)) break;
+        if (!step(acc2, acc)) break;
+    }
+#else
+    const bool lag = PANO_I8_STAGGER && wj == 1;
+#if PANO_I8_PRIO
+    if (wj == 1) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two waves per SIMD, item 4
+#endif
+    int jt = blockIdx.x, cur = 0, c3 = 0;
+    fetch(jt);
+    store(0, 0);
+    if (jt + n_split < n_jt) fetch(jt + n_split);
+    __syncthreads();                // tile jt complete in buffer cur
+    for (; jt < n_jt; jt += n_split, cur ^= 1, c3 = c3 == 2 ? 0 : c3 + 1) {
+        mma(acc, Bs2[cur]);
         if (jt + n_split < n_jt) {
             store(cur ^ 1, c3 == 2 ? 0 : c3 + 1);
             if (jt + 2 * n_split < n_jt) fetch(jt + 2 * n_split);
         }
         // past this barrier: tile jt + n_split complete in cur ^ 1, every wave done with cur
         if (lag) __syncthreads();
-        epilogue(Cs2[c3], jt);
+        epilogue(acc, Cs2[c3], jt);
         if (!lag) __syncthreads();
     }
+#endif
     auto imerge = [](int &b, int &j, int &s, int b2, int j2, int s2) {
         if (b2 < b || (b2 == b && j2 < j)) {
             s = min(s2, b);
