@@ -910,6 +910,29 @@ def test_descriptor_register_budgets_identical(gpu, parrington, monkeypatch):
         assert a.tobytes() == b.tobytes()
 
 
+def test_raw_order_descriptors_identical(gpu, parrington, monkeypatch):
+    """PANO_DESC_RAW=1 (descriptors of the raw keypoints beside the side-stream sort, rows
+    permuted to sorted order by emit_keypoints): the same keypoints, descriptor bytes and
+    panorama bytes, eager and graph-replayed."""
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    _, frames, focals, margin = parrington
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PANO_DESC_RAW", mode)
+        st = Stitcher("sift")
+        dev = st.upload(frames)
+        cyl, _ = st.cylindrical(dev, focals)
+        k, d, c = st.features(cyl)
+        cnt = c.cpu().numpy()
+        kh, dh = k.cpu().numpy(), d.cpu().numpy()
+        pano = [st.run(dev, focals, margin=margin, graph=g).panorama.cpu().numpy() for g in (False, True, True)]
+        res[mode] = (cnt, *[kh[i, :cnt[i]] for i in range(len(cnt))], *[dh[i, :cnt[i]] for i in range(len(cnt))],
+                     *pano)
+        st.release_graphs()
+    for a, b in zip(res["0"], res["1"]):
+        assert a.tobytes() == b.tobytes()
+
+
 def test_early_extrema_identical(gpu, parrington, monkeypatch):
     """PANO_EARLY_EXTREMA=1 (each large octave's extrema scan on a third stream right after its
     blur, joined before localize): the same keypoints, descriptors and panorama bytes, eager

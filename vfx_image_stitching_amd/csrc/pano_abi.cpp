@@ -125,9 +125,11 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     for (hipEvent_t e : ctx->ev_lvl)
         if (e) (void)hipEventDestroy(e);
     if (ctx->ev_lvl_join) (void)hipEventDestroy(ctx->ev_lvl_join);
+    if (ctx->ev_sort_fork) (void)hipEventDestroy(ctx->ev_sort_fork);
+    if (ctx->ev_sort_join) (void)hipEventDestroy(ctx->ev_sort_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
-                    ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->octs_sync, ctx->match_sync, ctx->sel_sync};
+                    ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->octs_sync, ctx->match_sync, ctx->sel_sync, ctx->descraw};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->jscratch) (void)hipFree(ctx->jscratch);

@@ -121,6 +121,9 @@ struct pano_ctx {
     // second side stream: levels nl-2.. of an octave (PANO_OCT_FORK) beside the next octave's
     // first levels, which need only level nl-3; joined before anything reads them
     hipStream_t lvl_side = nullptr;
+    // the keypoint sort beside the raw-order descriptors (PANO_DESC_RAW): fork / join on `side`
+    hipEvent_t ev_sort_fork = nullptr, ev_sort_join = nullptr;
+    uint8_t *descraw = nullptr; size_t descraw_bytes = 0;   // raw-order descriptors + norms
     hipEvent_t ev_lvl[PANO_MAX_OCTAVES] = {};
     hipEvent_t ev_lvl_join = nullptr;
     // third stream: the extrema scan of an octave launched right after its blur (early

@@ -1030,7 +1030,10 @@ emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cn
                const uint32_t *__restrict__ sorted, pano_kp *__restrict__ out, int cap,
                int32_t *__restrict__ counts, int32_t *__restrict__ err,
                const int32_t *__restrict__ ext_cnt, int ext_cap,
-               const int32_t *__restrict__ cand_cnt, int cand_cap) {
+               const int32_t *__restrict__ cand_cnt, int cand_cap,
+               const uint8_t *__restrict__ desc_raw = nullptr, const int32_t *__restrict__ norm_raw = nullptr,
+               uint8_t *__restrict__ desc_out = nullptr, int32_t *__restrict__ norm_out = nullptr,
+               int32_t *__restrict__ map = nullptr) {
     __shared__ int32_t wsum[kSortThreads / 64];
     __shared__ int32_t total;
     const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1086,6 +1089,7 @@ emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cn
                 q.response = r[k].response;
                 q.octave = (r[k].octave & ~255) | ((r[k].octave - 1) & 255);
                 out[(size_t)f * cap + pos] = q;
+                if (desc_raw) map[(size_t)f * raw_cap + pos] = (int32_t)v[k];
             }
             ++pos;
         }
@@ -1094,6 +1098,19 @@ emit_keypoints(const RawKp *__restrict__ raw, const int32_t *__restrict__ raw_cn
     if (tid == 0) {
         counts[f] = total;                       // the true count, even above cap
         if (total > cap) err[0] = PANO_E_OVERFLOW;   // keypoints past cap were dropped
+    }
+    if (desc_raw) {
+        // descriptors computed in raw order (descriptor_wave<.., RAW>): rows to sorted order,
+        // 8 lanes x 16 bytes per row
+        const int m = min(total, cap);
+        const int32_t *mp = map + (size_t)f * raw_cap;
+        for (int e = tid; e < m * 8; e += kSortThreads) {
+            const int kq = e >> 3, part = e & 7;
+            const int src = mp[kq];
+            const uint4 v = *(const uint4 *)(desc_raw + ((size_t)f * raw_cap + src) * PANO_DESC_DIM + 16 * part);
+            *(uint4 *)(desc_out + ((size_t)f * cap + kq) * PANO_DESC_DIM + 16 * part) = v;
+            if (part == 0) norm_out[(size_t)f * cap + kq] = norm_raw[(size_t)f * raw_cap + src];
+        }
     }
 }
 
@@ -1297,12 +1314,16 @@ static int desc_occ(long long) {
     return 4;
 }
 
-template <bool OUT_U8, int OCC>
+// RAW: the keypoints are orientation's raw records (RawKp [n][cap], counts strided by
+// kCntStride), converted on load exactly as emit_keypoints converts them; the descriptors go
+// to raw order and emit_keypoints permutes them (the sort runs beside this kernel).
+template <bool OUT_U8, int OCC, bool RAW = false>
 __global__ void __launch_bounds__(64 * kDescWaves, OCC)
 descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 const int32_t *__restrict__ counts, int n_frames, int cap, int32_t *__restrict__ work,
                 float *__restrict__ desc, uint8_t *__restrict__ desc_u8, int32_t *__restrict__ norms,
-                const int32_t *__restrict__ order) {
+                const int32_t *__restrict__ order, const RawKp *__restrict__ rawk = nullptr) {
+    constexpr int cstride = RAW ? kCntStride : 1;
     __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHistStride];
     __shared__ int col_lo[kDescWaves][kDescCols / kDescSS], col_pre[kDescWaves][kDescCols / kDescSS + 1];   // per super-strip
     __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
@@ -1319,7 +1340,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     // a window's pyramid rows are fetched into one XCD's L2, not eight
     int total = 0;
     for (int f0 = 0; f0 < n_frames; f0 += 64) {
-        int c = f0 + lane < n_frames ? counts[f0 + lane] : 0;
+        int c = f0 + lane < n_frames ? counts[(f0 + lane) * cstride] : 0;
         c = c < 0 ? 0 : (c < cap ? c : cap);
 #pragma unroll
         for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
@@ -1334,7 +1355,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     (void)nx;
     int f = 0, k = 0;
     FrameIndex fi;
-    fi.init(counts, 1, n_frames, cap);
+    fi.init(counts, cstride, n_frames, cap);
     int claim = 0;
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
@@ -1343,10 +1364,22 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         if (gk >= hi_k) break;
         if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
         if (fi.regs) fi.locate(gk, f, k);
-        else if (!locate_keypoint(counts, n_frames, cap, gk, f, k)) break;
+        else if (RAW ? !locate_strided(counts, n_frames, cap, gk, f, k) : !locate_keypoint(counts, n_frames, cap, gk, f, k))
+            break;
         if (order) k = order[(size_t)f * cap + k];     // locality order (desc_order)
         for (int i = lane; i < kDescCopies * kHistStride; i += 64) h0[i] = 0ull;
-        const pano_kp kp = kps[(size_t)f * cap + k];
+        pano_kp kp;
+        if constexpr (RAW) {                           // emit_keypoints' conversion, exactly
+            const RawKp r = rawk[(size_t)f * cap + k];
+            kp.x = r.x * 0.5f;
+            kp.y = r.y * 0.5f;
+            kp.size = r.size * 0.5f;
+            kp.angle = r.angle;
+            kp.response = r.response;
+            kp.octave = (r.octave & ~255) | ((r.octave - 1) & 255);
+        } else {
+            kp = kps[(size_t)f * cap + k];
+        }
         int oct = kp.octave & 255;
         if (oct >= 128) oct |= -128;
         const int lyr = (kp.octave >> 8) & 255;
@@ -1914,7 +1947,7 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
 namespace {
 int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &pa, const pano_kp *kps,
                        const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
-                       int32_t *norms);
+                       int32_t *norms, const RawKp *rawk = nullptr);
 
 // Scratch of the keypoint stage (per-frame capacities scaled with the pyramid, see kExtMin)
 // and the counter block: [err] [cand f] [raw f] [ext f] [descriptor, orientation work queues
@@ -2062,7 +2095,7 @@ int sift_early_extrema(pano_ctx *ctx, const pano_sift_params *p, int o) {
 namespace {
 int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &pa, const pano_kp *kps,
                        const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
-                       int32_t *norms);
+                       int32_t *norms, const RawKp *rawk);
 
 // raw_out != NULL: find_scale_space_extrema only (stops after the orientations and writes the
 // raw keypoints in scan order to raw_out [n][cap]; kps / desc unused)
@@ -2205,6 +2238,56 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         PANO_LAUNCH_CHECK(ctx, "raw_scan_order");
         return PANO_OK;
     }
+    // PANO_DESC_RAW=1 (read per call; u8 descriptors): the descriptors of the raw keypoints
+    // in orientation's order, with the sort (bucket_build, bucket_rank) on the side stream
+    // beside them; emit_keypoints then writes the kept keypoints AND their descriptor rows in
+    // sorted order.  A descriptor is a function of its keypoint alone, so the bytes are the
+    // sorted-order kernel's; duplicates (dropped by emit) cost a descriptor each.  Measured on
+    // MI355X (graph-replayed parrington): bit-identical but 0.997-1.002 against
+    // 0.986 ms -- the side-stream sort is starved by the persistent descriptor grid (bucket_rank
+    // 206 us beside it), the fork and join cost ~9 us each in the replayed graph, and the
+    // per-frame row copy makes emit 26 us instead of 8.5.  Off by default.
+    const char *dr_env = getenv("PANO_DESC_RAW");
+    const bool desc_raw = desc_u8 && norms && dr_env && atoi(dr_env) != 0;
+    if (desc_raw) {
+        dim3 grid(n, (unsigned)((raw_cap + 255) / 256));
+        if (nb > kSortMaxBuckets) return pano_fail(ctx, PANO_E_UNSUPPORTED, "frame too wide for the keypoint sort");
+        const size_t dbytes = per * PANO_DESC_DIM, nbytes = per * sizeof(int32_t);
+        rc = pano_grow(ctx, (void **)&ctx->descraw, &ctx->descraw_bytes, dbytes + nbytes);
+        if (rc) return rc;
+        uint8_t *draw = ctx->descraw;
+        int32_t *nraw = (int32_t *)(ctx->descraw + dbytes);
+        if (!ctx->side) PANO_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        if (!ctx->ev_sort_fork) {
+            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sort_fork, hipEventDisableTiming));
+            PANO_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sort_join, hipEventDisableTiming));
+        }
+        PANO_HIP(ctx, hipEventRecord(ctx->ev_sort_fork, ctx->stream));
+        PANO_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sort_fork, 0));
+        {
+            PanoProf prof_(ctx, PK_SORT, ctx->side);
+            bucket_build<<<n, kSortThreads, 0, ctx->side>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, bslot, mem);
+        }
+        PANO_LAUNCH_CHECK(ctx, "bucket_build");
+        {
+            PanoProf prof_(ctx, PK_SORT, ctx->side);
+            bucket_rank<<<grid, 256, 0, ctx->side>>>(ctx->raw, raw_cnt, (int)raw_cap, nb, bstart, mem, ctx->sorted);
+        }
+        PANO_LAUNCH_CHECK(ctx, "bucket_rank");
+        PANO_HIP(ctx, hipEventRecord(ctx->ev_sort_join, ctx->side));
+        rc = launch_descriptors(ctx, p, pa, nullptr, raw_cnt, (int)raw_cap, desc_work, nullptr, draw, nraw, ctx->raw);
+        if (rc) return rc;
+        PANO_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_sort_join, 0));
+        {
+            PanoProf prof_(ctx, PK_SORT);
+            // bslot (bucket_build's scratch) holds emit's position -> raw index map
+            emit_keypoints<<<n, kSortThreads, 0, ctx->stream>>>(ctx->raw, raw_cnt, (int)raw_cap, ctx->sorted, kps, cap,
+                                                                counts, err, ext_cnt, (int)ext_cap, cand_cnt,
+                                                                (int)cand_cap, draw, nraw, desc_u8, norms, bslot);
+        }
+        PANO_LAUNCH_CHECK(ctx, "emit_keypoints");
+        return PANO_OK;
+    }
     {
         dim3 grid(n, (unsigned)((raw_cap + 255) / 256));       // bucket_rank: (frame, block)
         if (nb > kSortMaxBuckets) return pano_fail(ctx, PANO_E_UNSUPPORTED, "frame too wide for the keypoint sort");
@@ -2235,7 +2318,7 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
 // round would leave the first round's CUs idle).  desc_work: 8 zeroed per-XCD queue counters.
 int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &pa, const pano_kp *kps,
                        const int32_t *counts, int cap, int32_t *desc_work, float *desc, uint8_t *desc_u8,
-                       int32_t *norms) {
+                       int32_t *norms, const RawKp *rawk) {
     const int n = ctx->n;
     DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
     // locality order (PANO_DESC_ORDER=1).  Measured on MI355X: 253 -> 262 us
@@ -2245,7 +2328,7 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
         return e ? atoi(e) != 0 : false;
     }();
     int32_t *order = nullptr;
-    if (use_order) {
+    if (use_order && !rawk) {
         OrderArgs oa{};
         oa.n_oct = pa.n_oct;
         oa.n_lvl = pa.n_lvl;
@@ -2289,7 +2372,10 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
         PanoProf prof_(ctx, PK_DESC);
         auto go = [&](auto occ_c) {
             constexpr int O = decltype(occ_c)::value;
-            if (desc_u8)
+            if (rawk)
+                descriptor_wave<true, O, true><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
+                    pa, dp, nullptr, counts, n, cap, desc_work, nullptr, desc_u8, norms, nullptr, rawk);
+            else if (desc_u8)
                 descriptor_wave<true, O><<<blocks, 64 * kDescWaves, 0, ctx->stream>>>(
                     pa, dp, kps, counts, n, cap, desc_work, nullptr, desc_u8, norms, order);
             else
