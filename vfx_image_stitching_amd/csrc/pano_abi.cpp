@@ -234,6 +234,7 @@ int pano_sift(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     ctx->early_armed = true;
     int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
     ctx->early_armed = false;
+    if (rc != PANO_OK) ctx->kp_zeroed = false;        // no keypoint stage follows
     if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, desc, nullptr, nullptr, cap, counts);
     sift_join_tail(ctx);
     sift_join_x(ctx);
@@ -251,6 +252,7 @@ int pano_sift_u8(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
     ctx->early_armed = true;
     int rc = launch_sift_pyramid(ctx, bgr, n, h, w, &p, /*defer_tail=*/true, /*full=*/false);
     ctx->early_armed = false;
+    if (rc != PANO_OK) ctx->kp_zeroed = false;        // no keypoint stage follows
     if (rc == PANO_OK) rc = launch_sift_keypoints(ctx, &p, kps, nullptr, desc_u8, norms, cap, counts);
     sift_join_tail(ctx);
     sift_join_x(ctx);

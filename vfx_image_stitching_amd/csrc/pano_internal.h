@@ -132,6 +132,7 @@ struct pano_ctx {
     hipEvent_t ev_x_fork = nullptr, ev_x_join = nullptr;
     bool x_pending = false;              // extrema enqueued on `xside`, not yet joined
     bool early_armed = false;            // pano_sift(_u8): the pyramid may start the extrema
+    bool kp_zeroed = false;              // the pyramid's gray_frames zeroed the keypoint counters
     int early_oct = -1;                  // last octave whose extrema went out early (-1: none)
     int o_tail = 0;                      // first octave of the tail
     bool pyr_full = false;               // every Gaussian level materialised (see launch_sift_pyramid)
@@ -211,6 +212,7 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
 // full = true materialises every Gaussian level (stage access, pano_sift_pyramid); the
 // hot path (pano_sift) skips the planes nothing downstream reads: level 0 of octaves > 0 and
 // the top level (only its DoG is used).
+int sift_kp_counters(pano_ctx *ctx, int32_t **p, size_t *words);   // keypoint counter block
 int launch_sift_pyramid(pano_ctx *ctx, const uint8_t *bgr, int n, int h, int w,
                         const pano_sift_params *p, bool defer_tail = false, bool full = true);
 // Pyramid input of the stage functions (sift_impl.py:45-97): exactly one source is set.

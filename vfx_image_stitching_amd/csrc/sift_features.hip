@@ -2064,6 +2064,18 @@ bool early_extrema_enabled() {
 }
 }  // namespace
 
+// The keypoint stage's counter block (allocated / grown here), for the pyramid's first
+// kernel to zero in passing (gray_frames): the separate fill launch sat between the last
+// blur and the extrema scan on the critical path.
+int sift_kp_counters(pano_ctx *ctx, int32_t **p, size_t *words) {
+    KpBufs b;
+    const int rc = kp_bufs(ctx, b);
+    if (rc) return rc;
+    *p = ctx->counters;
+    *words = b.cnt_ints;
+    return PANO_OK;
+}
+
 int sift_early_extrema(pano_ctx *ctx, const pano_sift_params *p, int o) {
     if (!early_extrema_enabled() || o != ctx->early_oct + 1) return PANO_OK;
     if (extrema_min_h() <= 0 || ctx->oct_h[o] < extrema_min_h()) return PANO_OK;
@@ -2115,10 +2127,11 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
     uint64_t *raw_ext = kb.raw_ext;
     int32_t *err = kb.err, *cand_cnt = kb.cand_cnt, *raw_cnt = kb.raw_cnt, *ext_cnt = kb.ext_cnt;
     int32_t *desc_work = kb.desc_work, *ori_work = kb.ori_work;
-    if (early < 0) {
+    if (early < 0 && !ctx->kp_zeroed) {     // else gray_frames zeroed them this call
         rc = launch_fill(ctx, ctx->counters, 0, kb.cnt_ints * sizeof(int32_t));
         if (rc) return rc;
     }
+    ctx->kp_zeroed = false;
 
     LocParams lp;
     lp.thresh = floor(0.5 * p->contrast_threshold / ni * 255);

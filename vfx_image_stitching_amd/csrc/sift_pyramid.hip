@@ -275,8 +275,12 @@ __device__ __forceinline__ void stage_base_interior(const LoadArgs &la, int f, i
 }
 
 // cvtColor(BGR2GRAY) of every frame, 4 pixels per thread (sift_impl.py:27-28).
+// zp / zn: a word block to zero in passing (the keypoint stage's counters, sift_kp_counters)
 __global__ void __launch_bounds__(256)
-gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t npx) {
+gray_frames(const uint8_t *__restrict__ bgr, uint8_t *__restrict__ gray, size_t npx,
+            int32_t *__restrict__ zp = nullptr, int zn = 0) {
+    if (zp && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < zn; i += 256) zp[i] = 0;
     const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (i0 + 4 <= npx) {
         const uint32_t *p = (const uint32_t *)(bgr + i0 * 3);   // 12 bytes, 4-aligned
@@ -2089,6 +2093,7 @@ int sift_reserve_pyramid(pano_ctx *ctx, int n, int h, int w, const pano_sift_par
 // the caller's base size, octave count capped at max_oct).
 int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, int w,
                             const pano_sift_params *p, bool defer_tail, bool full) {
+    ctx->kp_zeroed = false;
     sift_join_tail(ctx);                  // a previous call's tail must finish first
     sift_join_x(ctx);
     ctx->early_oct = -1;
@@ -2146,6 +2151,13 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         cas_taps = tl[l].n == kCasDefTaps[l] && memcmp(tl[l].k, kCasDefK[l], sizeof(float) * tl[l].n) == 0;
     auto cas_ok = [&](int o) { return cas_taps && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= kCasSW; };
     const bool cas_base = src.bgr && !src.base_only && cas_ok(0);
+    // pano_sift(_u8) runs the keypoint stage next: its counters are zeroed by gray_frames
+    int32_t *zp = nullptr;
+    size_t zn = 0;
+    if (ctx->early_armed && src.bgr && !src.base_only) {
+        rc = sift_kp_counters(ctx, &zp, &zn);
+        if (rc) return rc;
+    }
     if (src.base) {
         // generate_gaussian_images(base, ...): the caller's base is level 0 of octave 0
         PANO_HIP(ctx, hipMemcpyAsync(G + ctx->gauss_off[0][0], src.base,
@@ -2167,9 +2179,10 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         const unsigned blocks = (unsigned)((npx + 1023) / 1024);
         {
             PanoProf prof_(ctx, PK_BLUR);
-            gray_frames<<<blocks, 256, 0, ctx->stream>>>(src.bgr, ctx->gray, npx);
+            gray_frames<<<blocks, 256, 0, ctx->stream>>>(src.bgr, ctx->gray, npx, zp, (int)zn);
         }
         PANO_LAUNCH_CHECK(ctx, "gray_frames");
+        ctx->kp_zeroed = zp != nullptr;
     } else {
         // gray frames (u8) for the base image
         const size_t npx = (size_t)n * h * w;
@@ -2178,9 +2191,10 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         const unsigned blocks = (unsigned)((npx + 1023) / 1024);
         {
             PanoProf prof_(ctx, PK_BLUR);
-            gray_frames<<<blocks, 256, 0, ctx->stream>>>(src.bgr, ctx->gray, npx);
+            gray_frames<<<blocks, 256, 0, ctx->stream>>>(src.bgr, ctx->gray, npx, zp, (int)zn);
         }
         PANO_LAUNCH_CHECK(ctx, "gray_frames");
+        ctx->kp_zeroed = zp != nullptr;
         LoadArgs la{};
         la.gray = ctx->gray;
         la.sh = h;
