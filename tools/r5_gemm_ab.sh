@@ -1,5 +1,5 @@
 #!/bin/bash
-# dist_i8 at synthetic 1080p per library variant (tools/ab/libpano_<v>.so, "base" = the tree's):
+# dist_i8 / descriptor / orientation / extrema / tail kernel times per library variant (tools/ab/libpano_<v>.so, "base" = the tree's):
 # rocprofv3 kernel stats of a short eager bench, the dist_i8 average per variant.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -11,7 +11,7 @@ for v in ${VARIANTS:-base abl1 abl2 nostag w2}; do
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 for r in rows:
-    if "dist_i8" in r["Name"] or "descriptor_wave" in r["Name"]:
+    if any(k in r["Name"] for k in ("dist_i8", "descriptor_wave", "orientation", "extrema_stream", "blur_tail")):
         print(sys.argv[2], r["Name"][:40], "calls", r["Calls"], "avg_us", round(float(r["AverageNs"]) / 1e3, 1))
 PY
   rm -rf $O/$v

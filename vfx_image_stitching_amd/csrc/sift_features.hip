@@ -675,7 +675,11 @@ __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H,
                     const int e = e0 + 64 * u + lane;
                     const int r = e / P, c = e - (e / P) * P;
                     const int yy = min(max(by + r, 0), H - 1), xx = min(max(bx + c, 0), W - 1);
+#if PANO_ORI_ABL & 4                                  // timing ablation: no patch loads
+                    v[u] = (float)(yy ^ xx);
+#else
                     v[u] = e < P * P ? img[(size_t)yy * W + xx] : 0.0f;
+#endif
                 }
 #pragma unroll
                 for (int u = 0; u < kOriStage; ++u) {
