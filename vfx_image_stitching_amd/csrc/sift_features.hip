@@ -1269,6 +1269,9 @@ static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "str
 #ifndef PANO_DESC_RPI
 #define PANO_DESC_RPI 1               // fixed-point scale folded into the sample weight (fewer VALU)
 #endif
+#ifndef PANO_DESC_UNROLL
+#define PANO_DESC_UNROLL 0            // 1: the walk step unrolled 4x over rotating row buffers
+#endif
 #ifndef PANO_DESC_RING
 #define PANO_DESC_RING 0              // > 0: tap rows prefetched this many steps ahead via LDS-DMA
 #endif
@@ -1732,6 +1735,49 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                     }
                 };
                 strip_consts(sx);
+#if PANO_DESC_UNROLL
+                // the three-row window rotates through four buffers with static roles (the
+                // step unrolled 4x): no register moves per step
+                float XA[WN], XB[WN], XC[WN], XD[WN];
+                win(sx, ys - 1, XA);
+                win(sx, ys, XB);
+                win(sx, ys + 1, XC);
+                int j = t;
+                auto step = [&](float (&Tm)[WN], float (&T0)[WN], float (&Tp)[WN], float (&Nx)[WN]) -> bool {
+                    if (j >= tend) return false;
+                    int sn = sx, yn = ys + 1;
+                    const bool more = j + 1 < tend;
+                    const bool newstrip = more && yn >= yend;
+                    if (newstrip) {
+                        do { ++sn; } while (cpre[sn + 1] == cpre[sn]);
+                        yn = clo[sn];
+                    }
+                    if (more && !newstrip) win(sn, yn + 1, Nx);
+                    const float ysf = (float)ys, ys2 = ysf * ysf;
+#pragma unroll
+                    for (int i = 0; i < kDescSW; ++i)
+                        sample(T0[i + 2] - T0[i], Tm[i + 1] - Tp[i + 1], fmaf(ysf, ar, br[i]),
+                               fmaf(ysf, ac, bc[i]), __builtin_amdgcn_exp2f(kq * (ys2 + xs2[i])));
+                    if (newstrip) {
+                        sx = sn;
+                        yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                        strip_consts(sx);
+                        // the next step's (Tm, T0, Tp) are this step's (T0, Tp, Nx)
+                        win(sn, yn - 1, T0);
+                        win(sn, yn, Tp);
+                        win(sn, yn + 1, Nx);
+                    }
+                    ys = yn;
+                    ++j;
+                    return true;
+                };
+                for (;;) {
+                    if (!step(XA, XB, XC, XD)) break;
+                    if (!step(XB, XC, XD, XA)) break;
+                    if (!step(XC, XD, XA, XB)) break;
+                    if (!step(XD, XA, XB, XC)) break;
+                }
+#else
                 float Tm[WN], T0[WN], Tp[WN];
                 win(sx, ys - 1, Tm);
                 win(sx, ys, T0);
@@ -1783,6 +1829,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                     }
                     ys = yn;
                 }
+#endif
             }
 #endif
         } else {
