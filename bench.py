@@ -11,7 +11,12 @@ cylindrical projection -> SIFT features of every frame -> NN match (exact i8 MFM
 read back with the band head (one host read per rank), every band sent to rank 0 (RCCL P2P
 over xGMI), which assembles the canvas and crops the panorama -- inside the timed step].
 
-N = 1 (default): one stitch of the 18 parrington frames (BASELINE config 3, the headline).
+N = 1 (default): one stitch of the 18 parrington frames (BASELINE config 3, the headline);
+the K timed stitches go through pipeline.StitchPool (--contexts, default 2): stitch i on a
+private libpano context i % 2 with its own stream, so the device overlaps two stitches; every
+stitch completes and is read back, and the last one is checked byte for byte against the
+single-context stitch.  One context's run_sequence and synchronous run() over the same K
+stitches are reported beside (`single_context_ms_per_step`, `run_ms_per_step`).
 N > 1 (default): the north_star's scaling target, the synthetic 144-frame / 143-pair 1080p
 batch with its pairs sharded over the ranks (strong scaling; the line
 carries the committed N = 1 time of the same batch as `strong_n1_reference`), plus the weak
@@ -121,7 +126,7 @@ def blur_f32_flops(st, n_frames):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=None, choices=["parrington", "grail", "synthetic"],
                     help="default: parrington at N = 1 (the headline config); at N > 1 the "
@@ -134,6 +139,9 @@ def parse():
     ap.add_argument("--cap", type=int, default=0, help="keypoint capacity per frame (0 = auto)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch eagerly instead of replaying captured hipGraphs")
+    ap.add_argument("--contexts", type=int, default=2,
+                    help="N = 1 pipelined form: stitches dealt over this many private libpano "
+                         "contexts (pipeline.StitchPool); 1 = one Stitcher's run_sequence")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N=1 graph mode: time one synchronous run() per step instead of "
                          "Stitcher.run_sequence (two stitches in flight)")
@@ -315,10 +323,19 @@ def main():
     # other way round).
     pipelined = world == 1 and args.graph and args.pipeline
     seq_beside = world == 1 and args.graph and not args.pipeline
+    pool = None
     if args.graph:
         step(graph=True)
         if pipelined or seq_beside:
             for _ in st.run_sequence([(dev, focals)] * 3, margin=margin):   # both output slots
+                pass
+        if pipelined and args.contexts > 1:
+            # N = 1: the stitches dealt over private contexts (StitchPool): one stitch's
+            # latency-bound stages overlap another's on the device; every member's graphs are
+            # captured here, before the timed region
+            from vfx_image_stitching_amd.pipeline import StitchPool
+            pool = StitchPool(args.method, contexts=args.contexts, cap=cap, match=args.match)
+            for _ in pool.run_sequence([(dev, focals)] * (4 * args.contexts + 2), margin=margin):
                 pass
         torch.cuda.synchronize()
     else:
@@ -328,7 +345,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if pipelined:
+    pool_pano = None
+    if pool is not None:
+        # the last result's panorama is copied to the host after the timed region (it stays
+        # valid: nothing runs on its member afterwards); the first pageable device -> host copy
+        # of a process pays ~50 ms of HIP staging setup, which is not the stitch's
+        for r in pool.run_sequence([(dev, focals)] * args.steps, margin=margin):
+            pool_pano = r.panorama
+    elif pipelined:
         for _ in st.run_sequence([(dev, focals)] * args.steps, margin=margin):
             pass
     else:
@@ -351,6 +375,15 @@ def main():
                 pass
         torch.cuda.synchronize()
         ms_other = (time.perf_counter() - t1) / args.steps * 1e3
+    ms_single = None
+    if pool is not None:
+        # one context's run_sequence over the same K stitches, for the record (not `value`)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in st.run_sequence([(dev, focals)] * args.steps, margin=margin):
+            pass
+        torch.cuda.synchronize()
+        ms_single = (time.perf_counter() - t1) / args.steps * 1e3
     if args.graph:
         ctx.prof_enable(rk)
         ctx.prof_read(rk)
@@ -455,6 +488,12 @@ def main():
     parity = None
     if world == 1 and args.workload != "synthetic" and len(frames) == 18:
         parity = check_parity(st, dev, focals, margin, args.workload, args.method, args.graph)
+    if pool_pano is not None:
+        # the pool's last timed stitch against the single-context stitch, byte for byte
+        pool_pano = pool_pano.cpu().numpy()
+        ref = st.run(dev, focals, margin=margin, graph=args.graph).panorama.cpu().numpy()
+        same = ref.shape == pool_pano.shape and bool((ref == pool_pano).all())
+        parity = dict(parity or {}, pool_matches_single_context=same)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -477,7 +516,9 @@ def main():
         else f"Mpixels/s stitched ({args.workload}, {args.method})",
         "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-        "timed_form": "run_sequence" if pipelined else "run",
+        "timed_form": (f"StitchPool.run_sequence ({args.contexts} private contexts, items round-robin)"
+                       if pool is not None else "run_sequence" if pipelined else "run"),
+        "single_context_ms_per_step": round(ms_single, 4) if ms_single is not None else None,
         "run_sequence_ms_per_step" if seq_beside else "run_ms_per_step":
             round(ms_other, 4) if ms_other is not None else None,
         "higher_is_better": True,

@@ -67,16 +67,22 @@ def drift_correct(shifts):
 
 
 class Stitcher:
-    """Reusable device state for stitching sequences of equally sized frames."""
+    """Reusable device state for stitching sequences of equally sized frames.
+
+    Stitchers share the device's default libpano context (its scratch: pyramid, keypoints,
+    descriptors, ...), and every call is ordered on the caller's current stream; two Stitchers
+    whose work may overlap on the device (different streams) each need their own context:
+    ``Stitcher(..., ctx=_lib.Context(device))``."""
 
     def __init__(self, method: str = "sift", device: int | None = None, cap: int = 4096,
                  max_points: int = 200, ransac_thr: float = 3.0, desc_thresh: float | None = None,
-                 sift_params: dict | None = None, match: str | None = None, ratio: float = 0.0):
+                 sift_params: dict | None = None, match: str | None = None, ratio: float = 0.0,
+                 ctx=None):
         import os
         import torch
         self.torch = torch
         self.method = method
-        self.ctx = context(device)
+        self.ctx = ctx if ctx is not None else context(device)
         self.device = torch.device("cuda", self.ctx.device)
         self.cap = cap if method == "sift" else max_points
         self.max_points = max_points
@@ -726,3 +732,60 @@ class Stitcher:
                 y0 * canvas.stride(0) + x0 * 3)
         t["total"] = tick() - t0
         return StitchResult(pano, canvas, shifts, best_pairs, recs, (y0, y1, x0, x1), t)
+
+
+class StitchPool:
+    """A sequence of stitches over k Stitchers with PRIVATE libpano contexts (each its own
+    scratch) and streams: stitch i runs on member i % k, so one stitch's latency-bound stages
+    (the small blur octaves, the sort, the post-descriptor chain, the plan) overlap another's
+    bandwidth-bound ones on the device.  Each member keeps its own run_sequence (two stitches
+    in flight, graphs captured on its first items), so up to 2k stitches are in flight; the
+    results come back in item order and are bit-identical to Stitcher.run's.  A yielded result
+    stays valid until the generator is resumed (in fact until its member's next one, k items
+    later).  Measured on MI355X: parrington 0.83 ms per stitch at k = 2 against
+    0.99 with one context; k = 3 and 4 give 0.88.
+
+    ``kw`` are Stitcher's arguments (method, cap, match, ...)."""
+
+    def __init__(self, method: str = "sift", contexts: int = 2, device: int | None = None, **kw):
+        import torch
+        self.torch = torch
+        dev = torch.cuda.current_device() if device is None else device
+        if contexts < 1:
+            raise PanoError(_lib.PANO_E_ARG, "StitchPool needs at least one context")
+        self.members = [Stitcher(method, device=dev, ctx=_lib.Context(dev), **kw) for _ in range(contexts)]
+        self.streams = [torch.cuda.Stream(dev) for _ in range(contexts)]
+        self.device = self.members[0].device
+
+    def upload(self, frames):
+        """Frames to the device (one buffer every member reads)."""
+        return self.members[0].upload(frames)
+
+    def run_sequence(self, items, margin: int = 15):
+        """Generator over StitchResults of items ((frames_dev, focals) pairs) in order."""
+        T = self.torch
+        items = list(items)
+        k = len(self.members)
+        cur = T.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(cur)                   # inputs made on the caller's stream
+        gens = []
+        for m, (st, s) in enumerate(zip(self.members, self.streams)):
+            with T.cuda.stream(s):
+                gens.append(st.run_sequence(items[m::k], margin=margin))
+        try:
+            for i in range(len(items)):
+                m = i % k
+                with T.cuda.stream(self.streams[m]):
+                    r = next(gens[m])
+                yield r
+        finally:
+            for g, s in zip(gens, self.streams):
+                with T.cuda.stream(s):
+                    g.close()
+            for s in self.streams:
+                cur.wait_stream(s)
+
+    def release_graphs(self):
+        for st in self.members:
+            st.release_graphs()
