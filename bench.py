@@ -329,7 +329,9 @@ def main():
         if pipelined or seq_beside:
             for _ in st.run_sequence([(dev, focals)] * 3, margin=margin):   # both output slots
                 pass
-        if pipelined and args.contexts > 1:
+        if pipelined and args.contexts > 1 and n_local <= 32:
+            # (a large batch -- the 144-frame strong form at N = 1 -- keeps one context: each
+            # private context holds its own pyramid, ~70 GB at 144 x 1080p)
             # N = 1: the stitches dealt over private contexts (StitchPool): one stitch's
             # latency-bound stages overlap another's on the device; every member's graphs are
             # captured here, before the timed region
