@@ -2104,6 +2104,18 @@ int launch_extrema_stream(pano_ctx *ctx, const pano_sift_params *p, const XArgs 
     return PANO_OK;
 }
 
+// Fraction of the resident workgroups the persistent orientation / descriptor grids take
+// (PANO_PERSIST_FRAC, default 1): below 1, a stitch overlapping on another context
+// (pipeline.StitchPool) keeps CU slots while they run.
+double persist_frac() {
+    static const double v = [] {
+        const char *e = getenv("PANO_PERSIST_FRAC");
+        const double f = e ? atof(e) : 1.0;
+        return f > 0.05 && f <= 1.0 ? f : 1.0;
+    }();
+    return v;
+}
+
 // PANO_EARLY_EXTREMA=1 (read per call): each large octave's extrema scan goes out on a third
 // stream as soon as its DoG levels exist.  Measured on MI355X (same box): bit-exact
 // but 1.44-1.46 ms per graph-replayed parrington stitch against 1.09 ms, 11.9 against 11.0 ms at
@@ -2283,8 +2295,8 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
             ori_resident = per_cu * cus;
         }
         const size_t slots = ((size_t)n * cand_cap + 3) / 4;
-        const unsigned blocks = (unsigned)std::max<size_t>(8, std::min<size_t>((slots + 7) & ~size_t(7),
-                                                                              (size_t)ori_resident & ~size_t(7)));
+        const unsigned blocks = (unsigned)std::max<size_t>(
+            8, std::min<size_t>((slots + 7) & ~size_t(7), (size_t)(ori_resident * persist_frac()) & ~size_t(7)));
         {
             PanoProf prof_(ctx, PK_ORIENT);
             orientation<<<blocks, 256, 0, ctx->stream>>>(pa, op, ctx->cands, cand_cnt, (int)cand_cap, n, ori_work,
@@ -2431,7 +2443,7 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
     }
     const size_t slots = ((size_t)n * cap + kDescWaves - 1) / kDescWaves;
     const unsigned blocks = (unsigned)std::max<size_t>(
-        8, std::min<size_t>((slots + 7) & ~size_t(7), (size_t)res & ~size_t(7)));
+        8, std::min<size_t>((slots + 7) & ~size_t(7), (size_t)(res * persist_frac()) & ~size_t(7)));
     {
         PanoProf prof_(ctx, PK_DESC);
         auto go = [&](auto occ_c) {
