@@ -165,11 +165,12 @@ __device__ __forceinline__ int row_map(double fl, int yd, double inv_den, int xd
 
 // Largest row-major source index landing on destination pixel (xp, yp) by the per-pixel
 // candidate search (cyl_inverse's form; cyl_tile's fallback for very wide column ranges).
-__device__ long search_best(int2 cr, const double2 *__restrict__ cd, int xp, int yp, int h, int w, double fl) {
+template <typename CD>
+__device__ long search_best(int2 cr, CD cd, int xp, int yp, int h, int w, double fl) {
     const int cy = h / 2, k = yp - cy;
     long best = -1;
     for (int x = cr.x; x <= cr.y; ++x) {
-        const double2 ds = cd[x];
+        const double2 ds = cd(x);
         const double s = ds.y;
         const int r1 = (int)ceil((k + 0.5) * s) + 1, r0 = (int)floor((k - 0.5) * s) - 1;
         for (int yd = r1; yd >= r0; --yd) {
@@ -193,29 +194,89 @@ __device__ long search_best(int2 cr, const double2 *__restrict__ cd, int xp, int
 // column with the f64 map (cyl_inverse: ~half of its 29 us at parrington was that search).
 // The winner is still the largest row-major source index: the reference's last writer.
 constexpr int kTX = 64, kTY = 32, kTC = 128, kRMax = 64;
+
+// the row map's column constants of source column x: (1 / den, den / f), den = sqrt(xd^2 + f^2)
+__device__ __forceinline__ double2 col_consts(double fl, int x, int cx) {
+    const int k = x - cx;
+    const double den = sqrt((double)k * (double)k + fl * fl);
+    return make_double2(1.0 / den, den / fl);
+}
+
+// FUSED (the default): the tile derives its destination columns' source runs and the window's
+// column constants itself -- col_map at every window column (and one either side), a run's
+// ends where the map changes -- instead of reading cyl_columns_run's tables: one launch per
+// frame batch instead of two.  Where the window cannot hold a tile column's whole run (strong
+// distortion) each run comes from two binary searches over the monotone map.  The per-column
+// non-zero flag is the OR over the column strip's row tiles: each tile ORs its columns into a
+// u32 flag (device atomics), counts itself in on the strip, and the strip's last tile reads the
+// flags back (sc1 loads), writes colnz and re-zeroes flags and counter for the next launch.
+struct CylSync {
+    uint32_t *flags;                     // [n][w]
+    int32_t *cnt;                        // [n][strips]
+};
+
+template <bool FUSED>
 __global__ void __launch_bounds__(256)
 cyl_tile(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 *__restrict__ cols,
-         const double2 *__restrict__ colden, uint8_t *__restrict__ colnz, int h, int w, FocalArg focal) {
+         const double2 *__restrict__ colden, uint8_t *__restrict__ colnz, int h, int w, FocalArg focal,
+         CylSync sync) {
     __shared__ int T[kTY][kTC];
     __shared__ int2 cr[kTX];
     __shared__ int ylo_s[kTC], nrow_s[kTC];
-    __shared__ int xs_s[2], fb_s;
+    __shared__ int xs_s[2], fb_s, cov_s, last_s;
     __shared__ unsigned char nz_s[4][kTX];
     __shared__ double2 cd_s[kTC];
+    __shared__ int m_s[kTC + 2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int f = blockIdx.z, xp0 = blockIdx.x * kTX, yp0 = blockIdx.y * kTY;
     const double fl = focal.f[f];
     const int cx = w / 2, cy = h / 2;
-    const int2 *fc = cols + (size_t)f * w;
-    const double2 *cd = colden + (size_t)f * w;
+    const int2 *fc = FUSED ? nullptr : cols + (size_t)f * w;
+    const double2 *cd = FUSED ? nullptr : colden + (size_t)f * w;
     // the source columns' constants for a window from the inverse column map of the tile's
     // first column (f tan((x' - 1/2) / f), as cyl_columns bounds it), loaded together with the
     // tile's column ranges: one global round trip instead of two
     const double lim = 1.5707963267948966 - 1e-12;
     const double ta = fmax(fmin((xp0 - cx - 0.5) / fl, lim), -lim);
     const int wx0 = max((int)fmin(fmax(floor(fl * tan(ta)), -(double)cx - 2.0), (double)w) + cx - 2, 0);
-    if (tid < kTX) cr[tid] = xp0 + tid < w ? fc[xp0 + tid] : make_int2(1, 0);
-    else if (tid - kTX < kTC && wx0 + tid - kTX < w) cd_s[tid - kTX] = cd[wx0 + tid - kTX];
+    if constexpr (FUSED) {
+        // m_s[t] = col_map(window column t - 1), out-of-frame columns as +-infinity
+        if (tid < kTC + 2) {
+            const int x = wx0 - 1 + tid;
+            m_s[tid] = x < 0 ? -0x40000000 : (x >= w ? 0x40000000 : col_map(fl, x, cx));
+        }
+        if (tid >= kTC + 2 && tid < kTC + 2 + kTX) cr[tid - kTC - 2] = make_int2(1, 0);
+        if (tid < kTC && wx0 + tid < w) cd_s[tid] = col_consts(fl, wx0 + tid, cx);
+        if (tid == 0) cov_s = 1;
+        __syncthreads();
+        // runs of the tile's columns inside the window; covered iff the map leaves the tile's
+        // column range on both sides of the window (or the window reaches the frame's edge)
+        if (tid == 0) {
+            const int lo_ok = wx0 == 0 || m_s[0] < xp0;
+            const int hi_ok = wx0 + kTC >= w || m_s[kTC + 1] >= min(xp0 + kTX, w);
+            cov_s = lo_ok && hi_ok;
+        }
+        if (tid >= 1 && tid <= kTC) {
+            const int x = wx0 - 1 + tid, a = m_s[tid];
+            if (x < w && a >= xp0 && a < xp0 + kTX && a < w) {
+                if (m_s[tid - 1] != a) cr[a - xp0].x = x;
+                if (m_s[tid + 1] != a) cr[a - xp0].y = x;
+            }
+        }
+        __syncthreads();
+        if (!cov_s && tid < kTX && xp0 + tid < w) {
+            // the run of column xp0 + tid by two binary searches of the monotone map
+            const int a = xp0 + tid;
+            int lo = 0, hi = w;                      // first x with map(x) >= a
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (col_map(fl, mid, cx) >= a) hi = mid; else lo = mid + 1; }
+            int lo2 = lo, hi2 = w;                   // first x with map(x) > a
+            while (lo2 < hi2) { const int mid = (lo2 + hi2) >> 1; if (col_map(fl, mid, cx) > a) hi2 = mid; else lo2 = mid + 1; }
+            cr[tid] = lo < lo2 ? make_int2(lo, lo2 - 1) : make_int2(1, 0);
+        }
+    } else {
+        if (tid < kTX) cr[tid] = xp0 + tid < w ? fc[xp0 + tid] : make_int2(1, 0);
+        else if (tid - kTX < kTC && wx0 + tid - kTX < w) cd_s[tid - kTX] = cd[wx0 + tid - kTX];
+    }
     for (int i = tid; i < kTY * kTC; i += 256) (&T[0][0])[i] = -1;
     if (tid == 0) fb_s = 0;
     __syncthreads();
@@ -233,7 +294,7 @@ cyl_tile(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 
     const int xs0 = xs_s[0], ncols = xs_s[1] >= xs0 ? xs_s[1] - xs0 + 1 : 0;
     // source column x's constants: from the LDS window when it holds them
     const bool in_win = xs0 >= wx0 && xs0 + ncols <= wx0 + kTC && xs0 + ncols <= w;
-    auto cdx = [&](int x) { return in_win ? cd_s[x - wx0] : cd[x]; };
+    auto cdx = [&](int x) { return in_win ? cd_s[x - wx0] : (FUSED ? col_consts(fl, x, cx) : cd[x]); };
     if (ncols > kTC) {
         if (tid == 0) fb_s = 1;
     } else {
@@ -300,8 +361,10 @@ cyl_tile(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 
                         const long li = (long)y * w + x;
                         if (y >= 0 && li > b) b = li;
                     }
+                } else if constexpr (FUSED) {
+                    b = search_best(c, [&](int x) { return col_consts(fl, x, cx); }, xp, yp, h, w, fl);
                 } else {
-                    b = search_best(c, cd, xp, yp, h, w, fl);
+                    b = search_best(c, [&](int x) { return cd[x]; }, xp, yp, h, w, fl);
                 }
             }
             best[j] = (int)b;                        // h * w < 2^31 (launch_cylindrical)
@@ -356,7 +419,29 @@ cyl_tile(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 
     for (int j = 0; j < 4; ++j)
         if (nzq[j]) nzc[4 * q + j] = 1;                          // same value from every writer
     __syncthreads();
-    if (colnz && tid < kTX && xp0 + tid < w && nzc[tid]) colnz[(size_t)f * w + xp0 + tid] = 1;
+    if constexpr (FUSED) {
+        if (!colnz) return;
+        typedef __attribute__((address_space(1))) uint32_t g_u32;
+        typedef __attribute__((address_space(1))) int g_i32;
+        uint32_t *fl_f = sync.flags + (size_t)f * w;
+        if (tid < kTX && xp0 + tid < w && nzc[tid]) atomicOr(fl_f + xp0 + tid, 1u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its ORs performed
+        __syncthreads();
+        int32_t *cnt = sync.cnt + (size_t)f * gridDim.x + blockIdx.x;
+        if (tid == 0)
+            last_s = __hip_atomic_fetch_add((g_i32 *)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (int)gridDim.y - 1;
+        __syncthreads();
+        if (!last_s) return;
+        if (tid < kTX && xp0 + tid < w) {
+            const uint32_t v = __hip_atomic_load((g_u32 *)(fl_f + xp0 + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            colnz[(size_t)f * w + xp0 + tid] = v ? 1 : 0;
+            __hip_atomic_store((g_u32 *)(fl_f + xp0 + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) __hip_atomic_store((g_i32 *)cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (colnz && tid < kTX && xp0 + tid < w && nzc[tid]) colnz[(size_t)f * w + xp0 + tid] = 1;
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -422,6 +507,43 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
     if ((long long)h * w >= (1LL << 31)) return pano_fail(ctx, PANO_E_ARG, "frame too large");
     const size_t plane = (size_t)h * w;
     static const bool scatter_form = getenv("PANO_CYL_SCATTER") != nullptr;
+    // the fused tile (default; PANO_CYL_TWO=1: cyl_columns_run + cyl_tile, read per call)
+    const char *two_env = getenv("PANO_CYL_TWO");
+    const bool fused = !scatter_form && !(two_env && atoi(two_env) != 0) && !getenv("PANO_CYL_PIXEL") &&
+                       !getenv("PANO_CYL_COLSEARCH");
+    if (fused) {
+        const int strips = (w + kTX - 1) / kTX;
+        const size_t need = (size_t)n * w * sizeof(uint32_t) + (size_t)n * strips * sizeof(int32_t);
+        if (need > ctx->cyl_sync_bytes) {
+            if (ctx->capturing) return pano_fail(ctx, PANO_E_UNSUPPORTED, "cylindrical counters grown inside a graph capture");
+            if (ctx->cyl_sync) {
+                PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+                (void)hipFree(ctx->cyl_sync);
+                ctx->cyl_sync = nullptr;
+                ctx->cyl_sync_bytes = 0;
+                ++ctx->generation;
+            }
+            PANO_HIP(ctx, hipMalloc((void **)&ctx->cyl_sync, need));
+            PANO_HIP(ctx, hipMemset(ctx->cyl_sync, 0, need));      // each launch re-zeroes
+            ctx->cyl_sync_bytes = need;
+        }
+        uint32_t *flags = (uint32_t *)ctx->cyl_sync;
+        int32_t *cnt = (int32_t *)(flags + (size_t)n * w);
+        for (int f0 = 0; f0 < n; f0 += kFocalChunk) {
+            const int nf = n - f0 < kFocalChunk ? n - f0 : kFocalChunk;
+            FocalArg fa;
+            for (int i = 0; i < nf; ++i) fa.f[i] = h_focal[f0 + i];
+            CylSync cs{flags + (size_t)f0 * w, cnt + (size_t)f0 * strips};
+            {
+                PanoProf prof_(ctx, PK_CYL_GATHER);
+                cyl_tile<true><<<dim3(strips, (h + kTY - 1) / kTY, nf), 256, 0, ctx->stream>>>(
+                    src + f0 * plane * 3, dst + f0 * plane * 3, nullptr, nullptr,
+                    colnz ? colnz + (size_t)f0 * w : nullptr, h, w, fa, cs);
+            }
+            PANO_LAUNCH_CHECK(ctx, "cyl_tile");
+        }
+        return PANO_OK;
+    }
     if (!scatter_form) {
         int rc = pano_grow(ctx, &ctx->bscratch, &ctx->bscratch_bytes, (size_t)n * w * (sizeof(int2) + sizeof(double2)));
         if (rc) return rc;
@@ -451,9 +573,9 @@ int launch_cylindrical(pano_ctx *ctx, const uint8_t *src, uint8_t *dst, int n, i
                     colnz ? colnz + (size_t)f0 * w : nullptr, h, w, fa);
             } else {
                 PanoProf prof_(ctx, PK_CYL_GATHER);
-                cyl_tile<<<dim3((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, nf), 256, 0, ctx->stream>>>(
+                cyl_tile<false><<<dim3((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, nf), 256, 0, ctx->stream>>>(
                     src + f0 * plane * 3, dst + f0 * plane * 3, cols + (size_t)f0 * w, colden + (size_t)f0 * w,
-                    colnz ? colnz + (size_t)f0 * w : nullptr, h, w, fa);
+                    colnz ? colnz + (size_t)f0 * w : nullptr, h, w, fa, CylSync{});
             }
             PANO_LAUNCH_CHECK(ctx, "cyl_inverse");
         }

@@ -129,7 +129,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->ev_sort_join) (void)hipEventDestroy(ctx->ev_sort_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
-                    ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->octs_sync, ctx->match_sync, ctx->sel_sync, ctx->descraw};
+                    ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->octs_sync, ctx->match_sync, ctx->sel_sync, ctx->descraw, ctx->cyl_sync};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->jscratch) (void)hipFree(ctx->jscratch);

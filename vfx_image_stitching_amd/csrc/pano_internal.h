@@ -92,6 +92,7 @@ struct pano_ctx {
     int32_t *octs_sync = nullptr; size_t octs_sync_bytes = 0;   // blur_octs row counters (zeroed)
     int32_t *match_sync = nullptr; size_t match_sync_bytes = 0; // dist_i8 fold arrival counters (zeroed)
     int32_t *sel_sync = nullptr; size_t sel_sync_bytes = 0;     // pair_votes fold arrival counters (zeroed)
+    void *cyl_sync = nullptr; size_t cyl_sync_bytes = 0;        // cyl_tile column flags + strip counters (zeroed)
     uint8_t *gray = nullptr; size_t gray_bytes = 0;   // u8 gray frames (base blur input)
     int32_t *boxslots = nullptr; size_t boxslots_bytes = 0;   // crop-box partials (kBoxSlots x 4)
     // ---- match / ransac scratch
