@@ -2329,6 +2329,9 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     // 39 against ~28 -- the chain of 11 dependent levels costs one tile's latency each either
     // way, and a resident tile loop (poll, sc1 staging, drain, count) has the longer latency:
     // with no waits at all (PANO_OCTS_ABL=1) the launch still takes 154 us.  So off by default.
+    // Exclusive device only: the tile order is deadlock-free only with every workgroup of the
+    // launch resident, so beside another context's kernels (pipeline.StitchPool) waiting tiles
+    // run into their spin time-out (measured: 60-69 ms per pooled step) and read stale rows.
     const char *octs_env = getenv("PANO_BLUR_OCTS");
     const int octs_a = octs_env ? atoi(octs_env) : 0;
     const bool octs_on = octs_a >= 1 && !chain_on && !cas_taps && pair_mask == 0 && oct_fork < 0 && !tail_main &&
