@@ -89,6 +89,13 @@ typedef struct pano_step {
 int pano_ctx_create(int device, void *hip_stream, pano_ctx **out);
 int pano_ctx_destroy(pano_ctx *ctx);
 int pano_ctx_set_stream(pano_ctx *ctx, void *hip_stream);
+/* Scheduling options of this context (bit set; results identical in every setting).
+ * PANO_CTX_TAIL_MAIN: the small-octave blur tail on the context's own stream instead of a
+ * forked side stream -- fewer cross-stream graph edges, best when other contexts' work fills
+ * the device (pipeline.StitchPool); alone, the side stream hides the tail.
+ * No reference counterpart. */
+#define PANO_CTX_TAIL_MAIN 1
+int pano_ctx_set_flags(pano_ctx *ctx, int flags);
 /* Pre-size scratch for n frames of h x w with cap keypoints per frame (allocates). */
 int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap);
 /* Free every scratch buffer the context grew (after a large batch; the next call re-allocates

@@ -14,6 +14,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+PANO_CTX_TAIL_MAIN = 1        # pano_ctx_set_flags: the blur tail on the context's own stream
 # PANO_LIB: an alternative build of the same ABI (A/B timing of two revisions, tools/ab_build.sh)
 LIB_PATH = os.environ.get("PANO_LIB") or os.path.join(_HERE, "libpano.so")
 
@@ -95,6 +96,7 @@ SIGNATURES = {
     "pano_ctx_create": (_I, [_I, _P, ctypes.POINTER(_P)]),
     "pano_ctx_destroy": (_I, [_P]),
     "pano_ctx_set_stream": (_I, [_P, _P]),
+    "pano_ctx_set_flags": (_I, [_P, _I]),
     "pano_ctx_reserve": (_I, [_P, _I, _I, _I, _I]),
     "pano_sync": (_I, [_P]),
     "pano_ctx_release_scratch": (_I, [_P]),
@@ -219,6 +221,10 @@ class Context:
     def check(self, rc):
         if rc != PANO_OK:
             raise PanoError(rc, (self.lib.pano_last_error(self.h) or b"").decode())
+
+    def set_flags(self, flags: int):
+        """pano_ctx_set_flags: scheduling options of this context (PANO_CTX_*)."""
+        self.check(self.lib.pano_ctx_set_flags(self.h, int(flags)))
 
     def bind_stream(self):
         stream = self._torch.cuda.current_stream(self.device).cuda_stream

@@ -188,6 +188,12 @@ int pano_ctx_set_stream(pano_ctx *ctx, void *stream) {
     return PANO_OK;
 }
 
+int pano_ctx_set_flags(pano_ctx *ctx, int flags) {
+    if (!ctx || (flags & ~PANO_CTX_TAIL_MAIN)) return PANO_E_ARG;
+    ctx->flags_opt = flags;
+    return PANO_OK;
+}
+
 int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap) {
     if (!ctx || n <= 0 || h <= 0 || w <= 0 || cap <= 0) return PANO_E_ARG;
     pano_sift_params p;

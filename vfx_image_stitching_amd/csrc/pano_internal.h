@@ -134,6 +134,7 @@ struct pano_ctx {
     bool x_pending = false;              // extrema enqueued on `xside`, not yet joined
     bool early_armed = false;            // pano_sift(_u8): the pyramid may start the extrema
     bool kp_zeroed = false;              // the pyramid's gray_frames zeroed the keypoint counters
+    int flags_opt = 0;                   // pano_ctx_set_flags (PANO_CTX_*)
     int early_oct = -1;                  // last octave whose extrema went out early (-1: none)
     int o_tail = 0;                      // first octave of the tail
     bool pyr_full = false;               // every Gaussian level materialised (see launch_sift_pyramid)

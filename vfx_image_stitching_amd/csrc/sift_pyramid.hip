@@ -2226,7 +2226,7 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     // PANO_TAIL_MAIN=1 (read per call): the tail on the main stream, no fork in the launch
     // sequence (a captured graph is then one chain)
     const char *tail_main_env = getenv("PANO_TAIL_MAIN");
-    const bool tail_main = tail_main_env && atoi(tail_main_env) != 0;
+    const bool tail_main = (tail_main_env && atoi(tail_main_env) != 0) || (ctx->flags_opt & PANO_CTX_TAIL_MAIN);
     auto fork = [&]() -> int {
         if (tail_main) return PANO_OK;
         if (!ctx->side) {
