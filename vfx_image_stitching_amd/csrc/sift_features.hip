@@ -1206,9 +1206,8 @@ __device__ __forceinline__ float atan2_oct(float y, float x) {
 // gradient taps come from a sliding window of three image rows x (kDescSW + 2) columns: ONE
 // wide load per step serves the strip's kDescSW samples, the next step's load in flight while
 // the current samples are binned, and a group's loads of one step fall in ~one cache line.
-// The kernel is bound by its tap loads missing L1 (every step of a lane is a new image row;
-// a timing ablation with L1-resident taps runs 3x faster): 4 samples per load instead of 1
-// cut it 0.35 -> 0.25 ms at parrington.  Groups are Q steps apart: different cells /
+// 4 samples per load instead of 1 cut it 0.35 -> 0.25 ms at parrington; since then the
+// per-sample binning, not the loads, bounds it (L1-resident taps: -8 %, no LDS: -2 %).  Groups are Q steps apart: different cells /
 // orientations, few same-address LDS atomics.  Each sample is
 // spread trilinearly into the wave's 6 x 6 x 8 histogram (padding bins included: no bounds
 // branches) as 2^22 fixed-point u64 LDS atomics, into one of kDescCopies interleaved copies
@@ -1278,6 +1277,18 @@ static_assert(kDescSW == 1 || kDescSW == 2 || kDescSW == 4 || kDescSW == 8, "str
 #if PANO_DESC_RING
 constexpr int kRing = PANO_DESC_RING;
 #endif
+#ifndef PANO_DESC_ROWS
+#define PANO_DESC_ROWS 0              // 1: row-major walk over (row, strip) items (measured slower)
+#endif
+#ifndef PANO_DESC_COMPACT
+#define PANO_DESC_COMPACT 0           // 1: samples binned from a compaction queue, 64 at a time (measured slower)
+#endif
+constexpr int kDescQ = 128;           // queue entries per wave: <= 63 waiting + 64 appended
+#ifndef PANO_DESC_RLANES
+#define PANO_DESC_RLANES 8            // row walk: consecutive lanes on consecutive items
+#endif
+constexpr int kRowLanes = PANO_DESC_RLANES;
+constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; more: column walk)
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
                                       // 3: every sample's taps from one cached location)
@@ -1333,7 +1344,17 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     constexpr int cstride = RAW ? kCntStride : 1;
     __shared__ unsigned long long hist[kDescWaves][kDescCopies * kHistStride];
     __shared__ int col_lo[kDescWaves][kDescCols / kDescSS], col_pre[kDescWaves][kDescCols / kDescSS + 1];   // per super-strip
-    __shared__ float col_br[kDescWaves][kDescCols], col_bc[kDescWaves][kDescCols];
+    // column constants, 4 padding entries each side (rejecting values) for the row walk's
+    // memory-aligned strips, which can start up to 3 columns before the patch or end after it
+    __shared__ float col_br[kDescWaves][kDescCols + 8], col_bc[kDescWaves][kDescCols + 8];
+#if PANO_DESC_ROWS
+    __shared__ uint16_t row_tbl[kDescWaves][kRowTbl];   // row walk: (patch row, strip) per item
+#endif
+#if PANO_DESC_COMPACT
+    // per-wave ring of candidate samples that passed the bin test (compaction queue)
+    __shared__ float2 cq_g[kDescWaves][kDescQ], cq_b[kDescWaves][kDescQ];
+    __shared__ float cq_w[kDescWaves][kDescQ];
+#endif
 #if PANO_DESC_RING
     __shared__ __attribute__((aligned(16))) float ring[kDescWaves][PANO_DESC_RING][2][64 * 4];   // LDS-DMA tap rows, per wave
 #endif
@@ -1341,7 +1362,12 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     unsigned long long *h0 = hist[wv];
     unsigned long long *h = h0 + (lane & (kDescCopies - 1)) * kHistStride;   // this lane's copy
     int *clo = col_lo[wv], *cpre = col_pre[wv];
-    float *cbr = col_br[wv], *cbc = col_bc[wv];
+    float *cbr = col_br[wv] + 4, *cbc = col_bc[wv] + 4;
+    if (lane < 8) {                      // the padding: never written below, rejects every sample
+        const int c = lane < 4 ? lane - 4 : kDescCols + lane - 4;
+        cbr[c] = 1e30f;
+        cbc[c] = 1e30f;
+    }
     // XCD-aware split (workgroup b runs on XCD b % 8): each XCD takes one contiguous eighth of
     // the keypoints (x-sorted per frame: neighbouring windows), its waves striding over it, so
     // a window's pyramid rows are fetched into one XCD's L2, not eight
@@ -1425,8 +1451,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         // rbin = ys (cos / hw) + (xs sin / hw + 1.5), cbin = ys (-sin / hw) + (xs cos / hw + 1.5)
         const double sr = sin_a * inv_hw, cr = cos_a * inv_hw;
         const float ar = (float)cr, ac = (float)-sr;
-        auto sample = [&](float gx, float gy, float rbin, float cbin, float w) {
-            if (!(rbin > -1.0f && rbin < 4.0f && cbin > -1.0f && cbin < 4.0f)) return;
+        auto sample_in = [&](float gx, float gy, float rbin, float cbin, float w) {
             const float mag = __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
             float ob = atan2_oct(gy, gx) - a8;               // (-12, 4]
             ob = ob < 0.0f ? ob + 8.0f : ob;
@@ -1486,6 +1511,27 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             abl_sink += fix(v00 * nof) + fix(v00 * of) + fix(v01 * nof) + fix(v01 * of) + fix(v10 * nof) +
                         fix(v10 * of) + fix(v11 * nof) + fix(v11 * of) + (unsigned long long)(base + o0 + o1);
 #endif
+        };
+        auto sample = [&](float gx, float gy, float rbin, float cbin, float w) {
+            if (!(rbin > -1.0f && rbin < 4.0f && cbin > -1.0f && cbin < 4.0f)) return;
+            sample_in(gx, gy, rbin, cbin, w);
+        };
+        // very large patches (non-default parameters), or more row-walk items than its table:
+        // every sample of the square
+        auto square_walk = [&]() {
+            const int S = side * side;
+            for (int j = lane; j < S; j += 64) {
+                const int xi = j / side, yi = j - (j / side) * side;
+                const int xs = xi - half, ys = yi - half;
+                const int rr = py + ys, cc = px + xs;
+                if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
+                const double rq = ((double)xs * sin_a + (double)ys * cos_a) * inv_hw;
+                const double cq = ((double)xs * cos_a - (double)ys * sin_a) * inv_hw;
+                if (!(fabs(rq) < 2.5 + 1e-6 && fabs(cq) < 2.5 + 1e-6)) continue;
+                const float *q = img + (size_t)rr * cols + cc;
+                sample(q[1] - q[-1], q[-cols] - q[cols], (float)rq + 1.5f, (float)cq + 1.5f,
+                       (float)exp(-0.125 * (rq * rq + cq * cq)));
+            }
         };
         if (side <= kDescCols) {
             const double lim = 2.5 * hwd * (1.0 + 1e-9) + 1e-9;   // |rot| / hw < 2.5 with slack
@@ -1555,6 +1601,131 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if PANO_DESC_ROWS
+            // Row walk.  The column walk below hands each lane group a run of one strip's rows:
+            // the 64 lanes of a load touch 64 rows, and the four strips that share a 128-byte
+            // line reach it at different times, each fetch an L1 miss (timing ablations: with
+            // the same rows but the wave's lanes in one 64-column span of each, 0.085 against
+            // 0.220 ms at parrington).  Here the window's (row, strip) items are numbered row
+            // by row -- per row the exact column interval of the rotated square, strips of 4
+            // columns aligned to the image's 4-column grid -- and lane l takes items l, l + 64,
+            // ...: one load instruction covers ~5 consecutive rows, each row's strips side by
+            // side, and the rows above / below were fetched by the neighbouring lanes.  Same
+            // samples and arithmetic as the column walk (integer histogram: bit-identical).
+            bool rows_done = false;
+            {
+                const int ylo = max(-half, 1 - py), yhi = min(half, rows - 2 - py);
+                const int xlo = max(-half, 1 - px), xhi = min(half, cols - 2 - px);
+                // per row ys: rrot = xs sin + ys cos, crot = xs cos - ys sin
+                const double ib_r = fabs(sin_a) < 1e-12 ? 0.0 : 1.0 / sin_a;
+                const double ib_c = fabs(cos_a) < 1e-12 ? 0.0 : 1.0 / cos_a;
+                uint16_t *tb = row_tbl[wv];
+                if (lane < 4) {                    // a strip may end up to 3 columns past the patch
+                    cbr[side + lane] = 1e30f;
+                    cbc[side + lane] = 1e30f;
+                }
+                int rrun = 0;
+                for (int r4 = 0; r4 < side; r4 += 64) {
+                    const int r = r4 + lane, ys = r - half;
+                    int klo = 0, n = 0;
+                    if (r < side && ys >= ylo && ys <= yhi && xlo <= xhi) {
+                        int lo = xlo, hi = xhi;
+                        const double bvs[2] = {ys * cos_a, -ys * sin_a};
+                        const double ias[2] = {ib_r, ib_c};
+#pragma unroll
+                        for (int qd = 0; qd < 2; ++qd) {
+                            const double bv = bvs[qd], ia = ias[qd];
+                            if (ia == 0.0) {
+                                if (!(fabs(bv) < lim)) hi = lo - 1;
+                                continue;
+                            }
+                            const double t1 = (-lim - bv) * ia, t2 = (lim - bv) * ia;
+                            const double l = fmax(fmin(t1, t2) - 1e-6, -half - 1.0);
+                            const double u = fmin(fmax(t1, t2) + 1e-6, half + 1.0);
+                            lo = max(lo, (int)ceil(l));
+                            hi = min(hi, (int)floor(u));
+                        }
+                        if (hi >= lo) {                    // image columns px + lo .. px + hi
+                            klo = (px + lo) >> 2;
+                            n = ((px + hi) >> 2) - klo + 1;
+                        }
+                    }
+                    int incl = n;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const int tt = __shfl_up(incl, d);
+                        if (lane >= d) incl += tt;
+                    }
+                    const int b0 = rrun + incl - n;
+                    if (b0 + n <= kRowTbl)
+                        for (int k2 = 0; k2 < n; ++k2) tb[b0 + k2] = (uint16_t)((r << 8) | (klo + k2 - ((px - half) >> 2) + 1));
+                    rrun += __shfl(incl, 63);
+                }
+                if (rrun <= kRowTbl) {
+                    rows_done = true;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // strip k (stored relative to the patch's first strip, + 1 so it stays >= 0)
+                    // covers image columns 4k .. 4k + 3: taps 4k - 1 .. 4k + 4 of the row, 4k .. 4k + 3
+                    // of the rows above and below; 16-byte loads when rows start 16-byte aligned
+                    const int kb = ((px - half) >> 2) - 1;
+                    const bool al = ((cols & 3) == 0) && (((uintptr_t)img & 15) == 0);
+                    struct Taps { float m[4], c[6], p[4]; };
+                    auto fetch = [&](int t, Taps &T, int &ys, int &k) {
+                        const unsigned e = tb[t];
+                        ys = (int)(e >> 8) - half;
+                        k = kb + (int)(e & 255);
+                        const float *q = img + (size_t)(py + ys) * cols + 4 * k;
+                        if (al) {
+                            const float4 a = *(const float4 *)(q - cols), b = *(const float4 *)q,
+                                         c = *(const float4 *)(q + cols);
+                            T.m[0] = a.x; T.m[1] = a.y; T.m[2] = a.z; T.m[3] = a.w;
+                            T.c[1] = b.x; T.c[2] = b.y; T.c[3] = b.z; T.c[4] = b.w;
+                            T.p[0] = c.x; T.p[1] = c.y; T.p[2] = c.z; T.p[3] = c.w;
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                T.m[i] = q[i - cols];
+                                T.c[i + 1] = q[i];
+                                T.p[i] = q[i + cols];
+                            }
+                        }
+                        T.c[0] = q[-1];
+                        T.c[5] = q[4];
+                    };
+                    // kRowLanes consecutive lanes take consecutive items (one row span per load);
+                    // the 64 / kRowLanes lane sets walk their own contiguous part of the items,
+                    // in other rows -- other spatial cells, so the histogram atomics of a wave
+                    // spread over addresses (fully interleaved, adjacent pixels of one cell with
+                    // similar gradients serialise on the same LDS words)
+                    constexpr int NSET = 64 / kRowLanes;
+                    const int per = ((rrun + NSET - 1) / NSET + kRowLanes - 1) / kRowLanes * kRowLanes;
+                    const int t0 = (lane / kRowLanes) * per + (lane % kRowLanes);
+                    const int tend = min(t0 - (lane % kRowLanes) + per, rrun);
+                    Taps A, B;
+                    int ysA = 0, kA = 0;
+                    if (t0 < tend) fetch(t0, A, ysA, kA);
+                    for (int t = t0; t < tend; t += kRowLanes) {
+                        int ysB = 0, kB = 0;
+                        if (t + kRowLanes < tend) fetch(t + kRowLanes, B, ysB, kB);
+                        const float ysf = (float)ysA, ys2 = ysf * ysf;
+                        const int c0 = 4 * kA - px + half;       // patch column of the strip's first
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int xs = c0 + i - half;
+                            sample(A.c[i + 2] - A.c[i], A.m[i] - A.p[i], fmaf(ysf, ar, cbr[c0 + i]),
+                                   fmaf(ysf, ac, cbc[c0 + i]), __builtin_amdgcn_exp2f(kq * (ys2 + (float)(xs * xs))));
+                        }
+                        A = B;
+                        ysA = ysB;
+                        kA = kB;
+                    }
+                }
+            }
+            if (!rows_done) square_walk();
+#else
+            {
             // lane group g (kDescGrp adjacent lanes) walks its run of (super-strip, row) steps;
             // lane `sub` of the group takes strip `sub` of each super-strip, so one load
             // instruction covers a group's kDescSS-column row span in ~1 cache line
@@ -1564,7 +1735,115 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const int sub = lane & (kDescGrp - 1);
             int t = (lane / kDescGrp) * Q;
             const int tend = min(t + Q, nsamp);
-#if PANO_DESC_RING
+#if PANO_DESC_COMPACT
+            // Compaction.  About half the lane slots of the direct walk carry a rejected
+            // sample (the super-strip's union interval, the rotated square's corners, ragged
+            // run ends): measured at parrington, 175 VALU lane-slots per binned sample against
+            // ~87 instructions of binning.  Here the walk only forms each candidate's inputs
+            // (taps, bin coordinates, weight exponent) and appends the ones that pass the bin
+            // test to the wave's LDS ring (ballot + mbcnt); every time 64 are waiting, each lane
+            // bins one -- the same samples with the same arithmetic, so the integer histogram
+            // is bit-identical.  The walk runs Q wave-uniform steps, `live` per lane.
+            {
+                float2 *qg = cq_g[wv], *qb = cq_b[wv];
+                float *qw = cq_w[wv];
+                int qh = 0, qn = 0;                      // wave-uniform ring head / count
+                auto drain = [&](int n) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (lane < n) {
+                        const int e = (qh + lane) & (kDescQ - 1);
+                        const float2 g = qg[e], b = qb[e];
+                        sample_in(g.x, g.y, b.x, b.y, __builtin_amdgcn_exp2f(qw[e]));
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();     // read before the slots are refilled
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    qh = (qh + n) & (kDescQ - 1);
+                    qn -= n;
+                };
+                auto put = [&](bool live, float gx, float gy, float rbin, float cbin, float warg) {
+                    const bool ok = live && rbin > -1.0f && rbin < 4.0f && cbin > -1.0f && cbin < 4.0f;
+                    const unsigned long long m = __ballot(ok);
+                    if (ok) {
+                        const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                        const int e = (qh + qn + r) & (kDescQ - 1);
+                        qg[e] = make_float2(gx, gy);
+                        qb[e] = make_float2(rbin, cbin);
+                        qw[e] = warg;
+                    }
+                    qn += __popcll(m);
+                    if (qn >= 64) drain(64);
+                };
+                constexpr int WN = kDescSW + 2;
+                int sx = 0, ys = 0, yend = 0;
+                auto win = [&](int sxx, int y, float (&T)[WN]) {
+                    const float *q = img + (size_t)(py + y) * cols + (px + sxx * kDescSS + sub * kDescSW - half) - 1;
+#pragma unroll
+                    for (int i = 0; i < WN; ++i) T[i] = q[i];
+                };
+                float br[kDescSW], bc[kDescSW], xs2[kDescSW];
+                auto strip_consts = [&](int sxx) {
+#pragma unroll
+                    for (int i = 0; i < kDescSW; ++i) {
+                        const int c = sxx * kDescSS + sub * kDescSW + i;
+                        br[i] = cbr[c];
+                        bc[i] = cbc[c];
+                        xs2[i] = (float)((c - half) * (c - half));
+                    }
+                };
+                float Tm[WN], T0[WN], Tp[WN];
+                if (t < tend) {
+                    int shi = nstrip - 1;                // largest strip with cpre[sx] <= t
+                    while (sx < shi) {
+                        const int mid = (sx + shi + 1) >> 1;
+                        if (cpre[mid] <= t) sx = mid;
+                        else shi = mid - 1;
+                    }
+                    ys = clo[sx] + (t - cpre[sx]);
+                    yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                    strip_consts(sx);
+                    win(sx, ys - 1, Tm);
+                    win(sx, ys, T0);
+                    win(sx, ys + 1, Tp);
+                }
+                for (int it = 0; it < Q; ++it) {
+                    const int j = t + it;
+                    const bool live = j < tend;
+                    int sn = sx, yn = ys + 1;
+                    const bool more = j + 1 < tend;
+                    const bool newstrip = more && yn >= yend;
+                    if (newstrip) {
+                        do { ++sn; } while (cpre[sn + 1] == cpre[sn]);
+                        yn = clo[sn];
+                    }
+                    float N2[WN];
+                    if (more && !newstrip) win(sn, yn + 1, N2);
+                    const float ysf = (float)ys, ys2 = ysf * ysf;
+#pragma unroll
+                    for (int i = 0; i < kDescSW; ++i)
+                        put(live, T0[i + 2] - T0[i], Tm[i + 1] - Tp[i + 1], fmaf(ysf, ar, br[i]),
+                            fmaf(ysf, ac, bc[i]), kq * (ys2 + xs2[i]));
+                    if (more) {
+                        if (newstrip) {
+                            sx = sn;
+                            yend = clo[sx] + (cpre[sx + 1] - cpre[sx]);
+                            strip_consts(sx);
+                            win(sn, yn - 1, Tm);
+                            win(sn, yn, T0);
+                            win(sn, yn + 1, Tp);
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < WN; ++i) { Tm[i] = T0[i]; T0[i] = Tp[i]; Tp[i] = N2[i]; }
+                        }
+                        ys = yn;
+                    }
+                }
+                if (qn > 0) drain(qn);
+            }
+#elif PANO_DESC_RING
             // Tap rows prefetched kRing steps ahead through an LDS ring by LDS-DMA loads
             // (global_load_lds, 2 x 12 bytes per lane and step, no VGPRs): more of each wave's
             // scattered row loads in flight than the one-step register prefetch allows (its
@@ -1718,6 +1997,17 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                 auto win = [&](int sxx, int y, float (&T)[WN]) {
 #if PANO_DESC_ABL == 3
                     const float *q = img + (size_t)py * cols + px + ((sxx + y) & 1) - 1;   // L1-resident
+#elif PANO_DESC_ABL == 4
+                    // coalesced: every lane of the wave in the first active lane's row, 16-lane
+                    // groups over 64 consecutive columns (2 lines per load; values wrong)
+                    const int yu = __builtin_amdgcn_readfirstlane(y);
+                    const int cq = min(max(px - half - 1, 0) + (lane & 15) * 4, cols - WN);
+                    const float *q = img + (size_t)(py + yu) * cols + max(cq, 0);
+#elif PANO_DESC_ABL == 5
+                    // each lane's own row, the whole wave in one 64-column span of it (as 4 but
+                    // the rows scattered: lines per load = distinct rows)
+                    const int cq = min(max(px - half - 1, 0) + (lane & 15) * 4, cols - WN);
+                    const float *q = img + (size_t)(py + y) * cols + max(cq, 0);
 #else
                     const float *q = img + (size_t)(py + y) * cols + (px + sxx * kDescSS + sub * kDescSW - half) - 1;
 #endif
@@ -1832,21 +2122,10 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
 #endif
             }
 #endif
-        } else {
-            // very large patches (non-default parameters): every sample of the square
-            const int S = side * side;
-            for (int j = lane; j < S; j += 64) {
-                const int xi = j / side, yi = j - (j / side) * side;
-                const int xs = xi - half, ys = yi - half;
-                const int rr = py + ys, cc = px + xs;
-                if (!(rr > 0 && rr < rows - 1 && cc > 0 && cc < cols - 1)) continue;
-                const double rq = ((double)xs * sin_a + (double)ys * cos_a) * inv_hw;
-                const double cq = ((double)xs * cos_a - (double)ys * sin_a) * inv_hw;
-                if (!(fabs(rq) < 2.5 + 1e-6 && fabs(cq) < 2.5 + 1e-6)) continue;
-                const float *q = img + (size_t)rr * cols + cc;
-                sample(q[1] - q[-1], q[-cols] - q[cols], (float)rq + 1.5f, (float)cq + 1.5f,
-                       (float)exp(-0.125 * (rq * rq + cq * cq)));
             }
+#endif
+        } else {
+            square_walk();
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1860,7 +2139,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             return (float)((double)v * (1.0 / 4194304.0));
         };
         float lo = interior(lane), hi = interior(64 + lane);
-        if (PANO_DESC_ABL == 2) lo += (float)abl_sink;
+        if (PANO_DESC_ABL >= 2) lo += (float)abl_sink;   // keeps the ablations' samples alive
         const float thr = sqrtf(sdot_skx_wave128(lo, hi)) * dp.max_value;
         lo = lo > thr ? thr : lo;
         hi = hi > thr ? thr : hi;
