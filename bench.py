@@ -12,8 +12,8 @@ read back with the band head (one host read per rank), every band sent to rank 0
 over xGMI), which assembles the canvas and crops the panorama -- inside the timed step].
 
 N = 1 (default): one stitch of the 18 parrington frames (BASELINE config 3, the headline);
-the K timed stitches go through pipeline.StitchPool (--contexts, default 2): stitch i on a
-private libpano context i % 2 with its own stream, so the device overlaps two stitches; every
+the K timed stitches go through pipeline.StitchPool (--contexts, default 4): stitch i on a
+private libpano context i % 4 with its own stream, so the device overlaps four stitches; every
 stitch completes and is read back, and the last one is checked byte for byte against the
 single-context stitch.  One context's run_sequence and synchronous run() over the same K
 stitches are reported beside (`single_context_ms_per_step`, `run_ms_per_step`).
@@ -139,7 +139,7 @@ def parse():
     ap.add_argument("--cap", type=int, default=0, help="keypoint capacity per frame (0 = auto)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch eagerly instead of replaying captured hipGraphs")
-    ap.add_argument("--contexts", type=int, default=2,
+    ap.add_argument("--contexts", type=int, default=4,
                     help="N = 1 pipelined form: stitches dealt over this many private libpano "
                          "contexts (pipeline.StitchPool); 1 = one Stitcher's run_sequence")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",

@@ -258,7 +258,8 @@ def test_run_sequence_distinct_buffers(gpu, parrington):
     assert len(st._graphs) <= 2 * len(sets), len(st._graphs)
 
 
-def test_stitch_pool_matches_run(gpu, parrington):
+@pytest.mark.parametrize("contexts", [2, 4])
+def test_stitch_pool_matches_run(gpu, parrington, contexts):
     """StitchPool: stitches dealt round-robin over private contexts (own scratch, own stream)
     overlap on the device and give run()'s panoramas in item order -- one resident buffer
     re-stitched, and distinct buffers with different frame orders."""
@@ -269,14 +270,14 @@ def test_stitch_pool_matches_run(gpu, parrington):
     fsets = [list(np.roll(np.asarray(focals), k)) for k in (0, 5)]
     want = [st.run(st.upload(fr), fo, margin=margin).panorama.cpu().numpy().copy() for fr, fo in zip(sets, fsets)]
     st.release_graphs()
-    pool = StitchPool("sift", contexts=2)
+    pool = StitchPool("sift", contexts=contexts)
     dev = pool.upload(sets[0])
     n = 0
     for r in pool.run_sequence([(dev, fsets[0])] * 7, margin=margin):
         np.testing.assert_array_equal(r.panorama.cpu().numpy(), want[0], err_msg=f"item {n}")
         n += 1
     assert n == 7
-    order = [0, 1, 1, 0, 1, 0]
+    order = [0, 1, 1, 0, 1, 0, 0, 1, 1]
     items = [(pool.upload(sets[k]), fsets[k]) for k in order]
     for i, (k, r) in enumerate(zip(order, pool.run_sequence(items, margin=margin))):
         np.testing.assert_array_equal(r.panorama.cpu().numpy(), want[k], err_msg=f"distinct item {i}")
