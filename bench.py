@@ -126,7 +126,7 @@ def blur_f32_flops(st, n_frames):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=None, choices=["parrington", "grail", "synthetic"],
                     help="default: parrington at N = 1 (the headline config); at N > 1 the "
