@@ -1280,15 +1280,22 @@ constexpr int kRing = PANO_DESC_RING;
 #ifndef PANO_DESC_ROWS
 #define PANO_DESC_ROWS 0              // 1: row-major walk over (row, strip) items (measured slower)
 #endif
+#ifndef PANO_DESC_PK
+#define PANO_DESC_PK 0                // 1: the trilinear products as packed f32 pairs (measured slower)
+#endif
 #ifndef PANO_DESC_COMPACT
 #define PANO_DESC_COMPACT 0           // 1: samples binned from a compaction queue, 64 at a time (measured slower)
 #endif
+#if PANO_DESC_COMPACT
 constexpr int kDescQ = 128;           // queue entries per wave: <= 63 waiting + 64 appended
+#endif
 #ifndef PANO_DESC_RLANES
 #define PANO_DESC_RLANES 8            // row walk: consecutive lanes on consecutive items
 #endif
+#if PANO_DESC_ROWS
 constexpr int kRowLanes = PANO_DESC_RLANES;
-constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; more: column walk)
+constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; more: the square)
+#endif
 #ifndef PANO_DESC_ABL
 #define PANO_DESC_ABL 0               // timing ablations only (1: plain LDS stores, 2: no LDS,
                                       // 3: every sample's taps from one cached location)
@@ -1484,7 +1491,14 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const int base = ((int)fr + 1) * kRowC + ((int)fc + 1) * kCell;   // (r0 + 1, c0 + 1) bin
 #endif
             const float c1 = wm * rf, c0w = wm - c1;
+#if PANO_DESC_PK
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            const f2v cfv = {1.0f - cf, cf};
+            const f2v vt = (f2v){c0w, c0w} * cfv, vb = (f2v){c1, c1} * cfv;
+            const float v00 = vt.x, v01 = vt.y, v10 = vb.x, v11 = vb.y;
+#else
             const float v00 = c0w * (1.0f - cf), v01 = c0w * cf, v10 = c1 * (1.0f - cf), v11 = c1 * cf;
+#endif
             const float of = ob - fo;
             const float nof = 1.0f - of;
 #if PANO_DESC_RPI
@@ -1497,7 +1511,17 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             auto fix = [](float v) { return (unsigned long long)(uint32_t)fmaf(v, kFix, 0.5f); };
 #endif
             unsigned long long *hA = h + base + o0, *hB = h + base + o1;
-#if PANO_DESC_ABL == 0
+#if PANO_DESC_ABL == 0 && PANO_DESC_PK
+            // the same eight f32 products as below, as v_pk_mul_f32 pairs (identical roundings)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 ov = {nof, of};
+            const f2 p00 = (f2){v00, v00} * ov, p01 = (f2){v01, v01} * ov;
+            const f2 p10 = (f2){v10, v10} * ov, p11 = (f2){v11, v11} * ov;
+            atomicAdd(hA, fix(p00.x));      atomicAdd(hB, fix(p00.y));
+            atomicAdd(hA + kCell, fix(p01.x));  atomicAdd(hB + kCell, fix(p01.y));
+            atomicAdd(hA + kRowC, fix(p10.x)); atomicAdd(hB + kRowC, fix(p10.y));
+            atomicAdd(hA + kRowC + kCell, fix(p11.x)); atomicAdd(hB + kRowC + kCell, fix(p11.y));
+#elif PANO_DESC_ABL == 0
             atomicAdd(hA, fix(v00 * nof));      atomicAdd(hB, fix(v00 * of));
             atomicAdd(hA + kCell, fix(v01 * nof));  atomicAdd(hB + kCell, fix(v01 * of));
             atomicAdd(hA + kRowC, fix(v10 * nof)); atomicAdd(hB + kRowC, fix(v10 * of));
