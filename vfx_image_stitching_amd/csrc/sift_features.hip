@@ -1301,6 +1301,22 @@ constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; 
                                       // 3: every sample's taps from one cached location)
 #endif
 
+#ifndef PANO_DESC_COUNT
+#define PANO_DESC_COUNT 0             // 1: diagnostics build, lane-occupancy counters of the walk
+#endif
+#if PANO_DESC_COUNT
+// [0] candidate lane-samples, [1] passing, [2] sample blocks executed (any lane passing),
+// [3] walk steps (wave-level), [4] active lanes summed over steps, [5] keypoints
+__device__ unsigned long long g_desc_cnt[8];
+extern "C" int pano_dbg_desc_count(unsigned long long *out, int reset) {
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_desc_cnt), z, sizeof(z)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_desc_cnt), sizeof(g_desc_cnt)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // Frame of dense keypoint index gk (frames' keypoints back to back, counts clamped to
 // [0, cap]): chunked wave scan of the counts; false when gk is past the last keypoint.
 __device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ counts, int n_frames,
@@ -1407,6 +1423,9 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         else if (RAW ? !locate_strided(counts, n_frames, cap, gk, f, k) : !locate_keypoint(counts, n_frames, cap, gk, f, k))
             break;
         if (order) k = order[(size_t)f * cap + k];     // locality order (desc_order)
+#if PANO_DESC_COUNT
+        if (lane == 0) atomicAdd(&g_desc_cnt[5], 1ull);
+#endif
         for (int i = lane; i < kDescCopies * kHistStride; i += 64) h0[i] = 0ull;
         pano_kp kp;
         if constexpr (RAW) {                           // emit_keypoints' conversion, exactly
@@ -2118,6 +2137,26 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
                     if (more && !newstrip) win(sn, yn + 1, N2);
 #endif
                     const float ysf = (float)ys, ys2 = ysf * ysf;
+#if PANO_DESC_COUNT
+                    {
+                        const unsigned long long act = __ballot(1);
+                        const int first = __ffsll((long long)act) - 1;
+                        unsigned long long pass = 0, blocks = 0;
+                        for (int i = 0; i < kDescSW; ++i) {
+                            const float rb = fmaf(ysf, ar, br[i]), cb = fmaf(ysf, ac, bc[i]);
+                            const unsigned long long m = __ballot(rb > -1.0f && rb < 4.0f && cb > -1.0f && cb < 4.0f);
+                            pass += __popcll(m);
+                            blocks += m != 0;
+                        }
+                        if (lane == first) {
+                            atomicAdd(&g_desc_cnt[0], (unsigned long long)__popcll(act) * kDescSW);
+                            atomicAdd(&g_desc_cnt[1], pass);
+                            atomicAdd(&g_desc_cnt[2], blocks);
+                            atomicAdd(&g_desc_cnt[3], 1ull);
+                            atomicAdd(&g_desc_cnt[4], (unsigned long long)__popcll(act));
+                        }
+                    }
+#endif
                     // exp(-((rrot/hw)^2 + (crot/hw)^2) / 8) = exp2(kq (xs^2 + ys^2)): a rotation
                     // keeps the radius (no LDS read on the sample path)
 #pragma unroll
