@@ -1301,6 +1301,9 @@ constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; 
                                       // 3: every sample's taps from one cached location)
 #endif
 
+#ifndef PANO_DESC_ABL_TRIG
+#define PANO_DESC_ABL_TRIG 0
+#endif
 #ifndef PANO_DESC_COUNT
 #define PANO_DESC_COUNT 0             // 1: diagnostics build, lane-occupancy counters of the walk
 #endif
@@ -1464,7 +1467,11 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         const int py = (int)rint((double)scl * (double)kp.y);
         const double angle = 360.0 - (double)kp.angle;
         const double rad = angle * (3.141592653589793 / 180.0);
+#if PANO_DESC_ABL_TRIG                         // timing ablation: f32 hardware sin / cos
+        const double cos_a = (double)__cosf((float)rad), sin_a = (double)__sinf((float)rad);
+#else
         const double cos_a = cos(rad), sin_a = sin(rad);
+#endif
         const float hw = (dp.hw_mult * scl) * kp.size;
         const double hwd = (double)hw, inv_hw = 1.0 / hwd;
         int half = (int)rint(hwd * 1.4142135623730951 * 5.0 * 0.5);
