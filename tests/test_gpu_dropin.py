@@ -282,3 +282,13 @@ def test_stitch_pool_matches_run(gpu, parrington, contexts):
     for i, (k, r) in enumerate(zip(order, pool.run_sequence(items, margin=margin))):
         np.testing.assert_array_equal(r.panorama.cpu().numpy(), want[k], err_msg=f"distinct item {i}")
     pool.release_graphs()
+
+
+def test_ctx_set_flags(gpu):
+    """pano_ctx_set_flags: PANO_CTX_TAIL_MAIN accepted, unknown bits and a null context refused."""
+    from vfx_image_stitching_amd import _lib
+    ctx = _lib.Context(0)
+    assert ctx.lib.pano_ctx_set_flags(ctx.h, _lib.PANO_CTX_TAIL_MAIN) == _lib.PANO_OK
+    assert ctx.lib.pano_ctx_set_flags(ctx.h, 0) == _lib.PANO_OK
+    assert ctx.lib.pano_ctx_set_flags(ctx.h, 2) == _lib.PANO_E_ARG
+    assert ctx.lib.pano_ctx_set_flags(None, 0) == _lib.PANO_E_ARG
