@@ -95,6 +95,10 @@ int pano_ctx_set_stream(pano_ctx *ctx, void *hip_stream);
  * the device (pipeline.StitchPool); alone, the side stream hides the tail.
  * No reference counterpart. */
 #define PANO_CTX_TAIL_MAIN 1
+/* PANO_CTX_MATCH_WHOLE: the distance GEMM's query tiles walk every candidate tile themselves
+ * (no candidate splits, no partials to fold): fewer, longer workgroups, better when the device
+ * is already full (StitchPool), worse for one stitch's latency.  Same results. */
+#define PANO_CTX_MATCH_WHOLE 2
 int pano_ctx_set_flags(pano_ctx *ctx, int flags);
 /* Pre-size scratch for n frames of h x w with cap keypoints per frame (allocates). */
 int pano_ctx_reserve(pano_ctx *ctx, int n, int h, int w, int cap);

@@ -285,10 +285,12 @@ def test_stitch_pool_matches_run(gpu, parrington, contexts):
 
 
 def test_ctx_set_flags(gpu):
-    """pano_ctx_set_flags: PANO_CTX_TAIL_MAIN accepted, unknown bits and a null context refused."""
+    """pano_ctx_set_flags: PANO_CTX_TAIL_MAIN / PANO_CTX_MATCH_WHOLE accepted, unknown bits and a
+    null context refused."""
     from vfx_image_stitching_amd import _lib
     ctx = _lib.Context(0)
     assert ctx.lib.pano_ctx_set_flags(ctx.h, _lib.PANO_CTX_TAIL_MAIN) == _lib.PANO_OK
     assert ctx.lib.pano_ctx_set_flags(ctx.h, 0) == _lib.PANO_OK
-    assert ctx.lib.pano_ctx_set_flags(ctx.h, 2) == _lib.PANO_E_ARG
+    assert ctx.lib.pano_ctx_set_flags(ctx.h, _lib.PANO_CTX_TAIL_MAIN | _lib.PANO_CTX_MATCH_WHOLE) == _lib.PANO_OK
+    assert ctx.lib.pano_ctx_set_flags(ctx.h, 4) == _lib.PANO_E_ARG
     assert ctx.lib.pano_ctx_set_flags(None, 0) == _lib.PANO_E_ARG

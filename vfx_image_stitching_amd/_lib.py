@@ -15,6 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PANO_CTX_TAIL_MAIN = 1        # pano_ctx_set_flags: the blur tail on the context's own stream
+PANO_CTX_MATCH_WHOLE = 2      # pano_ctx_set_flags: no candidate splits in the distance GEMM
 # PANO_LIB: an alternative build of the same ABI (A/B timing of two revisions, tools/ab_build.sh)
 LIB_PATH = os.environ.get("PANO_LIB") or os.path.join(_HERE, "libpano.so")
 

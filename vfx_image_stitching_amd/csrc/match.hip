@@ -1078,7 +1078,8 @@ int launch_match_u8(pano_ctx *ctx, const uint8_t *desc, const int32_t *norms, co
             const char *e = getenv("PANO_MATCH_WGS");   // fewest workgroups the splits aim at
             return e ? std::max(1, atoi(e)) : 1024;
         }();
-        const int n_split = std::max(1, std::min(n_bt, (target_wgs + n_qt * np - 1) / (n_qt * np)));
+        const int tw = (ctx->flags_opt & PANO_CTX_MATCH_WHOLE) ? 1 : target_wgs;
+        const int n_split = std::max(1, std::min(n_bt, (tw + n_qt * np - 1) / (n_qt * np)));
         const size_t part_bytes = ((size_t)np * n_split * cap * sizeof(Part) + 255) & ~size_t(255);
         int rc = pano_grow(ctx, &ctx->mscratch, &ctx->mscratch_bytes, part_bytes);
         if (rc) return rc;

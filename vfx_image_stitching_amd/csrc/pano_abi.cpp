@@ -189,7 +189,7 @@ int pano_ctx_set_stream(pano_ctx *ctx, void *stream) {
 }
 
 int pano_ctx_set_flags(pano_ctx *ctx, int flags) {
-    if (!ctx || (flags & ~PANO_CTX_TAIL_MAIN)) return PANO_E_ARG;
+    if (!ctx || (flags & ~(PANO_CTX_TAIL_MAIN | PANO_CTX_MATCH_WHOLE))) return PANO_E_ARG;
     ctx->flags_opt = flags;
     return PANO_OK;
 }

@@ -760,8 +760,10 @@ class StitchPool:
             # the blur tail on each member's own stream: with another stitch filling the device
             # the side stream's fork / join edges cost more than the overlap it buys (bench A/B:
             # 0.832-0.837 against 0.839-0.842 ms per stitch)
+            # and the distance GEMM without candidate splits (fewer, longer workgroups: 0.741-0.743
+            # against 0.745-0.748 ms per stitch at four contexts)
             for st in self.members:
-                st.ctx.set_flags(_lib.PANO_CTX_TAIL_MAIN)
+                st.ctx.set_flags(_lib.PANO_CTX_TAIL_MAIN | _lib.PANO_CTX_MATCH_WHOLE)
         self.streams = [torch.cuda.Stream(dev) for _ in range(contexts)]
         self.device = self.members[0].device
 
