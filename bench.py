@@ -2,7 +2,8 @@
 """Headline benchmark: Mpixels/s stitched, 18-image parrington, SIFT path, MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload parrington|grail|synthetic]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+    python bench.py --gpus N ...        (N > 1: starts its own N rank processes, one per GPU)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (the same ranks)
 
 A step = one whole stitch of one rank's sequence, inputs resident in HBM:
 cylindrical projection -> SIFT features of every frame -> NN match (exact i8 MFMA) -> RANSAC
@@ -66,12 +67,14 @@ PMC_PROFILE_FRAMES = {"parrington": 18, "synthetic": 19}   # frames of the profi
 
 
 def pmc_traffic(kernel, workload, method, n_frames):
-    """HBM bytes per launch of a kernel class from the newest committed PMC traffic profile
+    """HBM bytes PER STEP of a kernel class from the newest committed PMC traffic profile
     (tools/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over the same
     SIFT step -- parrington, or the 19-frame synthetic 1080p one -- corrected per
     profiles/r01_fetch_calibration.txt).  A step of another frame count (the strong-scaling
     batch: 144 frames on one GPU) gets the profile's bytes scaled per frame -- every class
-    here moves bytes in proportion to its frames -- and the source says so."""
+    here moves bytes in proportion to its frames -- and the source says so.  Per step, not per
+    launch: the profile's launch count and the bench's need not agree (round 5's line mixed
+    them), the step is the unit both count."""
     import glob
     if workload not in ("parrington", "synthetic") or method != "sift":
         return None, None
@@ -80,15 +83,15 @@ def pmc_traffic(kernel, workload, method, n_frames):
         return None, None
     d = json.load(open(files[-1]))
     c = d.get("classes", {}).get(kernel)
-    if not c or not c.get("launches_per_step"):
+    if not c:
         return None, None
-    per_launch = c["hbm_bytes_per_step"] / c["launches_per_step"]
+    per_step = c["hbm_bytes_per_step"]
     src = os.path.relpath(files[-1], ROOT)
     prof_frames = d.get("frames", PMC_PROFILE_FRAMES[workload])
     if n_frames != prof_frames:
-        per_launch *= n_frames / prof_frames
+        per_step *= n_frames / prof_frames
         src += f" (a {prof_frames}-frame step, scaled per frame to {n_frames} frames)"
-    return per_launch, src
+    return per_step, src
 
 
 def blur_f32_flops(st, n_frames):
@@ -257,15 +260,46 @@ def kernel_bytes(name, st, n_frames, h, w):
     return None, None
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` with no launcher: start N rank processes of this same command
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would, rendezvous on
+    127.0.0.1), wait for all of them and return the worst exit status.  Runs before anything in
+    this process touches the GPU (children are started, never exec'd); rank 0 prints the line."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(spawn_ranks(args.gpus))
+    if os.environ.get("PANO_BENCH_SPAWN_PROBE") == "1":
+        # tests/test_bench_spawn.py: what a spawned rank was given, before any GPU work
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                         "MASTER_ADDR", "MASTER_PORT")}), flush=True)
+        return
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # rehearsal of the N > 1 path on a one-GPU box (tests only, never a reported line): every
     # rank on cuda:0 over gloo (PANO_BENCH_REHEARSE=1); the real run is one rank per GPU, RCCL
     rehearse = os.environ.get("PANO_BENCH_REHEARSE") == "1"
@@ -420,14 +454,17 @@ def main():
         if byts is not None:
             per_launch_bytes = byts / launches_per_step
             ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
-            traffic, tsrc = pmc_traffic(rk, args.workload, args.method, n_local)
+            traffic_step, tsrc = pmc_traffic(rk, args.workload, args.method, n_local)
             roof = {"bound": "hbm", "kernel": rk, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                     "timing": ("HIP events on the library stream, %d eager steps right after the "
                                "graph-replayed timed region" % args.steps) if args.graph
                     else "HIP events on the library stream over the timed region",
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-                    "traffic": round(traffic) if traffic else None,
-                    "traffic_unit": "HBM bytes per launch",
+                    "traffic": round(traffic_step / launches_per_step) if traffic_step else None,
+                    "traffic_unit": "HBM bytes per launch (the PMC step's bytes / this step's launches)",
+                    "traffic_per_step": round(traffic_step) if traffic_step else None,
+                    "algorithmic_bytes_per_step": round(byts),
+                    "traffic_over_algorithmic": round(traffic_step / byts, 3) if traffic_step else None,
                     "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": round(per_launch_bytes),
                     "avg_launch_ms": round(per_launch_ms, 5), "launches_per_step": launches_per_step,
@@ -520,6 +557,10 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
         "timed_form": (f"StitchPool.run_sequence ({args.contexts} private contexts, items round-robin)"
                        if pool is not None else "run_sequence" if pipelined else "run"),
+        "pooled_ms_per_stitch": round(ms_step, 4) if pool is not None else None,
+        "pooled_note": ("ms_per_step is the throughput of StitchPool (up to 2 stitches in flight per "
+                        "context); single_context_ms_per_step is the one-context figure rounds 1-4 "
+                        "reported as ms_per_step") if pool is not None else None,
         "single_context_ms_per_step": round(ms_single, 4) if ms_single is not None else None,
         "run_sequence_ms_per_step" if seq_beside else "run_ms_per_step":
             round(ms_other, 4) if ms_other is not None else None,

@@ -24,7 +24,7 @@ CLASSES = [
     (r"^(bbox_|gray_bbox)", "gray_bbox"),
     # timing-class names of _lib.KERNELS: the inverse-map pair (cyl_columns, cyl_inverse)
     # fills the slots the scatter pair (cyl_scatter, cyl_gather) named first
-    (r"^(cyl_scatter|cyl_columns)", "cyl_scatter"),
+    (r"^(cyl_scatter|cyl_columns|cyl_tile)", "cyl_scatter"),
     (r"^(cyl_gather|cyl_inverse)", "cyl_gather"),
     (r"^jpeg_", "jpeg_decode"),
 ]
@@ -43,25 +43,32 @@ root, runs = sys.argv[1], int(sys.argv[2])
 work = sys.argv[3] if len(sys.argv) > 3 else "parrington"
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, tools/pmc_traffic.sh, {work} SIFT step",
        "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (profiles/r01_fetch_calibration.txt)",
-       "steps": runs - 1, "classes": {}}
+       "classes": {}}
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
 launches = collections.defaultdict(int)
+steps = None
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = []
     for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
         rows += list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    # skip the first stitch: everything before the second projection dispatch
+    # a stitch starts with its projection launch; the first stitch (allocations, captures) is
+    # skipped and the rest are averaged.  Round 5's table divided three stitches by two: the
+    # one-launch projection (cyl_tile) was missing from the class patterns, so nothing was
+    # skipped and every class read 1.5x its true bytes per step.
     starts = [i for i, r in enumerate(rows) if cls(r["Kernel_Name"]) == "cyl_scatter"]
-    for r in rows[starts[1] if len(starts) > 1 else 0:]:
+    if len(starts) != runs:
+        sys.exit(f"{c}: {len(starts)} stitches found in the trace, {runs} expected")
+    steps = runs - 1
+    for r in rows[starts[1]:]:
         k = cls(r["Kernel_Name"])
         if k is None:
             continue
         acc[k][c] += float(r["Counter_Value"]) * 1024
         if c == "FETCH_SIZE":
             launches[k] += 1
+out["steps"] = steps
 for k, v in acc.items():
-    steps = runs - 1
     out["classes"][k] = {"hbm_bytes_per_step": round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) / steps),
                          "read_bytes_per_step": round(2 * v["FETCH_SIZE"] / steps),
                          "write_bytes_per_step": round(v["WRITE_SIZE"] / steps),

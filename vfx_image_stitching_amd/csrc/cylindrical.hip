@@ -428,11 +428,14 @@ cyl_tile(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, const int2 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its ORs performed
         __syncthreads();
         int32_t *cnt = sync.cnt + (size_t)f * gridDim.x + blockIdx.x;
-        if (tid == 0)
+        if (tid == 0) {
+            fold_release();
             last_s = __hip_atomic_fetch_add((g_i32 *)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                      (int)gridDim.y - 1;
+        }
         __syncthreads();
         if (!last_s) return;
+        fold_acquire();
         if (tid < kTX && xp0 + tid < w) {
             const uint32_t v = __hip_atomic_load((g_u32 *)(fl_f + xp0 + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             colnz[(size_t)f * w + xp0 + tid] = v ? 1 : 0;

@@ -934,11 +934,14 @@ dist_i8(const uint8_t *__restrict__ desc, const int32_t *__restrict__ norms, con
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every wave: its partials landed
     __syncthreads();
     int32_t *cnt = fold.cnt + (size_t)p * gridDim.z + blockIdx.z;
-    if (tid == 0)
+    if (tid == 0) {
+        fold_release();
         last = __hip_atomic_fetch_add((g_i32 *)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                min(n_split, n_jt) - 1;
+    }
     __syncthreads();
     if (!last) return;
+    fold_acquire();
     if (tid < QT && i0 + tid < cap) {
         const int gi = i0 + tid;
         float b = INFINITY, s = INFINITY;

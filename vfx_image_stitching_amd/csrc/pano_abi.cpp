@@ -161,6 +161,10 @@ int pano_ctx_release_scratch(pano_ctx *ctx) {
         {&ctx->hmscratch, &ctx->hmscratch_bytes},        {(void **)&ctx->flags, &ctx->flags_bytes},
         {&ctx->hscratch, &ctx->hscratch_bytes},          {&ctx->bscratch, &ctx->bscratch_bytes},
         {&ctx->jscratch, &ctx->jscratch_bytes},          {(void **)&ctx->raw_sorted, &dummy},
+        {(void **)&ctx->descraw, &ctx->descraw_bytes},   {&ctx->cyl_sync, &ctx->cyl_sync_bytes},
+        // arrival counters: zeroed when (re)allocated, so a released one comes back zeroed
+        {(void **)&ctx->octs_sync, &ctx->octs_sync_bytes}, {(void **)&ctx->match_sync, &ctx->match_sync_bytes},
+        {(void **)&ctx->sel_sync, &ctx->sel_sync_bytes},
     };
     for (const Slot &s : slots) {
         if (*s.p) (void)hipFree(*s.p);

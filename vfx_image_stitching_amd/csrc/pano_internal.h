@@ -23,6 +23,32 @@
 constexpr int kCntStride = 32;
 #define PANO_ORI_BINS 36
 
+// Cross-workgroup hand-off of the last-arriver folds (dist_i8 -> reduce, pair_votes ->
+// select, cyl_tile<true> -> column flags, blur_octs row counters): the partials are stored at
+// agent scope, every wave drains them (s_waitcnt vmcnt(0)) before the barrier, one lane counts
+// the workgroup in with an agent-scope add, and the last arriver reads the partials with
+// agent-scope loads.  On gfx950 (and gfx942) agent-scope relaxed stores and loads bypass the
+// XCD's private L2 (sc1), so drained partials are visible to the last arriver; the HIP / LLVM
+// memory model only promises that with a release before the add and an acquire after it.
+// PANO_FOLD_FENCE=1 inserts exactly those fences (fold_release / fold_acquire); any other
+// target must build with it.
+#ifndef PANO_FOLD_FENCE
+#define PANO_FOLD_FENCE 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && !PANO_FOLD_FENCE && !defined(__gfx950__) && !defined(__gfx942__)
+#error "the relaxed last-arriver folds rely on gfx950 / gfx942 sc1 semantics: build with -DPANO_FOLD_FENCE=1"
+#endif
+__device__ __forceinline__ void fold_release() {
+#if PANO_FOLD_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+}
+__device__ __forceinline__ void fold_acquire() {
+#if PANO_FOLD_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
+
 // Raw keypoint produced by the orientation kernel (before sort/dedup/convert), in base
 // (2x upsampled) coordinates, exactly the fields sift_impl.py:206-210/290 stores, plus a
 // deterministic scan-order tie-break.

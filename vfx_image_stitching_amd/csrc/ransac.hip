@@ -306,11 +306,13 @@ pair_votes(const double2 *__restrict__ moves, const int32_t *__restrict__ kcount
             for (int x = 0; x < VJS; ++x)
                 splits += (int)((long long)K * x / VJS) < (int)((long long)K * (x + 1) / VJS);
             const int n_live = ((K + VB - 1) / VB) * splits;
+            fold_release();
             last = __hip_atomic_fetch_add((g_i32 *)(sa.cnt + p), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                    n_live - 1;
         }
         __syncthreads();
         if (!last) return;
+        fold_acquire();
         int32_t *vp = votes + (size_t)p * cap;
         select_pair<VB>(ish, sa.kps, sa.xy, sa.counts, cap, sa.pairs.a[p], sa.pairs.b[p],
                         sa.best + (size_t)p * cap, mv, sa.midx + (size_t)p * cap, K,

@@ -1666,9 +1666,9 @@ int launch_pair(pano_ctx *ctx, const LoadArgs &la, float *out1, float *dog1, flo
 // Octaves o_a .. o_tail - 1 (parrington: 1-3, 1080p: 1-5) in ONE launch instead of one launch
 // per level.  Each of those levels is a few hundred to a few thousand 32 x 32 tiles, so a
 // per-level launch costs its wave fill and drain (~5-15 us) more than its work, and the
-// octaves run back to back.  Here resident workgroups take tiles in a fixed order (item =
-// block + k * grid; phases (octave, level) sorted by dependency depth, octave o + 1's level 1
-// right after octave o's level nl - 3), and a tile waits only for the tile ROWS of its source
+// octaves run back to back.  Here workgroups claim tiles by an atomic ticket in a fixed order
+// (phases (octave, level) sorted by dependency depth, octave o + 1's level 1 right after
+// octave o's level nl - 3), and a tile waits only for the tile ROWS of its source
 // that its halo reads: rows ty - 1 .. ty + 1 of level l - 1, or for level 1 the INTER_NEAREST
 // source rows in octave o - 1's level nl - 3.  Finished tiles are counted per (octave, level,
 // frame, tile row).  Hand-off across the 8 XCDs' private L2s (MI355X guide, visibility, R1):
@@ -1703,7 +1703,8 @@ struct OctsArgs {
     const float *taps;           // [level][PANO_MAX_TAPS] (ctx->taps)
     int ph_o[kOctsMaxPhase], ph_l[kOctsMaxPhase];
     long long ph_start[kOctsMaxPhase + 1];
-    int *sync;                   // [0] exited workgroups, [1] spin time-outs (sticky), counters
+    int *sync;                   // [0] exited workgroups, [1] spin time-outs (sticky), [2] the
+                                 // next ticket (tile claim order), counters
                                  // from kOctsSync0: [n_oct][nl][n][kOctsRows] finished tiles
     int ncnt;                    // counter words
     int abl;                     // timing ablations (PANO_OCTS_ABL, wrong planes): 1 no waits,
@@ -1852,7 +1853,19 @@ blur_octs(OctsArgs a) {
     __shared__ __attribute__((aligned(16))) float tin[(kOctsT + 2 * kOctsRMax) * kOctsIWP];
     __shared__ float ost[kOctsT * kOctsOP];
     __shared__ int last;
-    for (long long it = blockIdx.x; it < a.total; it += gridDim.x) {
+    __shared__ int ticket;
+    // Items are claimed by an atomic ticket (sync[2]) in dependency order, not dealt by block
+    // index: every item a tile waits for was claimed earlier by a workgroup that is running, and
+    // the lowest unfinished ticket never waits, so the launch progresses with any number of
+    // its workgroups resident -- beside another context's kernels too (StitchPool).  Round 5's
+    // dealt order (item = block + k * grid) needed the whole grid resident and spun into its
+    // time-out when it was not.
+    for (;;) {
+        if (threadIdx.x == 0)
+            ticket = __hip_atomic_fetch_add((g_i32 *)(a.sync + 2), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const long long it = ticket;
+        if (it >= a.total) break;
         int p = 0;
         while (p + 1 < a.nphase && it >= a.ph_start[p + 1]) ++p;
         const int oi = a.ph_o[p], l = a.ph_l[p];
@@ -1881,6 +1894,7 @@ blur_octs(OctsArgs a) {
             octs_wait(a.sync + kOctsSync0 + ((so * a.nl + sl) * a.n + f) * kOctsRows, r0, r1, a.ntx[so], a.sync);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler only: loads stay after the poll
         __syncthreads();
+        fold_acquire();
         const int H = a.H[oi], W = a.W[oi];
         const float *src;
         int sh = H, sw = W;
@@ -1905,12 +1919,16 @@ blur_octs(OctsArgs a) {
         }
         if (!(a.abl & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its stores landed
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
+            fold_release();
             __hip_atomic_fetch_add((g_i32 *)(a.sync + kOctsSync0 + ((oi * a.nl + l) * a.n + f) * kOctsRows + ty), 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // (the barrier after the next ticket draw orders this item's reads of `ticket` before
+        // thread 0 overwrites it)
     }
-    // the last workgroup out re-zeroes the counters for the next launch (graph replays): every
-    // other workgroup has finished all its polls by then
+    // the last workgroup out re-zeroes the counters and the ticket for the next launch (graph
+    // replays): every other workgroup has drawn its final ticket and finished its polls by then
     if (threadIdx.x == 0)
         last = __hip_atomic_fetch_add((g_i32 *)a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                (int)gridDim.x - 1;
@@ -1918,7 +1936,10 @@ blur_octs(OctsArgs a) {
     if (!last) return;
     for (int i = threadIdx.x; i < a.ncnt; i += kOctsThreads)
         __hip_atomic_store((g_i32 *)(a.sync + kOctsSync0 + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) __hip_atomic_store((g_i32 *)a.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store((g_i32 *)(a.sync + 2), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((g_i32 *)a.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Can octaves o_a .. o_b - 1 go to blur_octs?  The reference's level taps (the compiled tap
@@ -1989,7 +2010,8 @@ int launch_octs(pano_ctx *ctx, int o_a, int o_b, int n, int nl, bool full) {
         return e ? atoi(e) : 0;
     }();
     a.abl = abl;
-    // every workgroup resident at once (the tile order is deadlock-free only then)
+    // one round of resident workgroups (the ticket order needs none of them co-resident; more
+    // workgroups than fit would only queue behind the first round)
     static const int resident = [] {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
@@ -2005,6 +2027,20 @@ int launch_octs(pano_ctx *ctx, int o_a, int o_b, int n, int nl, bool full) {
         blur_octs<<<grid, kOctsThreads, 0, ctx->stream>>>(a);
     }
     PANO_LAUNCH_CHECK(ctx, "blur_octs");
+    if (!ctx->capturing) {
+        // the sticky spin time-out flag (sync[1]): a set flag means some tile read its source
+        // rows before they were complete, so the planes are wrong -- an error, never silent.
+        // (With the ticket order a time-out needs a fault elsewhere; inside a graph capture the
+        // flag is checked by the next eager launch.)
+        int flag = 0;
+        PANO_HIP(ctx, hipMemcpyAsync(&flag, ctx->octs_sync + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (flag) {
+            PANO_HIP(ctx, hipMemsetAsync(ctx->octs_sync + 1, 0, sizeof(int), ctx->stream));
+            return pano_fail(ctx, PANO_E_HIP, "blur_octs: a tile timed out waiting for its source rows "
+                                              "(persistent octaves; pyramid invalid)");
+        }
+    }
     return PANO_OK;
 }
 
@@ -2329,12 +2365,14 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
     // 39 against ~28 -- the chain of 11 dependent levels costs one tile's latency each either
     // way, and a resident tile loop (poll, sc1 staging, drain, count) has the longer latency:
     // with no waits at all (PANO_OCTS_ABL=1) the launch still takes 154 us.  So off by default.
-    // Exclusive device only: the tile order is deadlock-free only with every workgroup of the
-    // launch resident, so beside another context's kernels (pipeline.StitchPool) waiting tiles
-    // run into their spin time-out (measured: 60-69 ms per pooled step) and read stale rows.
+    // Round 5 dealt its tiles by block index, which is deadlock-free only with every workgroup
+    // resident: beside another context's kernels (pipeline.StitchPool) waiting tiles ran into
+    // their spin time-out (60-69 ms per pooled step) and read stale rows.  Tiles are now claimed
+    // by an atomic ticket in dependency order (no co-residency needed), and an eager launch
+    // reads the sticky time-out flag back and fails with PANO_E_HIP if it was ever set.
     const char *octs_env = getenv("PANO_BLUR_OCTS");
     const int octs_a = octs_env ? atoi(octs_env) : 0;
-    const bool octs_on = octs_a >= 1 && !chain_on && !cas_taps && pair_mask == 0 && oct_fork < 0 && !tail_main &&
+    const bool octs_on = octs_a >= 1 && !chain_on && !cas_taps && pair_mask == 0 && oct_fork < 0 &&
                          o_side == o_tail && octs_fits(ctx, octs_a, o_tail, nl, tl);
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];

@@ -361,6 +361,10 @@ def rank_band_launch(stitcher, cyl, colnz, gathered, pair_counts, f0, graph=Fals
     npin = nhead + 64 * world                    # + the gathered layout table (run_rank)
     pin = st._buf.get("band_pin")
     if pin is None or pin.numel() < npin:
+        if pin is not None and st._graphs:
+            # graphs captured under an earlier key copy their head into the old block: drop
+            # them (the key below also carries the pinned address)
+            st.release_graphs()
         pin = torch.empty(max(npin, 4096), dtype=torch.uint8, pin_memory=True)
         st._buf["band_pin"] = pin
 
@@ -383,7 +387,8 @@ def rank_band_launch(stitcher, cyl, colnz, gathered, pair_counts, f0, graph=Fals
 
     if graph:
         key = ("rank_band", cyl.data_ptr(), colnz.data_ptr(), tuple(cyl.shape), gathered.data_ptr(),
-               tuple(pair_counts), f0, st.method, Hcap, Wcap, res.data_ptr(), canvas.data_ptr())
+               tuple(pair_counts), f0, st.method, Hcap, Wcap, res.data_ptr(), canvas.data_ptr(),
+               pin.data_ptr())
         st._replay(key, seg)
     else:
         seg()

@@ -413,6 +413,10 @@ class Stitcher:
         nhead = off_plan + 32
         pin = self._buf.get("head_pin" + sfx)
         if pin is None or pin.numel() < nhead:
+            if pin is not None and self._graphs:
+                # graphs captured under an earlier key copy their head into the old block:
+                # drop them (the key below also carries the pinned address)
+                self.release_graphs()
             pin = T.empty(max(nhead, 4096), dtype=T.uint8, pin_memory=True)
             self._buf["head_pin" + sfx] = pin
         self._head_np = pin.numpy()
@@ -434,7 +438,7 @@ class Stitcher:
             "planned", frames_dev.data_ptr(), tuple(frames_dev.shape),
             tuple(float(f) for f in np.asarray(focals, np.float64)), self.method, self.match,
             bytes(self.params), self.cap, self.max_points, self.ransac_thr, self.desc_thresh,
-            self.ratio, res.data_ptr(), canvas.data_ptr())
+            self.ratio, res.data_ptr(), canvas.data_ptr(), pin.data_ptr())
         ent = self._graph_entry(key) if self._graph_mode else None
         if ent is not None:       # replay on the caller's stream and wait: one library call
             cur = self._raw_stream()
