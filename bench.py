@@ -441,7 +441,7 @@ def main():
     # of the cropped panorama inside every step (N = 1; reported beside `value`, never as it)
     pcie = jpg = None
     if world == 1:
-        pcie = pcie_inclusive(st, frames, dev, focals, margin, args.steps, args.graph, mpx)
+        pcie = pcie_inclusive(st, frames, dev, focals, margin, args.steps, args.graph, mpx, pool)
         if args.workload in ("parrington", "grail") and args.scaling == "weak":
             jpg = jpeg_inclusive(st, args.workload, dev, focals, margin, args.steps, args.graph, mpx)
 
@@ -658,7 +658,7 @@ def weak_laps_secondary(args, rank, world):
                     "assembled on rank 0 per step"}
 
 
-def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx):
+def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx, pool=None):
     """Host-to-host stitch rate: per step, the uint8 frames go pinned host -> HBM (into the
     resident input buffer), the stitch runs, and the crop's canvas rows come back to pinned
     host memory in one contiguous copy (the panorama is a view of them, as the device result
@@ -694,12 +694,34 @@ def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx):
         host_out[:flat.numel()].copy_(flat, non_blocking=True)
         cur.synchronize()
     el = (time.perf_counter() - t0) / steps
-    return {"value": round(mpx / el, 3), "unit": "Mpx/s", "ms_per_step": round(el * 1e3, 4),
-            "includes": "pinned H2D of the uint8 frames + stitch + pinned D2H of the crop's canvas "
-                        "rows, per step (SURVEY 8(d) wall, JPEG I/O excluded)",
-            "h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
-            "bytes_h2d": int(host_in.numel()), "bytes_d2h": int(flat.numel()),
-            "panorama_bytes": int(pano.numel())}
+    out = {"value": round(mpx / el, 3), "unit": "Mpx/s", "ms_per_step": round(el * 1e3, 4),
+           "includes": "pinned H2D of the uint8 frames + stitch + pinned D2H of the crop's canvas "
+                       "rows, per step (SURVEY 8(d) wall, JPEG I/O excluded)",
+           "h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
+           "bytes_h2d": int(host_in.numel()), "bytes_d2h": int(flat.numel()),
+           "panorama_bytes": int(pano.numel())}
+    if pool is not None:
+        # the same host-to-host stitches through the pool: each item's frames go pinned host ->
+        # its member's staging buffer and its panorama -> pinned host on that member's stream,
+        # so one member's PCIe legs overlap the other members' stitches (StitchPool.run_sequence
+        # to_host); the last panorama is checked byte for byte against the device one
+        ref = np.ascontiguousarray(pano.cpu().numpy())
+        for _ in pool.run_sequence([(host_in, focals)] * (2 * len(pool.members) + 2), margin=margin, to_host=True):
+            pass
+        torch.cuda.synchronize()
+        last = None
+        t0 = time.perf_counter()
+        for r in pool.run_sequence([(host_in, focals)] * steps, margin=margin, to_host=True):
+            last = r.host
+        torch.cuda.synchronize()
+        el_p = (time.perf_counter() - t0) / steps
+        out["pooled"] = {"value": round(mpx / el_p, 3), "unit": "Mpx/s", "ms_per_step": round(el_p * 1e3, 4),
+                         "form": f"StitchPool.run_sequence(to_host=True), {len(pool.members)} contexts: "
+                                 "per stitch pinned H2D of the frames and pinned D2H of the panorama "
+                                 "on the member's stream, overlapping the other members' stitches",
+                         "host_panorama_equals_device": bool(last is not None and last.shape == ref.shape
+                                                             and (last == ref).all())}
+    return out
 
 
 def jpeg_inclusive(st, name, dev, focals, margin, steps, graph, mpx):

@@ -284,6 +284,30 @@ def test_stitch_pool_matches_run(gpu, parrington, contexts):
     pool.release_graphs()
 
 
+def test_stitch_pool_host_to_host(gpu, parrington):
+    """StitchPool with frames in pinned host memory and to_host=True (SURVEY 8(d) wall: host
+    frames in, host panorama out): every item is uploaded and its panorama downloaded on its
+    member's stream; each host panorama equals run()'s byte for byte, also for two distinct
+    host frame sets interleaved."""
+    import torch
+    from vfx_image_stitching_amd.pipeline import StitchPool, Stitcher
+    names, frames, focals, margin = parrington
+    st = Stitcher("sift")
+    sets = [np.roll(frames, k, axis=0) for k in (0, 3)]
+    fsets = [list(np.roll(np.asarray(focals), k)) for k in (0, 3)]
+    want = [st.run(st.upload(fr), fo, margin=margin).panorama.cpu().numpy().copy() for fr, fo in zip(sets, fsets)]
+    st.release_graphs()
+    host = [torch.from_numpy(np.ascontiguousarray(fr)).pin_memory() for fr in sets]
+    pool = StitchPool("sift", contexts=2)
+    order = [0, 0, 1, 0, 1, 1, 0, 1]
+    n = 0
+    for k, r in zip(order, pool.run_sequence([(host[k], fsets[k]) for k in order], margin=margin, to_host=True)):
+        np.testing.assert_array_equal(r.host, want[k], err_msg=f"item {n}")
+        n += 1
+    assert n == len(order)
+    pool.release_graphs()
+
+
 def test_persistent_octaves_under_pool(gpu, parrington, monkeypatch):
     """blur_octs (PANO_BLUR_OCTS=1) inside a 2-context StitchPool: the two members' kernels share
     the device, so not every workgroup of a persistent launch is resident.  Tiles are claimed by

@@ -104,6 +104,34 @@ def test_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl, api):
                 assert np.array_equal(out.cpu().numpy(), ref), (o, l, dog)
 
 
+@pytest.mark.parametrize("hw,n", [((203, 301), 5), ((64, 97), 40), ((37, 53), 76)])
+def test_pyramid_odd_sizes_bit_exact(st_sift, hw, n):
+    """Every level of the full pyramid on odd frame sizes against the oracle (gray -> x2
+    INTER_LINEAR -> blur, levels, DoG): partial and edge tiles of the base's patch staging
+    (reflection at all four edges, the right / bottom clamp of the bilinear map).  n frames so
+    the base plane has >= 300 64 x 64 tiles per batch (the 64-wide tile kernel, not the 32 x 32
+    small-plane form); the first and last frames are checked."""
+    from vfx_image_stitching_amd import _lib
+    import torch
+    rng = np.random.default_rng(hw[0])
+    frames = rng.integers(0, 256, (n,) + hw + (3,), dtype=np.uint8)
+    dev = torch.from_numpy(frames).to(st_sift.device)
+    ctx = st_sift.ctx
+    ctx.check(ctx.lib.pano_sift_pyramid(ctx.h, _lib.ptr(dev), n, hw[0], hw[1], ctypes.byref(st_sift.params)))
+    for fi in (0, n - 1):
+        base = osift.base_image(osift.to_gray_f32(frames[fi]))
+        gp = osift.gaussian_pyramid(base, osift.n_octaves(base.shape), osift.level_sigmas())
+        dp = osift.dog_pyramid(gp)
+        for o in range(len(gp)):
+            h, w = ctypes.c_int32(), ctypes.c_int32()
+            ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(h), ctypes.byref(w), None))
+            for dog, levels in ((0, gp[o]), (1, dp[o])):
+                for l, ref in enumerate(levels):
+                    out = torch.empty((h.value, w.value), dtype=torch.float32, device=st_sift.device)
+                    ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, fi, o, l, dog, _lib.ptr(out)))
+                    assert np.array_equal(out.cpu().numpy(), ref), (hw, fi, o, l, dog)
+
+
 def test_fused_chain_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl, monkeypatch):
     """The fused level chains (PANO_BLUR_CHAIN=1: base+1+2 / 1+2 and 3+4+5 per octave in one
     launch each) give every level and DoG of the full pyramid bit for bit."""

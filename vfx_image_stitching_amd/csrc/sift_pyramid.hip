@@ -274,6 +274,76 @@ __device__ __forceinline__ void stage_base_interior(const LoadArgs &la, int f, i
     }
 }
 
+// Every tile of MODE_BASE (interior and edge alike): the gray source rows / columns the
+// tile's reflected x2 INTER_LINEAR window reads form one contiguous patch (lin_map is monotone
+// and BORDER_REFLECT_101 folds the window back inside [0, H) x [0, W)), loaded once into LDS as
+// floats -- all of a thread's byte loads issued before its LDS stores -- then every staged
+// element is Stager<MODE_BASE>::get's f32 bilinear expression over four LDS reads at its own
+// (clamped) source indices.  Replaces, for the edge tiles (a third of parrington's octave-0
+// tiles), stage_tile's four global byte loads and f64 row map per element.
+template <int R, int NTHR, int TYT = TY>
+__device__ __forceinline__ void stage_base_patch(const LoadArgs &la, int f, int H, int W, int x0, int y0,
+                                                 int ih, int iw, int IWP, float *t, float *patch) {
+    static_assert((TYT + 2 * R) / 2 + 3 <= kPatchR && (TX + 2 * R) / 2 + 3 <= kPatch, "patch capacity");
+    const uint8_t *fr = la.gray + (size_t)f * la.sh * la.sw;
+    int p0, pl, q0, ql, u;
+    float w_unused;
+    lin_map(max(y0 - R, 0), la.sh, p0, u, w_unused);                  // patch rows [p0, pl]
+    lin_map(min(y0 - R + ih - 1, H - 1), la.sh, u, pl, w_unused);
+    lin_map(max(x0 - R, 0), la.sw, q0, u, w_unused);                  // patch columns [q0, ql]
+    lin_map(min(x0 - R + iw - 1, W - 1), la.sw, u, ql, w_unused);
+    const int np = pl - p0 + 1, nq = ql - q0 + 1;
+    constexpr int MAXP = (kPatchR * kPatch + NTHR - 1) / NTHR;
+    uint8_t v[MAXP];
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) {
+        const int i = (int)threadIdx.x + NTHR * k, r = i / kPatch, c = i - r * kPatch;
+        v[k] = (r < np && c < nq) ? fr[(size_t)(p0 + r) * la.sw + q0 + c] : (uint8_t)0;
+    }
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) {
+        const int i = (int)threadIdx.x + NTHR * k, r = i / kPatch, c = i - r * kPatch;
+        if (r < np && c < nq) patch[r * kPatchP + c] = (float)v[k];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int NW = NTHR / 64;
+    // per-lane columns (lane, 64 + lane): patch columns of c0, c1 and the weight of c1
+    int cA0, cA1, cB0, cB1;
+    float wA, wB;
+    {
+        int a0, a1;
+        lin_map(reflect_fast(x0 - R + min(lane, iw - 1), W), la.sw, a0, a1, wA);
+        cA0 = a0 - q0;
+        cA1 = a1 - q0;
+        const int xb = 64 + lane < iw ? 64 + lane : min(lane, iw - 1);
+        lin_map(reflect_fast(x0 - R + xb, W), la.sw, a0, a1, wB);
+        cB0 = a0 - q0;
+        cB1 = a1 - q0;
+    }
+    for (int ty = wv; ty < ih; ty += NW) {
+        int r0, r1;
+        float wy;
+        lin_map(reflect_fast(y0 - R + ty, H), la.sh, r0, r1, wy);
+        const float *P0 = patch + (r0 - p0) * kPatchP, *P1 = patch + (r1 - p0) * kPatchP;
+        if (lane < iw) {
+            const float g00 = P0[cA0], g01 = P0[cA1], g10 = P1[cA0], g11 = P1[cA1];
+            const float wx0 = 1.0f - wA;
+            const float h0 = g00 * wx0 + g01 * wA;
+            const float h1 = g10 * wx0 + g11 * wA;
+            t[ty * IWP + lane] = h0 * (1.0f - wy) + h1 * wy;
+        }
+        if (64 + lane < iw) {
+            const float g00 = P0[cB0], g01 = P0[cB1], g10 = P1[cB0], g11 = P1[cB1];
+            const float wx0 = 1.0f - wB;
+            const float h0 = g00 * wx0 + g01 * wB;
+            const float h1 = g10 * wx0 + g11 * wB;
+            t[ty * IWP + 64 + lane] = h0 * (1.0f - wy) + h1 * wy;
+        }
+    }
+}
+
 // cvtColor(BGR2GRAY) of every frame, 4 pixels per thread (sift_impl.py:27-28).
 // zp / zn: a word block to zero in passing (the keypoint stage's counters, sift_kp_counters)
 __global__ void __launch_bounds__(256)
@@ -440,6 +510,11 @@ constexpr int tall_rows(int NT) { return ((128 - (NT - 1)) / 8) * 8; }
 // bound: blur_fast<..., 32, 256> uses 32 x 32 tiles of 256 threads with 8 row-pass and 4
 // column-pass outputs per thread -- a quarter of the serial FMA chain per thread and 4x the
 // workgroups of the 64 x 64 form.
+#ifndef PANO_BASE_PATCH
+#define PANO_BASE_PATCH 1   // 0: round-5 base staging (patch for interior tiles only) for A/B
+#endif
+constexpr bool base_patch = PANO_BASE_PATCH != 0;
+
 template <int MODE, int NT, int TYT = TY, int TXT = TX, int NTHR = 512>
 __global__ void __launch_bounds__(NTHR, 6)
 blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
@@ -461,6 +536,8 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
         for (int i = tid; i < (TYT + 2 * R) * IWP; i += NTHR) tin[i] = (float)(i & 255);
     } else if (MODE == MODE_LEVEL && (W & 3) == 0 && x0 >= R && y0 >= R && x0 + TXT + R <= W && y0 + TYT + R <= H)
         stage_interior<R, NTHR, TYT, TXT>(la.src + (size_t)f * H * W, W, x0, y0, IWP, tin);
+    else if (TXT == TX && MODE == MODE_BASE && base_patch)
+        stage_base_patch<R, NTHR, TYT>(la, f, H, W, x0, y0, ih, iw, IWP, tin, tin + (TYT + 2 * R) * IWP);
     else if (TXT == TX && MODE == MODE_BASE && x0 - R >= 2 && y0 - R >= 2 && x0 + TX + R <= W - 2 &&
              y0 + TYT + R <= H - 2)
         stage_base_interior<R, NTHR, TYT>(la, f, x0, y0, IWP, tin, tin + (TYT + 2 * R) * IWP);

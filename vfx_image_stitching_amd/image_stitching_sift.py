@@ -2,8 +2,9 @@
 
 Same function names and signatures; ``run_panorama`` takes its three interactive answers
 as arguments.  compute_shift_sift (image_stitching_sift.py:52-83) extracts both frames'
-features in one batched pano_sift launch, matches with the fp32 MFMA distance GEMM and
-votes the translation on the GPU.
+features in one batched pano_sift_u8 launch (byte descriptors), matches with the exact i8
+MFMA distance GEMM (pano_match_u8: v_mfma_i32_32x32x32_i8 on the descriptor bytes - 128,
+integer distances, first-index ties) and votes the translation on the GPU.
 """
 from __future__ import annotations
 

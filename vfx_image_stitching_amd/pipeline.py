@@ -54,6 +54,8 @@ class StitchResult:
     records: np.ndarray                # PAIR_NP records
     bbox: tuple                        # (y0, y1, x0, x1) crop rows/cols, inclusive
     timings: dict = field(default_factory=dict)
+    host: "object" = None              # StitchPool.run_sequence(to_host=True): the panorama in
+                                       # pinned host memory (numpy view)
 
 
 def drift_correct(shifts):
@@ -518,15 +520,19 @@ class Stitcher:
         items = list(items)
         T = self.torch
         inflight = None                  # (index, slot, event, replay state)
-        shared = len({(f.data_ptr(), tuple(f.shape)) for f, _ in items}) <= 1
+        # host items (pinned uint8 frames, SURVEY 8(d)'s wall: frames on the host): uploaded into
+        # the slot's staging buffer on the stream, right before the slot's graph replays
+        on_host = any(f.device.type == "cpu" for f, _ in items)
+        shared = not on_host and len({(f.data_ptr(), tuple(f.shape)) for f, _ in items}) <= 1
+        dev = T.device("cuda", self.device) if isinstance(self.device, int) else T.device(self.device)
 
         def src_of(i):
             frames_dev = items[i][0]
             if shared:
                 return frames_dev
             stg = self._stage.get(i % 2)
-            if stg is None or stg.shape != frames_dev.shape or stg.device != frames_dev.device:
-                stg = self._stage[i % 2] = T.empty_like(frames_dev)
+            if stg is None or stg.shape != frames_dev.shape or stg.dtype != frames_dev.dtype:
+                stg = self._stage[i % 2] = T.empty(frames_dev.shape, dtype=frames_dev.dtype, device=dev)
             return stg
 
         def launch(i):
@@ -775,8 +781,15 @@ class StitchPool:
         """Frames to the device (one buffer every member reads)."""
         return self.members[0].upload(frames)
 
-    def run_sequence(self, items, margin: int = 15):
-        """Generator over StitchResults of items ((frames_dev, focals) pairs) in order."""
+    def run_sequence(self, items, margin: int = 15, to_host: bool = False):
+        """Generator over StitchResults of items ((frames, focals) pairs) in order.
+
+        Host-to-host form (SURVEY 8(d)'s wall: decoded frames on the host -> cropped panorama on
+        the host): items whose frames are pinned host tensors are uploaded on their member's
+        stream right before its stitch, and with to_host=True every panorama is copied to a
+        pinned host buffer on the same stream (``result.host``, a numpy view valid until the
+        member's next result, k items later).  The copies of one member overlap the other
+        members' stitches on the device, so the PCIe legs leave the per-stitch rate."""
         T = self.torch
         items = list(items)
         k = len(self.members)
@@ -787,11 +800,24 @@ class StitchPool:
         for m, (st, s) in enumerate(zip(self.members, self.streams)):
             with T.cuda.stream(s):
                 gens.append(st.run_sequence(items[m::k], margin=margin))
+        pins = [None] * k
         try:
             for i in range(len(items)):
                 m = i % k
                 with T.cuda.stream(self.streams[m]):
                     r = next(gens[m])
+                    if to_host:
+                        pano = r.panorama
+                        pin = pins[m]
+                        if pin is None or pin.numel() < pano.numel():
+                            pin = pins[m] = T.empty(max(pano.numel(), 1 << 20), dtype=T.uint8, pin_memory=True)
+                        hv = pin[:pano.numel()].view(pano.shape)
+                        hv.copy_(pano, non_blocking=True)
+                        ev = T.cuda.Event()
+                        ev.record(self.streams[m])
+                if to_host:
+                    ev.synchronize()
+                    r.host = hv.numpy()
                 yield r
         finally:
             for g, s in zip(gens, self.streams):
