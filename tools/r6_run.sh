@@ -18,6 +18,9 @@ for st in ${STAGES:-tests}; do
     timeout -k 10 ${TLIM:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1
     rc=$?; echo "pytest rc=$rc"; tail -n 3 $O/pytest.txt
     [ $rc -ne 0 ] && exit $rc ;;
+  t2)   # a second test selection (TESTS2) whose failure is reported but does not end the call
+    timeout -k 10 ${TLIM2:-300} python -u -m pytest ${TESTS2} -m gpu -x -v --timeout ${TTO2:-100} --timeout-method thread > $O/pytest2.txt 2>&1
+    echo "pytest2 rc=$?"; tail -n 40 $O/pytest2.txt | cut -c1-300 ;;
   pmc)
     for w in ${WORKS:-parrington synthetic}; do
       D=$O/pmc_$w; rm -rf $D; mkdir -p $D

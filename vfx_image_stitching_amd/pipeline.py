@@ -7,16 +7,17 @@ rectangle crop.
 
 Here every stage runs as libpano kernels over the whole frame batch, on one HIP stream:
 
-    pano_cylindrical   all frames, one launch pair
-    pano_sift/harris   all frames once (the reference recomputes interior frames for both
-                       of their pairs; features are a pure function of the frame)
-    pano_match         all pairs (fp32 MFMA distance GEMM for SIFT)
+    pano_cylindrical   all frames, one launch (cyl_tile)
+    pano_sift_u8 / pano_harris   all frames once (the reference recomputes interior frames for
+                       both of their pairs; features are a pure function of the frame)
+    pano_match_u8      all pairs (exact i8 MFMA distance GEMM on the descriptor bytes for SIFT;
+                       pano_match's bf16 / f32 MFMA forms for f32 descriptors)
     pano_pair_shifts   all pairs (match filter + exhaustive vote RANSAC)
-      -- host: 17 records come back (~1 KB); drift correction + composite plan (C) --
-    pano_composite_bbox  pre-sized canvas; one parallel pass when no column is covered by
-                       three frames (else the per-step fold), crop box fused (16 B back)
-
-Two small device->host reads are the only synchronisation points.
+    pano_plan_composite_device   drift correction + composite plan on the GPU, then the
+                       planned composite into a capacity-sized canvas, crop box fused
+      -- one pinned copy of the records, crop box and plan header (~1.3 KB): the one host
+         read per stitch; the host-planned form (pano_plan_composite + pano_composite_bbox,
+         two reads) runs when the device plan reports an overflow or a three-frame column --
 """
 from __future__ import annotations
 
