@@ -155,53 +155,6 @@ def test_fused_chain_pyramid_bit_exact(st_sift, parr_dev, parrington_cyl, monkey
                     assert np.array_equal(out.cpu().numpy(), ref), (fi, o, l, dog)
 
 
-def _full_pyramid(st, frames):
-    """Every Gaussian and DoG plane of pano_sift_pyramid over `frames` (device u8 BGR)."""
-    from vfx_image_stitching_amd import _lib
-    import torch
-    ctx = st.ctx
-    n = frames.shape[0]
-    ctx.check(ctx.lib.pano_sift_pyramid(ctx.h, _lib.ptr(frames), n, frames.shape[1], frames.shape[2],
-                                        ctypes.byref(st.params)))
-    out = {}
-    o = 0
-    while True:
-        h, w, no = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-        ctx.check(ctx.lib.pano_sift_level_shape(ctx.h, o, ctypes.byref(h), ctypes.byref(w), ctypes.byref(no)))
-        for fi in range(n):
-            for dog, nl in ((0, 6), (1, 5)):
-                for l in range(nl):
-                    t = torch.empty((h.value, w.value), dtype=torch.float32, device=st.device)
-                    ctx.check(ctx.lib.pano_sift_copy_level(ctx.h, fi, o, l, dog, _lib.ptr(t)))
-                    out[(fi, o, l, dog)] = t.cpu().numpy()
-        o += 1
-        if o >= no.value:
-            return out
-
-
-@pytest.mark.parametrize("case", ["parrington", "odd"])
-def test_persistent_octaves_bit_exact(st_sift, parr_dev, case, monkeypatch):
-    """The persistent octave launch (blur_octs, PANO_BLUR_OCTS=k: octaves k .. the tail in one
-    launch, tiles waiting on their source rows) gives every plane of the full pyramid bit for
-    bit as the level-by-level launches (PANO_BLUR_OCTS=0), which test_pyramid_bit_exact pins
-    to the oracle; twice in a row (the counters re-zeroed by the launch itself).  Odd sizes:
-    partial tiles, W % 4 != 0 (4-byte write-through stores)."""
-    import torch
-    dev, cyl, _ = parr_dev
-    if case == "parrington":
-        frames = cyl[:6].contiguous()
-    else:
-        rng = np.random.default_rng(11)
-        frames = torch.from_numpy(rng.integers(0, 256, (3, 203, 301, 3), dtype=np.uint8)).to(st_sift.device)
-    monkeypatch.setenv("PANO_BLUR_OCTS", "0")
-    ref = _full_pyramid(st_sift, frames)
-    for start in ("1", "2", "1"):
-        monkeypatch.setenv("PANO_BLUR_OCTS", start)
-        got = _full_pyramid(st_sift, frames)
-        for key, r in ref.items():
-            assert np.array_equal(got[key], r), (start, key)
-
-
 # ------------------------------------------------------------------ S5..S9
 def _gpu_feats(st, cyl):
     from vfx_image_stitching_amd import _lib

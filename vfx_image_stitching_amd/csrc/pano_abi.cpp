@@ -129,7 +129,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->ev_sort_join) (void)hipEventDestroy(ctx->ev_sort_join);
     void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
-                    ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->octs_sync, ctx->match_sync, ctx->sel_sync, ctx->descraw, ctx->cyl_sync};
+                    ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->match_sync, ctx->sel_sync, ctx->descraw, ctx->cyl_sync};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->jscratch) (void)hipFree(ctx->jscratch);
@@ -163,7 +163,7 @@ int pano_ctx_release_scratch(pano_ctx *ctx) {
         {&ctx->jscratch, &ctx->jscratch_bytes},          {(void **)&ctx->raw_sorted, &dummy},
         {(void **)&ctx->descraw, &ctx->descraw_bytes},   {&ctx->cyl_sync, &ctx->cyl_sync_bytes},
         // arrival counters: zeroed when (re)allocated, so a released one comes back zeroed
-        {(void **)&ctx->octs_sync, &ctx->octs_sync_bytes}, {(void **)&ctx->match_sync, &ctx->match_sync_bytes},
+        {(void **)&ctx->match_sync, &ctx->match_sync_bytes},
         {(void **)&ctx->sel_sync, &ctx->sel_sync_bytes},
     };
     for (const Slot &s : slots) {

@@ -24,7 +24,7 @@ constexpr int kCntStride = 32;
 #define PANO_ORI_BINS 36
 
 // Cross-workgroup hand-off of the last-arriver folds (dist_i8 -> reduce, pair_votes ->
-// select, cyl_tile<true> -> column flags, blur_octs row counters): the partials are stored at
+// select, cyl_tile<true> -> column flags): the partials are stored at
 // agent scope, every wave drains them (s_waitcnt vmcnt(0)) before the barrier, one lane counts
 // the workgroup in with an agent-scope add, and the last arriver reads the partials with
 // agent-scope loads.  On gfx950 (and gfx942) agent-scope relaxed stores and loads bypass the
@@ -115,7 +115,6 @@ struct pano_ctx {
     float *taps = nullptr;               // device Gaussian taps (f32), per level [L][PANO_MAX_TAPS]
     float taps_host[PANO_MAX_LEVELS * PANO_MAX_TAPS];    // what *taps holds
     bool taps_valid = false;
-    int32_t *octs_sync = nullptr; size_t octs_sync_bytes = 0;   // blur_octs row counters (zeroed)
     int32_t *match_sync = nullptr; size_t match_sync_bytes = 0; // dist_i8 fold arrival counters (zeroed)
     int32_t *sel_sync = nullptr; size_t sel_sync_bytes = 0;     // pair_votes fold arrival counters (zeroed)
     void *cyl_sync = nullptr; size_t cyl_sync_bytes = 0;        // cyl_tile column flags + strip counters (zeroed)

@@ -1739,388 +1739,6 @@ int launch_pair(pano_ctx *ctx, const LoadArgs &la, float *out1, float *dog1, flo
     return PANO_E_UNSUPPORTED;
 }
 
-// ------------------------------------------------------------------ persistent octaves
-// Octaves o_a .. o_tail - 1 (parrington: 1-3, 1080p: 1-5) in ONE launch instead of one launch
-// per level.  Each of those levels is a few hundred to a few thousand 32 x 32 tiles, so a
-// per-level launch costs its wave fill and drain (~5-15 us) more than its work, and the
-// octaves run back to back.  Here workgroups claim tiles by an atomic ticket in a fixed order
-// (phases (octave, level) sorted by dependency depth, octave o + 1's level 1 right after
-// octave o's level nl - 3), and a tile waits only for the tile ROWS of its source
-// that its halo reads: rows ty - 1 .. ty + 1 of level l - 1, or for level 1 the INTER_NEAREST
-// source rows in octave o - 1's level nl - 3.  Finished tiles are counted per (octave, level,
-// frame, tile row).  Hand-off across the 8 XCDs' private L2s (MI355X guide, visibility, R1):
-// the Gaussian planes read inside the launch are stored write-through (sc1) and drained
-// (s_waitcnt vmcnt(0) in every wave, barrier) before one lane's device-scope add to the row
-// counter, and EVERY load of them is an sc1 load -- no release or acquire fence.  DoG planes
-// and level-0 copies are read only by later launches: plain stores.  Per output the arithmetic
-// is blur_fast's (row_seg / col_seg: sequential fma in tap order), hence bit-identical.
-constexpr int kOctsT = 32;                         // tile edge
-constexpr int kOctsThreads = 256;
-constexpr int kOctsMaxOct = 8;
-constexpr int kOctsRows = 64;                      // counter slots per plane: ceil(H / 32) <= 64
-constexpr int kOctsMaxPhase = kOctsMaxOct * 5;
-constexpr int kOctsRMax = 13;                      // widest reference kernel: 27 taps
-constexpr int kOctsIWP = (kOctsT + 2 * kOctsRMax) | 1;
-constexpr int kOctsOP = kOctsT + 1;                // output staging pitch
-constexpr int kOctsSync0 = 16;                     // sync words before the counters
-constexpr long long kOctsSpinTicks = 20000000;     // 0.2 s of the 100 MHz clock: give up, flag
-constexpr int kOctsTaps[6] = {0, 11, 13, 17, 21, 27};   // compiled tap counts, levels 1-5
-
-typedef __attribute__((address_space(1))) float g_f32;
-typedef __attribute__((address_space(1))) int g_i32;
-
-struct OctsArgs {
-    const float *prev;           // G[o_a - 1][nl - 3]: level-1 source of the first octave
-    int ph, pw;
-    int n, nl, n_oct, nphase;
-    long long total;             // items (tiles of every phase)
-    int H[kOctsMaxOct], W[kOctsMaxOct], nty[kOctsMaxOct], ntx[kOctsMaxOct];
-    float *G[kOctsMaxOct][PANO_MAX_LEVELS];   // null: plane not kept (level 0 / top unless full)
-    float *D[kOctsMaxOct][PANO_MAX_LEVELS];
-    const float *taps;           // [level][PANO_MAX_TAPS] (ctx->taps)
-    int ph_o[kOctsMaxPhase], ph_l[kOctsMaxPhase];
-    long long ph_start[kOctsMaxPhase + 1];
-    int *sync;                   // [0] exited workgroups, [1] spin time-outs (sticky), [2] the
-                                 // next ticket (tile claim order), counters
-                                 // from kOctsSync0: [n_oct][nl][n][kOctsRows] finished tiles
-    int ncnt;                    // counter words
-    int abl;                     // timing ablations (PANO_OCTS_ABL, wrong planes): 1 no waits,
-                                 // 2 plain loads, 4 no store drain, 8 plain G stores
-};
-
-__device__ __forceinline__ float ld_sc1(const float *p) {
-    return __hip_atomic_load((g_f32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Stage the (ih x iw) input tile at (y0 - R, x0 - R), iw <= 64: wave w rows w, w + 4, ...,
-// lane = column, every load sc1.  src: this frame's source plane (sh x sw).
-template <int MODE, int R>
-__device__ __forceinline__ void octs_stage(const float *src, int sh, int sw, double ifx, double ify, int H, int W,
-                                           int x0, int y0, int ih, int iw, float *t, bool plain) {
-    constexpr int RPW = (kOctsT + 2 * R + 3) / 4;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int x = reflect_fast(x0 - R + min(lane, iw - 1), W);
-    int c = x;
-    if constexpr (MODE == MODE_DOWN) {
-        const int tt = (int)floor(x * ifx);
-        c = tt < sw - 1 ? tt : sw - 1;
-    }
-    float v[RPW];
-#pragma unroll
-    for (int k = 0; k < RPW; ++k) {
-        const int ty = wv + 4 * k;
-        if (ty < ih) {
-            int sy = reflect_fast(y0 - R + ty, H);
-            if constexpr (MODE == MODE_DOWN) {
-                sy = (int)floor(sy * ify);
-                sy = sy < sh - 1 ? sy : sh - 1;
-            }
-            v[k] = plain ? src[(size_t)sy * sw + c] : ld_sc1(src + (size_t)sy * sw + c);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < RPW; ++k) {
-        const int ty = wv + 4 * k;
-        if (ty < ih && lane < iw) t[ty * kOctsIWP + lane] = v[k];
-    }
-}
-
-// One 32 x 32 tile of level l (octave index oi) of frame f: blur_fast<MODE, NT, 32, 32, 256>'s
-// passes, G through the output staging tile and 16-byte write-through stores.
-template <int MODE, int NT>
-__device__ __forceinline__ void octs_tile(const float *src, int sh, int sw, int H, int W, float *outp, float *dg,
-                                          float *inc, const float *k, int ty, int tx, float *tin, float *ost, int abl) {
-    constexpr int R = (NT - 1) / 2, T = kOctsT, IWP = kOctsIWP, SR = 8, SC = 4;
-    const int x0 = tx * T, y0 = ty * T;
-    const int tw = min(T, W - x0), th = min(T, H - y0);
-    const int ih = th + 2 * R, iw = tw + 2 * R;
-    const int tid = threadIdx.x;
-    if constexpr (MODE == MODE_DOWN) {
-        const double ifx = 1.0 / ((double)W / sw), ify = 1.0 / ((double)H / sh);
-        octs_stage<MODE_DOWN, R>(src, sh, sw, ifx, ify, H, W, x0, y0, ih, iw, tin, abl & 2);
-    } else {
-        octs_stage<MODE_LEVEL, R>(src, H, W, 0.0, 0.0, H, W, x0, y0, ih, iw, tin, abl & 2);
-    }
-    __syncthreads();
-    const int nrs = (th + SC - 1) / SC;
-    const bool colw = tid < tw * nrs;
-    const int cxp = colw ? tid % tw : 0, crs = colw ? tid / tw : 0;
-    float cen[SC];
-#pragma unroll
-    for (int j = 0; j < SC; ++j) cen[j] = colw ? tin[(crs * SC + j + R) * IWP + cxp + R] : 0.0f;
-    const int nseg = (tw + SR - 1) / SR;
-    const bool roww = tid < ih * nseg;
-    const int row = roww ? tid % ih : 0, sg = roww ? tid / ih : 0;
-    float ro[SR];
-    if (roww) {
-        float acc[SR];
-        row_seg<NT, SR>(tin + row * IWP + sg * SR, k, acc);
-#pragma unroll
-        for (int j = 0; j < SR; ++j) ro[j] = acc[j];
-    }
-    __syncthreads();
-    if (roww) {
-#pragma unroll
-        for (int j = 0; j < SR; ++j) tin[row * IWP + sg * SR + j] = ro[j];
-    }
-    __syncthreads();
-    if (colw) {
-        float acc[SC];
-        col_seg<NT, SC>(tin + crs * SC * IWP + cxp, IWP, k, acc);
-        float o[SC];
-#pragma unroll
-        for (int j = 0; j < SC; ++j) {
-            o[j] = acc[j];
-            asm volatile("" ::"v"(o[j]));
-        }
-        const int nvalid = th - crs * SC;
-        const size_t g0 = ((size_t)y0 + crs * SC) * W + x0 + cxp;
-#pragma unroll
-        for (int j = 0; j < SC; ++j) {
-            if (j >= nvalid) continue;
-            const size_t gi = g0 + (size_t)j * W;
-            if (dg) dg[gi] = o[j] - cen[j];
-            if (inc) inc[gi] = cen[j];
-            if (outp) ost[(crs * SC + j) * kOctsOP + cxp] = o[j];
-        }
-    }
-    if (outp) {                                  // uniform
-        __syncthreads();
-        const int r = tid >> 3, q = tid & 7;    // row r, columns 4q .. 4q + 3
-        if (r < th && 4 * q < tw) {
-            const float *s = ost + r * kOctsOP + 4 * q;
-            float *plane = outp;
-            if (abl & 8) {
-                for (int c = 0; c < 4 && 4 * q + c < tw; ++c) plane[(size_t)(y0 + r) * W + x0 + 4 * q + c] = s[c];
-            } else if ((W & 3) == 0) {           // tw % 4 == 0: whole quads
-                typedef int v4i __attribute__((ext_vector_type(4)));
-                v4i v;
-                v.x = __float_as_int(s[0]);
-                v.y = __float_as_int(s[1]);
-                v.z = __float_as_int(s[2]);
-                v.w = __float_as_int(s[3]);
-                const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(plane, 0, H * W * 4, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ((y0 + r) * W + x0 + 4 * q) * 4, 0, 16);
-            } else {
-                for (int c = 0; c < 4 && 4 * q + c < tw; ++c)
-                    __hip_atomic_store((g_f32 *)(plane + (size_t)(y0 + r) * W + x0 + 4 * q + c), s[c],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-}
-
-// Lane 0: wait until rows r0 .. r1 of a counter row set reach `need` (bounded spin; a
-// time-out sets the sticky flag sync[1] and returns: wrong planes, never a hung GPU).
-__device__ __noinline__ void octs_wait(const int *cnt, int r0, int r1, int need, int *sync) {
-    const unsigned long long t0 = wall_clock64();
-    for (int r = r0; r <= r1; ++r)
-        while (__hip_atomic_load((g_i32 *)(cnt + r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > (unsigned long long)kOctsSpinTicks) {
-                __hip_atomic_store((g_i32 *)(sync + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return;
-            }
-        }
-}
-
-__global__ void __launch_bounds__(kOctsThreads)
-blur_octs(OctsArgs a) {
-    __shared__ __attribute__((aligned(16))) float tin[(kOctsT + 2 * kOctsRMax) * kOctsIWP];
-    __shared__ float ost[kOctsT * kOctsOP];
-    __shared__ int last;
-    __shared__ int ticket;
-    // Items are claimed by an atomic ticket (sync[2]) in dependency order, not dealt by block
-    // index: every item a tile waits for was claimed earlier by a workgroup that is running, and
-    // the lowest unfinished ticket never waits, so the launch progresses with any number of
-    // its workgroups resident -- beside another context's kernels too (StitchPool).  Round 5's
-    // dealt order (item = block + k * grid) needed the whole grid resident and spun into its
-    // time-out when it was not.
-    for (;;) {
-        if (threadIdx.x == 0)
-            ticket = __hip_atomic_fetch_add((g_i32 *)(a.sync + 2), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const long long it = ticket;
-        if (it >= a.total) break;
-        int p = 0;
-        while (p + 1 < a.nphase && it >= a.ph_start[p + 1]) ++p;
-        const int oi = a.ph_o[p], l = a.ph_l[p];
-        const int per = a.nty[oi] * a.ntx[oi];
-        const long long loc = it - a.ph_start[p];
-        const int f = (int)(loc / per), t = (int)(loc - (long long)f * per);
-        const int ty = t / a.ntx[oi], tx = t - ty * a.ntx[oi];
-        // the source rows this tile's halo reads: level l - 1 rows ty - 1 .. ty + 1, or for
-        // level 1 the INTER_NEAREST rows of octave oi - 1's level nl - 3 (reflections fold
-        // inside the destination range [y0 - R, y0 + 31 + R])
-        int so = oi, sl = l - 1, r0 = max(0, ty - 1), r1 = min(a.nty[oi] - 1, ty + 1);
-        bool wait = true;
-        if (l == 1) {
-            wait = oi > 0;                       // octave o_a: source written before the launch
-            if (wait) {
-                so = oi - 1;
-                sl = a.nl - 3;
-                const int H = a.H[oi], sh = a.H[oi - 1];
-                const double ify = 1.0 / ((double)H / sh);
-                const int ylo = max(0, ty * kOctsT - kOctsRMax), yhi = min(H - 1, ty * kOctsT + kOctsT - 1 + kOctsRMax);
-                r0 = min(sh - 1, (int)floor(ylo * ify)) / kOctsT;
-                r1 = min(sh - 1, (int)floor(yhi * ify)) / kOctsT;
-            }
-        }
-        if (wait && threadIdx.x == 0 && !(a.abl & 1))
-            octs_wait(a.sync + kOctsSync0 + ((so * a.nl + sl) * a.n + f) * kOctsRows, r0, r1, a.ntx[so], a.sync);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler only: loads stay after the poll
-        __syncthreads();
-        fold_acquire();
-        const int H = a.H[oi], W = a.W[oi];
-        const float *src;
-        int sh = H, sw = W;
-        if (l == 1) {
-            sh = oi == 0 ? a.ph : a.H[oi - 1];
-            sw = oi == 0 ? a.pw : a.W[oi - 1];
-            src = oi == 0 ? a.prev : a.G[oi - 1][a.nl - 3];
-        } else {
-            src = a.G[oi][l - 1];
-        }
-        src += (size_t)f * sh * sw;
-        float *outp = a.G[oi][l] ? a.G[oi][l] + (size_t)f * H * W : nullptr;
-        float *dg = a.D[oi][l - 1] + (size_t)f * H * W;
-        float *inc = l == 1 && a.G[oi][0] ? a.G[oi][0] + (size_t)f * H * W : nullptr;
-        const float *k = a.taps + l * PANO_MAX_TAPS;
-        switch (l) {
-            case 1: octs_tile<MODE_DOWN, 11>(src, sh, sw, H, W, outp, dg, inc, k, ty, tx, tin, ost, a.abl); break;
-            case 2: octs_tile<MODE_LEVEL, 13>(src, sh, sw, H, W, outp, dg, inc, k, ty, tx, tin, ost, a.abl); break;
-            case 3: octs_tile<MODE_LEVEL, 17>(src, sh, sw, H, W, outp, dg, inc, k, ty, tx, tin, ost, a.abl); break;
-            case 4: octs_tile<MODE_LEVEL, 21>(src, sh, sw, H, W, outp, dg, inc, k, ty, tx, tin, ost, a.abl); break;
-            default: octs_tile<MODE_LEVEL, 27>(src, sh, sw, H, W, outp, dg, inc, k, ty, tx, tin, ost, a.abl); break;
-        }
-        if (!(a.abl & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its stores landed
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            fold_release();
-            __hip_atomic_fetch_add((g_i32 *)(a.sync + kOctsSync0 + ((oi * a.nl + l) * a.n + f) * kOctsRows + ty), 1,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // (the barrier after the next ticket draw orders this item's reads of `ticket` before
-        // thread 0 overwrites it)
-    }
-    // the last workgroup out re-zeroes the counters and the ticket for the next launch (graph
-    // replays): every other workgroup has drawn its final ticket and finished its polls by then
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add((g_i32 *)a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               (int)gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    for (int i = threadIdx.x; i < a.ncnt; i += kOctsThreads)
-        __hip_atomic_store((g_i32 *)(a.sync + kOctsSync0 + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) {
-        __hip_atomic_store((g_i32 *)(a.sync + 2), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((g_i32 *)a.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Can octaves o_a .. o_b - 1 go to blur_octs?  The reference's level taps (the compiled tap
-// counts), nl == 6, every plane <= kOctsRows tile rows.
-bool octs_fits(const pano_ctx *ctx, int o_a, int o_b, int nl, const Taps *tl) {
-    if (o_a < 1 || o_b <= o_a || o_b - o_a > kOctsMaxOct || nl != 6) return false;
-    for (int l = 1; l < nl; ++l)
-        if (tl[l].n != kOctsTaps[l]) return false;
-    for (int o = o_a; o < o_b; ++o)
-        if ((ctx->oct_h[o] + kOctsT - 1) / kOctsT > kOctsRows || ctx->oct_h[o] < 1 || ctx->oct_w[o] < 1) return false;
-    return true;
-}
-
-int launch_octs(pano_ctx *ctx, int o_a, int o_b, int n, int nl, bool full) {
-    const int no = o_b - o_a;
-    OctsArgs a{};
-    float *G = ctx->pyr, *D = ctx->dog;
-    a.prev = G + ctx->gauss_off[o_a - 1][nl - 3];
-    a.ph = ctx->oct_h[o_a - 1];
-    a.pw = ctx->oct_w[o_a - 1];
-    a.n = n;
-    a.nl = nl;
-    a.n_oct = no;
-    a.taps = ctx->taps;
-    for (int oi = 0; oi < no; ++oi) {
-        const int o = o_a + oi;
-        a.H[oi] = ctx->oct_h[o];
-        a.W[oi] = ctx->oct_w[o];
-        a.nty[oi] = (a.H[oi] + kOctsT - 1) / kOctsT;
-        a.ntx[oi] = (a.W[oi] + kOctsT - 1) / kOctsT;
-        for (int l = 0; l < nl; ++l)
-            a.G[oi][l] = (full || (l > 0 && l < nl - 1)) ? G + ctx->gauss_off[o][l] : nullptr;
-        for (int l = 0; l + 1 < nl; ++l) a.D[oi][l] = D + ctx->dog_off[o][l];
-    }
-    // phases by dependency depth (nl - 3) * oi + l; at equal depth the deeper octave first
-    // (octave o + 1's level 1 is on the critical path, octave o's level nl - 2 is not)
-    long long start = 0;
-    for (int key = 1; key <= (nl - 3) * (no - 1) + nl - 1; ++key)
-        for (int oi = no - 1; oi >= 0; --oi) {
-            const int l = key - (nl - 3) * oi;
-            if (l < 1 || l > nl - 1) continue;
-            a.ph_o[a.nphase] = oi;
-            a.ph_l[a.nphase] = l;
-            a.ph_start[a.nphase] = start;
-            start += (long long)n * a.nty[oi] * a.ntx[oi];
-            ++a.nphase;
-        }
-    a.ph_start[a.nphase] = start;
-    a.total = start;
-    a.ncnt = no * nl * n * kOctsRows;
-    const size_t need = (size_t)(kOctsSync0 + a.ncnt) * sizeof(int);
-    if (need > ctx->octs_sync_bytes) {
-        if (ctx->capturing) return pano_fail(ctx, PANO_E_UNSUPPORTED, "blur_octs counters grown inside a graph capture");
-        if (ctx->octs_sync) {
-            PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            (void)hipFree(ctx->octs_sync);
-            ctx->octs_sync = nullptr;
-            ctx->octs_sync_bytes = 0;
-            ++ctx->generation;
-        }
-        PANO_HIP(ctx, hipMalloc((void **)&ctx->octs_sync, need));
-        PANO_HIP(ctx, hipMemset(ctx->octs_sync, 0, need));      // zero once; each launch re-zeroes
-        ctx->octs_sync_bytes = need;
-    }
-    a.sync = ctx->octs_sync;
-    static const int abl = [] {
-        const char *e = getenv("PANO_OCTS_ABL");
-        return e ? atoi(e) : 0;
-    }();
-    a.abl = abl;
-    // one round of resident workgroups (the ticket order needs none of them co-resident; more
-    // workgroups than fit would only queue behind the first round)
-    static const int resident = [] {
-        int dev = 0, cus = 0, per = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, blur_octs, kOctsThreads, 0);
-        const char *e = getenv("PANO_OCTS_WGS");     // workgroups per CU (cap)
-        const int cap = e ? std::max(1, atoi(e)) : 8;
-        return std::max(1, cus) * std::max(1, std::min(per, cap));
-    }();
-    const unsigned grid = (unsigned)std::min<long long>(a.total, resident);
-    {
-        PanoProf prof_(ctx, PK_BLUR);
-        blur_octs<<<grid, kOctsThreads, 0, ctx->stream>>>(a);
-    }
-    PANO_LAUNCH_CHECK(ctx, "blur_octs");
-    if (!ctx->capturing) {
-        // the sticky spin time-out flag (sync[1]): a set flag means some tile read its source
-        // rows before they were complete, so the planes are wrong -- an error, never silent.
-        // (With the ticket order a time-out needs a fault elsewhere; inside a graph capture the
-        // flag is checked by the next eager launch.)
-        int flag = 0;
-        PANO_HIP(ctx, hipMemcpyAsync(&flag, ctx->octs_sync + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        PANO_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        if (flag) {
-            PANO_HIP(ctx, hipMemsetAsync(ctx->octs_sync + 1, 0, sizeof(int), ctx->stream));
-            return pano_fail(ctx, PANO_E_HIP, "blur_octs: a tile timed out waiting for its source rows "
-                                              "(persistent octaves; pyramid invalid)");
-        }
-    }
-    return PANO_OK;
-}
-
 }  // namespace
 
 // Scalars of S1/S2 exactly as the reference computes them (Python/numpy doubles; glibc
@@ -2434,35 +2052,8 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         return e ? atoi(e) : -1;
     }();
     bool lvl_forked = false;
-    // persistent octaves (blur_octs): octaves octs_a .. o_tail - 1 in one launch, the tail forked
-    // after it.  PANO_BLUR_OCTS (read per call: tests compare both forms): the first octave of
-    // the launch, 0 = off (one launch per level).  Measured on MI355X (graph-
-    // replayed parrington): bit-exact, but slower from every start octave -- octaves 1-3 in
-    // 225-236 us against ~150 us of per-level launches, 2-3 in 81-87 against ~68, octave 3 in
-    // 39 against ~28 -- the chain of 11 dependent levels costs one tile's latency each either
-    // way, and a resident tile loop (poll, sc1 staging, drain, count) has the longer latency:
-    // with no waits at all (PANO_OCTS_ABL=1) the launch still takes 154 us.  So off by default.
-    // Round 5 dealt its tiles by block index, which is deadlock-free only with every workgroup
-    // resident: beside another context's kernels (pipeline.StitchPool) waiting tiles ran into
-    // their spin time-out (60-69 ms per pooled step) and read stale rows.  Tiles are now claimed
-    // by an atomic ticket in dependency order (no co-residency needed), and an eager launch
-    // reads the sticky time-out flag back and fails with PANO_E_HIP if it was ever set.
-    const char *octs_env = getenv("PANO_BLUR_OCTS");
-    const int octs_a = octs_env ? atoi(octs_env) : 0;
-    const bool octs_on = octs_a >= 1 && !chain_on && !cas_taps && pair_mask == 0 && oct_fork < 0 &&
-                         o_side == o_tail && octs_fits(ctx, octs_a, o_tail, nl, tl);
     for (int o = 0; o < o_tail; ++o) {
         const int H = ctx->oct_h[o], W = ctx->oct_w[o];
-        if (octs_on && o == octs_a) {
-            ctx->stream = main_stream;
-            rc = launch_octs(ctx, octs_a, o_tail, n, nl, full);
-            if (rc) return rc;
-            if (o_tail < no) {
-                rc = fork();
-                if (rc) return rc;
-            }
-            break;
-        }
         ctx->stream = o >= o_side && !tail_main ? ctx->side : main_stream;     // side-stream octaves
         const bool fork_lvl = oct_fork >= 0 && o >= oct_fork && o < o_side && nl >= 4 && !chain_ok(o) && !cas_ok(o);
         if (cas_ok(o)) {
