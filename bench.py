@@ -260,6 +260,12 @@ def kernel_bytes(name, st, n_frames, h, w):
     return None, None
 
 
+def progress(msg):
+    """One progress line on stderr (long runs: a line every phase, never on stdout, which holds
+    only the JSON result)."""
+    print(f"[bench rank {os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -315,8 +321,10 @@ def main():
     from vfx_image_stitching_amd import distributed as D
     from vfx_image_stitching_amd.pipeline import Stitcher
 
+    progress(f"workload {args.workload} ({args.scaling}), world {world}")
     frames, focals, margin, (h, w), distinct, counts = workload(args.workload, rank, world, args.scaling)
     n_local = len(frames)
+    progress(f"{n_local} frames ready")
     cap = args.cap or (4096 if args.workload != "synthetic" else 65536)
     st = Stitcher(args.method, cap=cap, match=args.match)
     dev = st.upload(frames)                                   # resident in HBM
@@ -330,6 +338,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    progress("warm-up done")
 
     # pick the dominant kernel from one profiled (untimed) step
     ctx = st.ctx
@@ -377,6 +386,7 @@ def main():
     else:
         ctx.prof_enable(rk)
         ctx.prof_read(rk)                                      # reset
+    progress("timed region")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -434,6 +444,7 @@ def main():
 
     ms_step = el / args.steps * 1e3
     mpx = distinct * h * w / 1e6
+    progress(f"timed: {ms_step:.4f} ms per step; side measurements")
     value = mpx / (el / args.steps)
 
     # SURVEY 8(d) "wall": decoded uint8 frames on the host -> cropped uint8 panorama on the

@@ -41,8 +41,12 @@ for st in ${STAGES:-tests}; do
         echo "r$r [$v] ms_per_step single_context: $ms" | tee -a $O/ab_summary.txt
       done
     done ;;
+  rehearse)   # the N > 1 bench path on this one-GPU box: N ranks on cuda:0 over gloo, no launcher
+    PANO_BENCH_REHEARSE=1 timeout -k 10 ${TLIM_R:-900} python bench.py --gpus ${NR:-2} --steps 3 --warmup 1 > $O/rehearse_n${NR:-2}.txt 2> $O/rehearse_n${NR:-2}.err
+    rc=$?; echo "rehearse rc=$rc"; tail -n 1 $O/rehearse_n${NR:-2}.txt | cut -c1-600; tail -n 3 $O/rehearse_n${NR:-2}.err
+    [ $rc -ne 0 ] && exit $rc ;;
   bench)
-    timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $O/bench.txt 2>&1 || { tail -5 $O/bench.txt; exit 1; }
+    timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $O/bench.txt 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
     tail -1 $O/bench.txt | cut -c1-400 ;;
   prof)
     rm -rf $O/prof
