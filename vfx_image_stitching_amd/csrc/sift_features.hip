@@ -181,6 +181,20 @@ __device__ __forceinline__ uint64_t scan_key(int o, int layer0, int y, int x) {
     return ((uint64_t)(o * 8 + layer0) << 32) | ((uint64_t)y << 16) | (uint64_t)x;
 }
 
+// Extremum cubes (round 6).  extrema_stream holds every extremum's 3 x 3 x 3 DoG neighbourhood
+// in registers when it finds it, so it also writes it out as one 112-byte record ([dz][dy][dx],
+// 27 floats + pad) and localize's first Newton step reads that record instead of nine scattered
+// DoG rows (one 128-byte line per row: ~1.15 KB of HBM lines per candidate in the per-launch PMC
+// table, 1.6 GB per 1080p step).  Later steps, after a move, read the planes as before; the
+// values are the same floats, so localisation is bit-identical.  Each streaming item (one wave)
+// owns kCubeK record slots; the record of a key is named by a code in the key's bits 40-63
+// (item << 6 | slot, all ones: none -- the small octaves' tile scan and an item's hits past
+// kCubeK), which localize strips before the key is used as the scan order.
+constexpr int kCube = 28;
+constexpr int kCubeK = 64;
+constexpr uint64_t kKeyMask = (1ull << 40) - 1;
+constexpr uint32_t kCubeNone = 0xFFFFFFu;
+
 template <int NL>
 __global__ void __launch_bounds__(256)
 extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
@@ -289,7 +303,7 @@ extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
         const int b = __ffs(hits) - 1;
         hits &= hits - 1;
         if (slot < raw_cap)
-            raw[(size_t)f * raw_cap + slot] = scan_key(o, b & 7, y0 + py0 + (b >> 3), x);
+            raw[(size_t)f * raw_cap + slot] = scan_key(o, b & 7, y0 + py0 + (b >> 3), x) | ((uint64_t)kCubeNone << 40);
         ++slot;
     }
 }
@@ -346,15 +360,20 @@ __device__ __forceinline__ float min3f(float a, float b, float c) { return fminf
 template <int NL, int SR>
 __global__ void __launch_bounds__(256, PANO_XSTREAM_BLOCKS)
 extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
-               int32_t *__restrict__ raw_cnt, int raw_cap, int item_base, int item_end) {
+               int32_t *__restrict__ raw_cnt, int raw_cap, int item_base, int item_end,
+               float *__restrict__ cube) {
     constexpr int ni = NL - 2;
     constexpr int BUF = 64;
     __shared__ uint64_t kbuf[4][BUF];
+    __shared__ __attribute__((aligned(16))) float cbuf[4][64][kCube];    // one ballot's cubes
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int f = blockIdx.y;
     int t = item_base + (int)blockIdx.x * 4 + wv;
     if (t >= item_end) return;                                     // whole wave
+    const int item = t;                                            // this wave's cube slots
+    float *cslots = cube ? cube + ((size_t)f * a.item_start[a.n_oct] + item) * (kCubeK * kCube) : nullptr;
+    int ncube = 0;                                                 // wave-uniform
     int o = 0;
     while (o + 1 < a.n_oct && t >= a.item_start[o + 1]) ++o;
     t -= a.item_start[o];
@@ -389,7 +408,7 @@ extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
             for (int l = 0; l < NL; ++l) nx[k][l] = p[l][(size_t)r * W];
         }
     }
-    float hxA[NL], hnA[NL], hxB[NL], hnB[NL], cB[NL];               // rows r-2 (A), r-1 (B)
+    float hxA[NL], hnA[NL], hxB[NL], hnB[NL], cA[NL], cB[NL];       // rows r-2 (A), r-1 (B)
     for (int r0 = y0 - 1; r0 <= yend; r0 += XPD) {
 #pragma unroll
         for (int k = 0; k < XPD; ++k) {
@@ -427,10 +446,48 @@ extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
                     if (m) {                                        // wave-uniform
                         const int k2 = __popcll(m);
                         if (nbuf + k2 > BUF) flush();
-                        if (ext) {
-                            const int pos = nbuf + __popcll(m & ((1ull << lane) - 1));
-                            kbuf[wv][pos] = scan_key(o, L, r - 1, x);
+                        const int pre = __popcll(m & ((1ull << lane) - 1));    // rank in the ballot
+                        const int pos = nbuf + pre;
+                        const int cs = ncube + pre;                                // cube slot
+                        uint64_t code = (uint64_t)kCubeNone << 40;
+                        if (cslots && cs < kCubeK) code = (uint64_t)(((uint32_t)item << 6) | (uint32_t)cs) << 40;
+                        if (ext) kbuf[wv][pos] = scan_key(o, L, r - 1, x) | code;
+                        if (cslots && ncube < kCubeK) {
+                            // the ballot's 3 x 3 x 3 cubes (levels L - 1 .. L + 1, rows r - 2,
+                            // r - 1, r, columns x - 1 .. x + 1) assembled in LDS: every lane
+                            // writes its own column's nine values into its own record (dx = 1)
+                            // and into its hit neighbours' (dx = 2 of lane - 1's, dx = 0 of
+                            // lane + 1's), whose ranks follow from the ballot -- no lane shifts,
+                            // no extra live registers; then each hit lane stores its record
+                            const bool hl = lane > 0 && ((m >> (lane - 1)) & 1);
+                            const bool hr = lane < 63 && ((m >> (lane + 1)) & 1);
+                            float *dm = &cbuf[wv][pre & 63][1];
+                            float *dr = &cbuf[wv][(pre + (ext ? 1 : 0)) & 63][0];
+                            float *dl = &cbuf[wv][(pre - 1) & 63][2];
+#pragma unroll
+                            for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+                                for (int dy = 0; dy < 3; ++dy) {
+                                    const float v = dy == 0 ? cA[L - 1 + dz] : dy == 1 ? cB[L - 1 + dz] : c[L - 1 + dz];
+                                    const int e = dz * 9 + dy * 3;
+                                    if (ext) dm[e] = v;
+                                    if (hr) dr[e] = v;
+                                    if (hl) dl[e] = v;
+                                }
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                            __builtin_amdgcn_wave_barrier();
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                            if (ext && cs < kCubeK) {
+                                const float4 *srcq = (const float4 *)&cbuf[wv][pre][0];
+                                float4 *dstq = (float4 *)(cslots + (size_t)cs * kCube);
+#pragma unroll 1
+                                for (int q = 0; q < kCube / 4; ++q) dstq[q] = srcq[q];
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                            __builtin_amdgcn_wave_barrier();     // records read before the next ballot's writes
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                         }
+                        ncube += k2;
                         nbuf += k2;
                     }
                 }
@@ -439,6 +496,7 @@ extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
             for (int l = 0; l < NL; ++l) {
                 hxA[l] = hxB[l]; hnA[l] = hnB[l];
                 hxB[l] = hxC[l]; hnB[l] = hnC[l];
+                cA[l] = cB[l];
                 cB[l] = c[l];
             }
         }
@@ -460,7 +518,8 @@ __device__ __forceinline__ float div255(float v) {
     return fmaf(fmaf(-q, 255.0f, v), y, q);
 }
 
-__device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key, int f, Cand &k) {
+__device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key, int f, Cand &k,
+                             const float *__restrict__ cube0 = nullptr) {
     const int o = (int)(key >> 32) / 8, layer0 = (int)(key >> 32) % 8;
     const int y = (int)((key >> 16) & 65535), x = (int)(key & 65535);
     const int ni = lp.ni, border = lp.border;
@@ -470,10 +529,22 @@ __device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key
     float c[3][3][3];
     float g[3], Hs[3][3], u[3];
     for (int it = 0; it < lp.max_iter; ++it) {
-        for (int dz = 0; dz < 3; ++dz)
-            for (int dy = 0; dy < 3; ++dy)
-                for (int dx = 0; dx < 3; ++dx)
-                    c[dz][dy][dx] = div255(dog_at(a, o, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx));
+        if (it == 0 && cube0) {              // the scan's record of this cube (kCube floats)
+            float *cf = &c[0][0][0];
+#pragma unroll
+            for (int q = 0; q < kCube / 4; ++q) {
+                const float4 t = ((const float4 *)cube0)[q];
+                cf[4 * q] = div255(t.x);
+                cf[4 * q + 1] = div255(t.y);
+                cf[4 * q + 2] = div255(t.z);
+                if (4 * q + 3 < 27) cf[4 * q + 3] = div255(t.w);
+            }
+        } else {
+            for (int dz = 0; dz < 3; ++dz)
+                for (int dy = 0; dy < 3; ++dy)
+                    for (int dx = 0; dx < 3; ++dx)
+                        c[dz][dy][dx] = div255(dog_at(a, o, li - 1 + dz, f, yi - 1 + dy, xi - 1 + dx));
+        }
         const float cv = c[1][1][1];
         g[0] = 0.5f * (c[1][1][2] - c[1][1][0]);
         g[1] = 0.5f * (c[1][2][1] - c[1][0][1]);
@@ -526,10 +597,10 @@ __device__ bool localize_one(const DogArgs &a, const LocParams &lp, uint64_t key
     return true;
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 4)   // 128 VGPRs: 4 waves per SIMD (the cube path pushed it to 132)
 localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
          const int32_t *__restrict__ raw_cnt, int raw_cap, Cand *__restrict__ cands,
-         int32_t *__restrict__ cand_cnt, int cand_cap) {
+         int32_t *__restrict__ cand_cnt, int cand_cap, const float *__restrict__ cube, int n_items) {
     // grid (frame, block): the dispatcher walks x fastest, so every frame's live blocks (the
     // low block indices; the grid is sized by the capacity) go out before the empty ones
     const int f = blockIdx.x;
@@ -539,7 +610,13 @@ localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
     if ((int)blockIdx.y * 256 >= cnt) return;   // uniform
     bool keep = false;
     Cand k;
-    if (ci < cnt) keep = localize_one(a, lp, raw[(size_t)f * raw_cap + ci], f, k);
+    if (ci < cnt) {
+        const uint64_t kr = raw[(size_t)f * raw_cap + ci];
+        const uint32_t code = (uint32_t)(kr >> 40);                 // the scan's cube record
+        const float *c0 = cube && code != kCubeNone
+            ? cube + (((size_t)f * n_items + (code >> 6)) * kCubeK + (code & 63)) * kCube : nullptr;
+        keep = localize_one(a, lp, kr & kKeyMask, f, k, c0);
+    }
     const unsigned long long m = __ballot(keep);
     const int lane = threadIdx.x & 63;
     int base = 0;
@@ -2355,10 +2432,24 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
 struct KpBufs {
     size_t ext_cap, cand_cap, raw_cap, cnt_ints;
     uint64_t *raw_ext;
+    float *cube;                 // extremum cubes (nullptr: PANO_EXT_CUBE=0, localize reads the planes)
+    int n_items;                 // streaming extrema items per frame (kCubeK cube slots each)
     int32_t *err, *cand_cnt, *raw_cnt, *ext_cnt, *desc_work, *ori_work;
 };
 
-int kp_bufs(pano_ctx *ctx, KpBufs &b) {
+// PANO_EXT_CUBE=0 (read once): no extremum cube records, localize reads every step from the
+// DoG planes (the round-5 form, for the A/B)
+bool ext_cube_on() {
+    static const bool v = [] {
+        const char *e = getenv("PANO_EXT_CUBE");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
+XArgs x_args(const pano_ctx *ctx, int border);
+
+int kp_bufs(pano_ctx *ctx, KpBufs &b, int border) {
     const int n = ctx->n, no = ctx->n_oct;
     size_t spo = 0;
     for (int o = 0; o < no; ++o) spo += (size_t)ctx->oct_h[o] * ctx->oct_w[o];
@@ -2372,6 +2463,14 @@ int kp_bufs(pano_ctx *ctx, KpBufs &b) {
     rc = pano_grow(ctx, (void **)&ctx->frame_off, &ctx->ext_bytes, b.ext_cap * n * sizeof(uint64_t));
     if (rc) return rc;
     b.raw_ext = (uint64_t *)ctx->frame_off;
+    b.cube = nullptr;
+    b.n_items = border >= 0 ? x_args(ctx, border).item_start[no] : 0;
+    if (border >= 0 && ext_cube_on()) {
+        rc = pano_grow(ctx, (void **)&ctx->ext_cube, &ctx->ext_cube_bytes,
+                       (size_t)n * b.n_items * kCubeK * kCube * sizeof(float));
+        if (rc) return rc;
+        b.cube = ctx->ext_cube;
+    }
     b.cnt_ints = (3 * (size_t)n + 1 + 16) * kCntStride;
     rc = pano_grow(ctx, (void **)&ctx->counters, &ctx->counters_n, b.cnt_ints * sizeof(int32_t));
     if (rc) return rc;
@@ -2436,9 +2535,9 @@ int launch_extrema_stream(pano_ctx *ctx, const pano_sift_params *p, const XArgs 
         PanoProf prof_(ctx, PK_EXTREMA, st);
 #define PANO_EXTREMA(NLV)                                                                          \
     (xsr == 16 ? extrema_stream<NLV, 16><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext,   \
-                                                              b.ext_cnt, (int)b.ext_cap, t0, t1)  \
+                                                              b.ext_cnt, (int)b.ext_cap, t0, t1, b.cube) \
                : extrema_stream<NLV, XSR><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext,  \
-                                                               b.ext_cnt, (int)b.ext_cap, t0, t1))
+                                                               b.ext_cnt, (int)b.ext_cap, t0, t1, b.cube))
         switch (ni + 2) {
             case 3: PANO_EXTREMA(3); break;
             case 4: PANO_EXTREMA(4); break;
@@ -2481,7 +2580,7 @@ bool early_extrema_enabled() {
 // blur and the extrema scan on the critical path.
 int sift_kp_counters(pano_ctx *ctx, int32_t **p, size_t *words) {
     KpBufs b;
-    const int rc = kp_bufs(ctx, b);
+    const int rc = kp_bufs(ctx, b, -1);                  // the counters only (no cube slots)
     if (rc) return rc;
     *p = ctx->counters;
     *words = b.cnt_ints;
@@ -2494,7 +2593,7 @@ int sift_early_extrema(pano_ctx *ctx, const pano_sift_params *p, int o) {
     if (p->num_intervals + 2 < 3 || p->num_intervals + 2 > 7) return PANO_OK;   // the keypoint stage reports it
     if (ctx->h > 4096 || ctx->w > 4096) return PANO_OK;
     KpBufs b;
-    int rc = kp_bufs(ctx, b);
+    int rc = kp_bufs(ctx, b, p->border);
     if (rc) return rc;
     if (ctx->early_oct < 0) {               // the counters start at zero before any scan
         rc = launch_fill(ctx, ctx->counters, 0, b.cnt_ints * sizeof(int32_t));
@@ -2533,7 +2632,7 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         return pano_fail(ctx, PANO_E_ARG, "pano_sift: bad outputs");
     if (n > PANO_MAX_FRAMES) return pano_fail(ctx, PANO_E_ARG, "pano_sift: more than PANO_MAX_FRAMES frames");
     KpBufs kb;
-    int rc = kp_bufs(ctx, kb);
+    int rc = kp_bufs(ctx, kb, p->border);
     if (rc) return rc;
     const size_t ext_cap = kb.ext_cap, cand_cap = kb.cand_cap, raw_cap = kb.raw_cap;
     uint64_t *raw_ext = kb.raw_ext;
@@ -2612,7 +2711,7 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         {
             PanoProf prof_(ctx, PK_EXTREMA);
             localize<<<g2, 256, 0, ctx->stream>>>(da, lp, raw_ext, ext_cnt, (int)ext_cap, ctx->cands,
-                                                  cand_cnt, (int)cand_cap);
+                                                  cand_cnt, (int)cand_cap, kb.cube, kb.n_items);
         }
         PANO_LAUNCH_CHECK(ctx, "localize");
     }

@@ -546,7 +546,17 @@ class Stitcher:
                     or fast[1][7] != self.ctx.generation()):
                 return None
             if src is not frames_dev:
-                src.copy_(frames_dev, non_blocking=True)      # same stream as the replay
+                if on_host:
+                    # the upload on a copy stream: it overlaps the running stitch i - 1 (the
+                    # slot's previous reader, stitch i - 2, has finished: its result was read)
+                    cs = self._copy_stream()
+                    with T.cuda.stream(cs):
+                        src.copy_(frames_dev, non_blocking=True)
+                        up = T.cuda.Event()
+                        up.record(cs)
+                    T.cuda.current_stream(self.device).wait_event(up)
+                else:
+                    src.copy_(frames_dev, non_blocking=True)  # same stream as the replay
             g = fast[1][0]
             self.ctx.check(self.ctx.lib.pano_graph_launch_stream(self.ctx.h, g, _lib._P(self._raw_stream())))
             ev = T.cuda.Event()
@@ -598,6 +608,13 @@ class Stitcher:
             if inflight is not None:
                 inflight[2].synchronize()
             self._use_slot(0)
+
+    def _copy_stream(self):
+        """A private stream for the host-item uploads and downloads of run_sequence /
+        StitchPool.run_sequence(to_host=True)."""
+        if getattr(self, "_cstream", None) is None:
+            self._cstream = self.torch.cuda.Stream(self.device)
+        return self._cstream
 
     def _rerun(self, items, i, margin, src_of):
         self._use_slot(i % 2)
@@ -807,16 +824,22 @@ class StitchPool:
                 m = i % k
                 with T.cuda.stream(self.streams[m]):
                     r = next(gens[m])
-                    if to_host:
-                        pano = r.panorama
-                        pin = pins[m]
-                        if pin is None or pin.numel() < pano.numel():
-                            pin = pins[m] = T.empty(max(pano.numel(), 1 << 20), dtype=T.uint8, pin_memory=True)
-                        hv = pin[:pano.numel()].view(pano.shape)
+                if to_host:
+                    # the stitch is complete (its head was read); the download goes on the
+                    # member's copy stream -- its own stream already holds the next stitch,
+                    # which the copy must not wait behind -- and later work on the member
+                    # stream (the stitch that reuses this canvas slot) waits for it
+                    st, cs = self.members[m], self.members[m]._copy_stream()
+                    pano = r.panorama
+                    pin = pins[m]
+                    if pin is None or pin.numel() < pano.numel():
+                        pin = pins[m] = T.empty(max(pano.numel(), 1 << 20), dtype=T.uint8, pin_memory=True)
+                    hv = pin[:pano.numel()].view(pano.shape)
+                    with T.cuda.stream(cs):
                         hv.copy_(pano, non_blocking=True)
                         ev = T.cuda.Event()
-                        ev.record(self.streams[m])
-                if to_host:
+                        ev.record(cs)
+                    self.streams[m].wait_event(ev)
                     ev.synchronize()
                     r.host = hv.numpy()
                 yield r
