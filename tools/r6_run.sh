@@ -35,7 +35,8 @@ for st in ${STAGES:-tests}; do
     : > $O/ab_summary.txt
     for r in $(seq 1 ${ROUNDS:-2}); do
       for v in base ${VARIANTS:-}; do
-        lib=""; [ "$v" != base ] && lib="PANO_LIB=tools/ab/libpano_$v.so"
+        lib=""
+        case $v in base) ;; env:*) lib="${v#env:}" ;; *) lib="PANO_LIB=tools/ab/libpano_$v.so" ;; esac
         env $lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-60} ${BENCH_ARGS:-} > $O/ab_run.txt 2> $O/ab_run.err || { tail -5 $O/ab_run.err; exit 1; }
         ms=$(tail -1 $O/ab_run.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); k=d.get("kernels_ms_per_step", {}); print(d["ms_per_step"], d.get("single_context_ms_per_step"), "blur", k.get("blur_level"), "extrema", k.get("extrema_localize"), "desc", k.get("descriptor"))')
         echo "r$r [$v] ms_per_step single_context: $ms" | tee -a $O/ab_summary.txt
