@@ -127,7 +127,7 @@ int pano_ctx_destroy(pano_ctx *ctx) {
     if (ctx->ev_lvl_join) (void)hipEventDestroy(ctx->ev_lvl_join);
     if (ctx->ev_sort_fork) (void)hipEventDestroy(ctx->ev_sort_fork);
     if (ctx->ev_sort_join) (void)hipEventDestroy(ctx->ev_sort_join);
-    void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->ext_cube, ctx->raw_sorted,
+    void *bufs[] = {ctx->pyr, ctx->cands, ctx->raw, ctx->counters, ctx->frame_off, ctx->raw_sorted,
                     ctx->taps, ctx->mscratch, ctx->flags, ctx->hscratch, ctx->bscratch, ctx->gray, ctx->sorted,
                     ctx->boxslots, ctx->hmscratch, ctx->dorder, ctx->match_sync, ctx->sel_sync, ctx->descraw, ctx->cyl_sync};
     for (void *b : bufs)
@@ -156,7 +156,6 @@ int pano_ctx_release_scratch(pano_ctx *ctx) {
         {(void **)&ctx->pyr, &ctx->pyr_bytes},           {(void **)&ctx->cands, &ctx->cand_cap},
         {(void **)&ctx->raw, &ctx->raw_cap},             {(void **)&ctx->counters, &ctx->counters_n},
         {(void **)&ctx->frame_off, &ctx->ext_bytes},     {(void **)&ctx->sorted, &ctx->sorted_bytes},
-        {(void **)&ctx->ext_cube, &ctx->ext_cube_bytes},
         {(void **)&ctx->dorder, &ctx->dorder_bytes},     {(void **)&ctx->gray, &ctx->gray_bytes},
         {(void **)&ctx->boxslots, &ctx->boxslots_bytes}, {&ctx->mscratch, &ctx->mscratch_bytes},
         {&ctx->hmscratch, &ctx->hmscratch_bytes},        {(void **)&ctx->flags, &ctx->flags_bytes},

@@ -109,8 +109,6 @@ struct pano_ctx {
     size_t counters_n = 0;
     int32_t *frame_off = nullptr;        // raw extrema (scan keys) before localisation
     size_t ext_bytes = 0;
-    float *ext_cube = nullptr;           // each raw extremum's 3x3x3 DoG cube (kCube floats)
-    size_t ext_cube_bytes = 0;
     RawKp *raw_sorted = nullptr;
     uint32_t *sorted = nullptr; size_t sorted_bytes = 0;   // per-frame sorted raw indices
     int32_t *dorder = nullptr; size_t dorder_bytes = 0;    // descriptor processing order
