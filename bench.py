@@ -717,7 +717,8 @@ def pcie_inclusive(st, frames, dev, focals, margin, steps, graph, mpx, pool=None
         # so one member's PCIe legs overlap the other members' stitches (StitchPool.run_sequence
         # to_host); the last panorama is checked byte for byte against the device one
         ref = np.ascontiguousarray(pano.cpu().numpy())
-        for _ in pool.run_sequence([(host_in, focals)] * (2 * len(pool.members) + 2), margin=margin, to_host=True):
+        # every member's two output slots capture their graphs on the staging buffers first
+        for _ in pool.run_sequence([(host_in, focals)] * (4 * len(pool.members) + 2), margin=margin, to_host=True):
             pass
         torch.cuda.synchronize()
         last = None

@@ -819,30 +819,50 @@ class StitchPool:
             with T.cuda.stream(s):
                 gens.append(st.run_sequence(items[m::k], margin=margin))
         pins = [None] * k
+        pending = None                           # (result, its download's event): yielded one item late
         try:
             for i in range(len(items)):
                 m = i % k
                 with T.cuda.stream(self.streams[m]):
                     r = next(gens[m])
-                if to_host:
-                    # the stitch is complete (its head was read); the download goes on the
-                    # member's copy stream -- its own stream already holds the next stitch,
-                    # which the copy must not wait behind -- and later work on the member
-                    # stream (the stitch that reuses this canvas slot) waits for it
-                    st, cs = self.members[m], self.members[m]._copy_stream()
-                    pano = r.panorama
-                    pin = pins[m]
-                    if pin is None or pin.numel() < pano.numel():
-                        pin = pins[m] = T.empty(max(pano.numel(), 1 << 20), dtype=T.uint8, pin_memory=True)
-                    hv = pin[:pano.numel()].view(pano.shape)
-                    with T.cuda.stream(cs):
-                        hv.copy_(pano, non_blocking=True)
-                        ev = T.cuda.Event()
-                        ev.record(cs)
-                    self.streams[m].wait_event(ev)
+                if not to_host:
+                    yield r
+                    continue
+                # the stitch is complete (its head was read); the download goes on the member's
+                # copy stream -- its own stream already holds the next stitch, which the copy must
+                # not wait behind -- and later work on the member stream (the stitch that reuses
+                # this canvas slot) waits for it.  The result is yielded one item later, when its
+                # download has had the next item's host work to finish in (with one member, at once)
+                # the crop's canvas rows are one contiguous byte range: one plain copy (no
+                # device-side gather of the strided view), the host array a strided view of it
+                cs = self.members[m]._copy_stream()
+                pano, canvas = r.panorama, r.canvas
+                row = canvas.stride(0)
+                off = pano.storage_offset() - canvas.storage_offset()
+                first, col0 = off // row, off % row
+                nb = pano.shape[0] * row
+                pin = pins[m]
+                if pin is None or pin.numel() < nb:
+                    pin = pins[m] = T.empty(max(nb, 1 << 20), dtype=T.uint8, pin_memory=True)
+                with T.cuda.stream(cs):
+                    pin[:nb].copy_(canvas.reshape(-1)[first * row:first * row + nb], non_blocking=True)
+                    ev = T.cuda.Event()
+                    ev.record(cs)
+                self.streams[m].wait_event(ev)
+                r.host = np.lib.stride_tricks.as_strided(pin.numpy()[col0:], shape=tuple(pano.shape),
+                                                         strides=(row, pano.stride(1), pano.stride(2)),
+                                                         writeable=False)
+                if k == 1:
                     ev.synchronize()
-                    r.host = hv.numpy()
-                yield r
+                    yield r
+                    continue
+                if pending is not None:
+                    pending[1].synchronize()
+                    yield pending[0]
+                pending = (r, ev)
+            if pending is not None:
+                pending[1].synchronize()
+                yield pending[0]
         finally:
             for g, s in zip(gens, self.streams):
                 with T.cuda.stream(s):
