@@ -1310,6 +1310,9 @@ constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; 
 #ifndef PANO_DESC_ABL_TRIG
 #define PANO_DESC_ABL_TRIG 0
 #endif
+#ifndef PANO_DESC_ABL_NOWALK
+#define PANO_DESC_ABL_NOWALK 0        // timing ablation: no sample walk (setup, intervals, epilogue only)
+#endif
 #ifndef PANO_DESC_COUNT
 #define PANO_DESC_COUNT 0             // 1: diagnostics build, lane-occupancy counters of the walk
 #endif
@@ -1785,7 +1788,11 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             // lane group g (kDescGrp adjacent lanes) walks its run of (super-strip, row) steps;
             // lane `sub` of the group takes strip `sub` of each super-strip, so one load
             // instruction covers a group's kDescSS-column row span in ~1 cache line
+#if PANO_DESC_ABL_NOWALK
+            const int nsamp = 0;                           // timing ablation: per-keypoint work only
+#else
             const int nsamp = run;                         // (super-strip, row) steps
+#endif
             constexpr int NG = 64 / kDescGrp;
             const int Q = (nsamp + NG - 1) / NG;
             const int sub = lane & (kDescGrp - 1);
