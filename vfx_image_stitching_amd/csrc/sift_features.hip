@@ -1310,6 +1310,12 @@ constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; 
 #ifndef PANO_DESC_ABL_TRIG
 #define PANO_DESC_ABL_TRIG 0
 #endif
+#ifndef PANO_DESC_ABL_NOCOL
+#define PANO_DESC_ABL_NOCOL 0         // timing ablation: no per-column row intervals
+#endif
+#ifndef PANO_DESC_ABL_NOEPI
+#define PANO_DESC_ABL_NOEPI 0         // timing ablation: no clamp / norm epilogue
+#endif
 #ifndef PANO_DESC_ABL_NOWALK
 #define PANO_DESC_ABL_NOWALK 0        // timing ablation: no sample walk (setup, intervals, epilogue only)
 #endif
@@ -1601,7 +1607,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             const float kq = (float)(-0.125 * 1.4426950408889634 * inv_hw * inv_hw);
             constexpr int kEmpty = 1 << 20;
             int run = 0;                                   // wave-wide running total
-            for (int c4 = 0; c4 < side; c4 += 64) {
+            for (int c4 = 0; c4 < (PANO_DESC_ABL_NOCOL ? 0 : side); c4 += 64) {
                 const int c = c4 + lane;
                 int lo = kEmpty, hi = -kEmpty;
                 // a column outside the patch or the image gets a bin base no sample passes
@@ -2223,10 +2229,14 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         };
         float lo = interior(lane), hi = interior(64 + lane);
         if (PANO_DESC_ABL >= 2) lo += (float)abl_sink;   // keeps the ablations' samples alive
+#if PANO_DESC_ABL_NOEPI                        // timing ablation: no norms (plain scaling)
+        float nv = 1.0f;
+#else
         const float thr = sqrtf(sdot_skx_wave128(lo, hi)) * dp.max_value;
         lo = lo > thr ? thr : lo;
         hi = hi > thr ? thr : hi;
         float nv = sqrtf(sdot_skx_wave128(lo, hi));
+#endif
         if (nv < 1e-7f) nv = 1e-7f;
         float dlo = rintf(512.0f * (lo / nv)), dhi = rintf(512.0f * (hi / nv));
         dlo = dlo < 0.0f ? 0.0f : (dlo > 255.0f ? 255.0f : dlo);
