@@ -564,6 +564,10 @@ localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
 #define PANO_ORI_COPIES 1      // histogram copies per wave (measured: 4 and 8 no faster)
 #endif
 constexpr int kOriCopies = PANO_ORI_COPIES;
+#ifndef PANO_ORI_CLAIM
+#define PANO_ORI_CLAIM 1       // candidates claimed per atomic (per-XCD work counter)
+#endif
+constexpr int kOriClaim = PANO_ORI_CLAIM;
 constexpr float kInv360 = 1.0f / 360.0f;   // RN(1 / 360)
 constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
 #ifndef PANO_ORI_STAGE
@@ -805,12 +809,23 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     FrameIndex fi;
     fi.init(cand_cnt, kCntStride, n_frames, cand_cap);
     int claim = 0;
+    int cl_next = 0, cl_end = 0;                 // wave-uniform: claimed candidates [cl_next, cl_end)
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
-        if (!kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
-        const int gk = lo_k + __shfl(claim, 0);
-        if (gk >= hi_k) break;
-        if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
+        int gk;
+        if constexpr (kClaimAhead) {
+            gk = lo_k + __shfl(claim, 0);
+            if (gk >= hi_k) break;
+            if (lane == 0) claim = atomicAdd(wq, 1);
+        } else {
+            if (cl_next >= cl_end) {              // kOriClaim candidates per atomic (as the descriptor)
+                if (lane == 0) claim = atomicAdd(wq, kOriClaim);
+                cl_next = __shfl(claim, 0);
+                cl_end = cl_next + kOriClaim;
+            }
+            gk = lo_k + cl_next++;
+            if (gk >= hi_k) break;
+        }
         int f = 0, ci = 0;
         if (fi.regs) fi.locate(gk, f, ci);
         else if (!locate_strided(cand_cnt, n_frames, cand_cap, gk, f, ci)) break;
@@ -1310,6 +1325,10 @@ constexpr int kRowTbl = 1920;         // row walk items per keypoint (u16 each; 
 #ifndef PANO_DESC_ABL_TRIG
 #define PANO_DESC_ABL_TRIG 0
 #endif
+#ifndef PANO_DESC_CLAIM
+#define PANO_DESC_CLAIM 1             // keypoints claimed per atomic (per-XCD work counter)
+#endif
+constexpr int kDescClaim = PANO_DESC_CLAIM;
 #ifndef PANO_DESC_ABL_NOCOL
 #define PANO_DESC_ABL_NOCOL 0         // timing ablation: no per-column row intervals
 #endif
@@ -1431,12 +1450,26 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     FrameIndex fi;
     fi.init(counts, cstride, n_frames, cap);
     int claim = 0;
+    int cl_next = 0, cl_end = 0;                 // wave-uniform: claimed keypoints [cl_next, cl_end)
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
-        if (!kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
-        const int gk = lo_k + __shfl(claim, 0);
-        if (gk >= hi_k) break;
-        if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
+        int gk;
+        if constexpr (kClaimAhead) {
+            gk = lo_k + __shfl(claim, 0);
+            if (gk >= hi_k) break;
+            if (lane == 0) claim = atomicAdd(wq, 1);
+        } else {
+            // kDescClaim keypoints per atomic: the XCD's counter serialises its waves' claims
+            // (the per-keypoint phase alone, no sample walk, took 76 us at parrington whatever
+            // its arithmetic -- the claims, not the work)
+            if (cl_next >= cl_end) {
+                if (lane == 0) claim = atomicAdd(wq, kDescClaim);
+                cl_next = __shfl(claim, 0);
+                cl_end = cl_next + kDescClaim;
+            }
+            gk = lo_k + cl_next++;
+            if (gk >= hi_k) break;
+        }
         if (fi.regs) fi.locate(gk, f, k);
         else if (RAW ? !locate_strided(counts, n_frames, cap, gk, f, k) : !locate_keypoint(counts, n_frames, cap, gk, f, k))
             break;
