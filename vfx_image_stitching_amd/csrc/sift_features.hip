@@ -2302,7 +2302,10 @@ struct OrderArgs {
     int bstart[PANO_MAX_OCTAVES + 1];   // first bucket of plane octave O (its layers x bands)
     int nband[PANO_MAX_OCTAVES];        // 16-row bands of octave O
     int n_oct, n_lvl, nb;               // octaves, levels, buckets per frame
+    int by_size;                        // 1: largest window first (buckets = kOrderHalves - half)
+    float hw_mult;                      // DescParams::hw_mult (the window's half width)
 };
+constexpr int kOrderHalves = 128;       // size order: window half widths 0 .. 127 (larger: bucket 0)
 
 __device__ __forceinline__ int desc_bucket(const pano_kp &kp, const OrderArgs &oa) {
     int oct = kp.octave & 255;
@@ -2310,6 +2313,11 @@ __device__ __forceinline__ int desc_bucket(const pano_kp &kp, const OrderArgs &o
     const int lyr = (kp.octave >> 8) & 255, O = oct + 1;
     if (O < 0 || O >= oa.n_oct || lyr >= oa.n_lvl) return 0;
     const float scl = oct >= 0 ? 1.0f / (float)(1 << oct) : (float)(1 << -oct);
+    if (oa.by_size) {                   // descriptor_wave's own half width, largest first
+        const float hw = (oa.hw_mult * scl) * kp.size;
+        const int half = (int)rint((double)hw * 1.4142135623730951 * 5.0 * 0.5);
+        return kOrderHalves - 1 - min(max(half, 0), kOrderHalves - 1);
+    }
     int band = (int)rint((double)scl * (double)kp.y) >> 4;
     band = band < 0 ? 0 : (band >= oa.nband[O] ? oa.nband[O] - 1 : band);
     return oa.bstart[O] + lyr * oa.nband[O] + band;
@@ -2802,11 +2810,12 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
                        int32_t *norms, const RawKp *rawk) {
     const int n = ctx->n;
     DescParams dp{(float)(p->scale_multiplier * 0.5), (float)p->descriptor_max};
-    // locality order (PANO_DESC_ORDER=1).  Measured on MI355X: 253 -> 262 us
-    // per parrington step with it, so the emit order stays the default
-    static const bool use_order = [] {
+    // processing order: 0 the emit order (default); 1 locality (plane + 16-row band; measured on
+    // MI355X, DESIGN.md 3: 253 -> 262 us per parrington step); 2 largest window first (the
+    // persistent waves' tail then holds the small keypoints)
+    static const int use_order = [] {
         const char *e = getenv("PANO_DESC_ORDER");
-        return e ? atoi(e) != 0 : false;
+        return e ? atoi(e) : 0;
     }();
     int32_t *order = nullptr;
     if (use_order && !rawk) {
@@ -2821,6 +2830,11 @@ int launch_descriptors(pano_ctx *ctx, const pano_sift_params *p, const PyrArgs &
         }
         oa.bstart[pa.n_oct] = nb;
         oa.nb = nb;
+        oa.hw_mult = dp.hw_mult;
+        if (use_order == 2) {
+            oa.by_size = 1;
+            oa.nb = nb = kOrderHalves;
+        }
         if (nb <= kSortMaxBuckets) {
             int rc = pano_grow(ctx, (void **)&ctx->dorder, &ctx->dorder_bytes, (size_t)n * cap * sizeof(int32_t));
             if (rc) return rc;
