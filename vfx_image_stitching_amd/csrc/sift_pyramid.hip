@@ -510,6 +510,9 @@ constexpr int tall_rows(int NT) { return ((128 - (NT - 1)) / 8) * 8; }
 // bound: blur_fast<..., 32, 256> uses 32 x 32 tiles of 256 threads with 8 row-pass and 4
 // column-pass outputs per thread -- a quarter of the serial FMA chain per thread and 4x the
 // workgroups of the 64 x 64 form.
+#ifndef PANO_BASE_ROWS
+#define PANO_BASE_ROWS 0    // > 0: output rows of the base level's tall tile (0: tall_rows(NT))
+#endif
 #ifndef PANO_BASE_PATCH
 #define PANO_BASE_PATCH 1   // 0: round-5 base staging (patch for interior tiles only) for A/B
 #endif
@@ -1641,7 +1644,9 @@ int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, fl
             PANO_LAUNCH_CHECK(ctx, "blur_fast");
             return PANO_OK;
         }
-        constexpr int TYT = tall_rows(NT);
+        // the base (MODE_BASE) also holds its gray patch in LDS: PANO_BASE_ROWS output rows per
+        // tile (default: the levels' tall tile) -- 88 fits tile + patch in 40 KB, 4 workgroups per CU
+        constexpr int TYT = MODE == MODE_BASE && PANO_BASE_ROWS > 0 ? PANO_BASE_ROWS : tall_rows(NT);
         // tall tiles only where they still leave >= 6 workgroups per CU (octave 0 of a batch):
         // on smaller planes the lost parallelism costs more than the halo saves
         static const long tall_min = [] {
@@ -1650,8 +1655,9 @@ int launch_blur_nt(pano_ctx *ctx, const LoadArgs &la, float *out, float *dog, fl
         }();
         const bool use_tall = tall && (long)grid.x * ((H + TYT - 1) / TYT) * n >= tall_min;
         const int ty = use_tall ? TYT : TY;
-        const size_t sm = (size_t)((ty + 2 * R) * ((TX + 2 * R) | 1) + (MODE == MODE_BASE ? kPatchR * kPatchP : 0)) *
-                          sizeof(float);
+        // base: the patch rows its window needs ((ty + 2R) / 2 + 3), not the capacity
+        const size_t sm = (size_t)((ty + 2 * R) * ((TX + 2 * R) | 1) +
+                                   (MODE == MODE_BASE ? ((ty + 2 * R) / 2 + 3) * kPatchP : 0)) * sizeof(float);
         {
             PanoProf prof_(ctx, PK_BLUR);
             if (use_tall) {
