@@ -511,7 +511,7 @@ constexpr int tall_rows(int NT) { return ((128 - (NT - 1)) / 8) * 8; }
 // column-pass outputs per thread -- a quarter of the serial FMA chain per thread and 4x the
 // workgroups of the 64 x 64 form.
 #ifndef PANO_BASE_ROWS
-#define PANO_BASE_ROWS 0    // > 0: output rows of the base level's tall tile (0: tall_rows(NT))
+#define PANO_BASE_ROWS 88   // output rows of the base level's tall tile (0: the levels' tall_rows(NT); measured: 88 fits tile + patch in 4 workgroups per CU, profiles/r06_base_rows_ab.txt)
 #endif
 #ifndef PANO_BASE_PATCH
 #define PANO_BASE_PATCH 1   // 0: round-5 base staging (patch for interior tiles only) for A/B
