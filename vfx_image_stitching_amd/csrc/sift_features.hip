@@ -616,6 +616,10 @@ __device__ __forceinline__ bool locate_strided(const int32_t *__restrict__ count
 #define PANO_CLAIM_AHEAD 0
 #endif
 constexpr bool kClaimAhead = PANO_CLAIM_AHEAD != 0;
+#ifndef PANO_CLAIM_STATIC
+#define PANO_CLAIM_STATIC 1    // orientation / descriptor: each wave's first item dealt, not claimed
+#endif
+constexpr bool kClaimStatic = PANO_CLAIM_STATIC != 0 && !kClaimAhead;
 
 // The dense work index of a persistent wave -> (frame, index).  For <= 64 frames the clamped
 // counts and their inclusive prefix live in registers (lane = frame), loaded once per wave, so
@@ -810,6 +814,14 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     fi.init(cand_cnt, kCntStride, n_frames, cand_cap);
     int claim = 0;
     int cl_next = 0, cl_end = 0;                 // wave-uniform: claimed candidates [cl_next, cl_end)
+    // every wave's first chunk without an atomic (wave i of the XCD takes chunk i; the counter
+    // hands out the rest after them): claiming at launch serialised ~770 atomics on each XCD's
+    // counter before its last wave could start
+    const int nw_x = kClaimStatic ? (int)(gridDim.x >> 3) * 4 : 0;
+    if (kClaimStatic) {
+        cl_next = ((int)(blockIdx.x >> 3) * 4 + wv) * kOriClaim;
+        cl_end = cl_next + kOriClaim;
+    }
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
         int gk;
@@ -820,7 +832,7 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         } else {
             if (cl_next >= cl_end) {              // kOriClaim candidates per atomic (as the descriptor)
                 if (lane == 0) claim = atomicAdd(wq, kOriClaim);
-                cl_next = __shfl(claim, 0);
+                cl_next = nw_x * kOriClaim + __shfl(claim, 0);
                 cl_end = cl_next + kOriClaim;
             }
             gk = lo_k + cl_next++;
@@ -1451,6 +1463,12 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     fi.init(counts, cstride, n_frames, cap);
     int claim = 0;
     int cl_next = 0, cl_end = 0;                 // wave-uniform: claimed keypoints [cl_next, cl_end)
+    // every wave's first chunk without an atomic (as orientation)
+    const int nw_x = kClaimStatic ? (int)(gridDim.x >> 3) * kDescWaves : 0;
+    if (kClaimStatic) {
+        cl_next = ((int)(blockIdx.x >> 3) * kDescWaves + wv) * kDescClaim;
+        cl_end = cl_next + kDescClaim;
+    }
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
         int gk;
@@ -1464,7 +1482,7 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             // its arithmetic -- the claims, not the work)
             if (cl_next >= cl_end) {
                 if (lane == 0) claim = atomicAdd(wq, kDescClaim);
-                cl_next = __shfl(claim, 0);
+                cl_next = nw_x * kDescClaim + __shfl(claim, 0);
                 cl_end = cl_next + kDescClaim;
             }
             gk = lo_k + cl_next++;
