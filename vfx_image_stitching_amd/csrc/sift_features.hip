@@ -620,6 +620,18 @@ constexpr bool kClaimAhead = PANO_CLAIM_AHEAD != 0;
 #define PANO_CLAIM_STATIC 1    // orientation / descriptor: each wave's first item dealt, not claimed
 #endif
 constexpr bool kClaimStatic = PANO_CLAIM_STATIC != 0 && !kClaimAhead;
+// Prefetched claims (orientation / descriptor): while a wave's item is more than PANO_CLAIM_FAR
+// items per XCD wave from its range's end, the wave issues the atomic for its next item before
+// working on this one, so the atomic's round trip overlaps the item's loads; the last items are
+// claimed on demand, so no wave holds a claimed item behind a long one while others drain
+// (what made kClaimAhead slower).  0 = off.  Measured slower too (profiles/r06_claim_far_ab.txt:
+// orientation 0.089 -> 0.101 ms, descriptor 0.215 -> 0.226 ms at parrington with 2): the returning
+// atomic joins the in-order vmcnt queue ahead of the item's own loads, so its contended latency
+// lands on the first load wait instead of overlapping.
+#ifndef PANO_CLAIM_FAR
+#define PANO_CLAIM_FAR 0
+#endif
+constexpr int kClaimFar = kClaimAhead ? 0 : PANO_CLAIM_FAR;
 
 // The dense work index of a persistent wave -> (frame, index).  For <= 64 frames the clamped
 // counts and their inclusive prefix live in registers (lane = frame), loaded once per wave, so
@@ -814,10 +826,11 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
     fi.init(cand_cnt, kCntStride, n_frames, cand_cap);
     int claim = 0;
     int cl_next = 0, cl_end = 0;                 // wave-uniform: claimed candidates [cl_next, cl_end)
+    bool pre = false;                            // wave-uniform: a claim is in flight in lane 0's claim
     // every wave's first chunk without an atomic (wave i of the XCD takes chunk i; the counter
     // hands out the rest after them): claiming at launch serialised ~770 atomics on each XCD's
     // counter before its last wave could start
-    const int nw_x = kClaimStatic ? (int)(gridDim.x >> 3) * 4 : 0;
+    const int wx = (int)(gridDim.x >> 3) * 4, nw_x = kClaimStatic ? wx : 0;   // waves per XCD
     if (kClaimStatic) {
         cl_next = ((int)(blockIdx.x >> 3) * 4 + wv) * kOriClaim;
         cl_end = cl_next + kOriClaim;
@@ -831,12 +844,17 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             if (lane == 0) claim = atomicAdd(wq, 1);
         } else {
             if (cl_next >= cl_end) {              // kOriClaim candidates per atomic (as the descriptor)
-                if (lane == 0) claim = atomicAdd(wq, kOriClaim);
+                if (!pre && lane == 0) claim = atomicAdd(wq, kOriClaim);
                 cl_next = nw_x * kOriClaim + __shfl(claim, 0);
                 cl_end = cl_next + kOriClaim;
+                pre = false;
             }
             gk = lo_k + cl_next++;
             if (gk >= hi_k) break;
+            if (kClaimFar && cl_next >= cl_end && gk + kClaimFar * wx * kOriClaim < hi_k) {
+                if (lane == 0) claim = atomicAdd(wq, kOriClaim);    // next claim in flight
+                pre = true;
+            }
         }
         int f = 0, ci = 0;
         if (fi.regs) fi.locate(gk, f, ci);
@@ -1463,8 +1481,9 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
     fi.init(counts, cstride, n_frames, cap);
     int claim = 0;
     int cl_next = 0, cl_end = 0;                 // wave-uniform: claimed keypoints [cl_next, cl_end)
+    bool pre = false;                            // wave-uniform: a claim is in flight in lane 0's claim
     // every wave's first chunk without an atomic (as orientation)
-    const int nw_x = kClaimStatic ? (int)(gridDim.x >> 3) * kDescWaves : 0;
+    const int wx = (int)(gridDim.x >> 3) * kDescWaves, nw_x = kClaimStatic ? wx : 0;
     if (kClaimStatic) {
         cl_next = ((int)(blockIdx.x >> 3) * kDescWaves + wv) * kDescClaim;
         cl_end = cl_next + kDescClaim;
@@ -1481,12 +1500,17 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
             // (the per-keypoint phase alone, no sample walk, took 76 us at parrington whatever
             // its arithmetic -- the claims, not the work)
             if (cl_next >= cl_end) {
-                if (lane == 0) claim = atomicAdd(wq, kDescClaim);
+                if (!pre && lane == 0) claim = atomicAdd(wq, kDescClaim);
                 cl_next = nw_x * kDescClaim + __shfl(claim, 0);
                 cl_end = cl_next + kDescClaim;
+                pre = false;
             }
             gk = lo_k + cl_next++;
             if (gk >= hi_k) break;
+            if (kClaimFar && cl_next >= cl_end && gk + kClaimFar * wx * kDescClaim < hi_k) {
+                if (lane == 0) claim = atomicAdd(wq, kDescClaim);   // next claim in flight
+                pre = true;
+            }
         }
         if (fi.regs) fi.locate(gk, f, k);
         else if (RAW ? !locate_strided(counts, n_frames, cap, gk, f, k) : !locate_keypoint(counts, n_frames, cap, gk, f, k))
