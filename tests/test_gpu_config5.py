@@ -5,9 +5,10 @@
 
 * the generator's ground truth on every pair: dx = -1229 (the strip step), dy = the jitter
   difference, each within 1.5 px -- size-independent properties of the sequence;
-* the oracle's golden for pairs 0 and 1 (tests/golden/synthetic_1080p.json, the oracle being
-  pinned bit-exactly to the reference at the reference's own sizes): ransac move and match
-  count at the bars of test_synthetic_1080p_vs_oracle_golden;
+* the oracle's golden for pairs 0 and 1 (tests/golden/synthetic_1080p.json) and for pairs 35,
+  71, 107 and 142 (synthetic_1080p_spread.json), the oracle being pinned bit-exactly to the
+  reference at the reference's own sizes: ransac move and match count at the bars of
+  test_synthetic_1080p_vs_oracle_golden;
 * the sharded form: each of the 8 strong-scaling shards (tools of distributed.py, what a rank
   runs before the record gather) gives byte-identical records to the matching slice of the
   whole-batch records.
@@ -57,9 +58,12 @@ def test_config5_every_pair_recovers_the_generator_shift(batch):
 
 def test_config5_first_pairs_equal_the_oracle_golden(batch, gold_json):
     _, _, _, _, res = batch
-    meta = gold_json("synthetic_1080p.json")
     r = res.records
-    for p, want in enumerate(meta["pairs"]):
+    # the first pairs and the four spread over the sequence (make_golden_1080p_spread.py)
+    pairs = gold_json("synthetic_1080p.json")["pairs"] + gold_json("synthetic_1080p_spread.json")["pairs"]
+    assert len(pairs) == 6
+    for want in pairs:
+        p = want["pair"][0]
         assert abs(int(r[p]["n_matches"]) - want["n_matches"]) <= max(2, want["n_matches"] // 1000)
         assert abs(r[p]["dx"] - want["move"][0]) <= 1e-3 and abs(r[p]["dy"] - want["move"][1]) <= 1e-3, \
             (p, r[p], want)

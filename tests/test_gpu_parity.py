@@ -756,6 +756,43 @@ def test_synthetic_1080p_vs_oracle_golden(gpu, gold_json, gold_npz):
             (p, r[p], want)
 
 
+def test_synthetic_1080p_spread_pairs_vs_oracle_golden(gpu, gold_json, gold_npz):
+    """Config 5 beyond its first pairs: pairs (35, 36), (71, 72), (107, 108), (142, 143) against
+    the oracle (tests/golden/make_golden_1080p_spread.py), each frame generated on its own:
+    cylindrical digest, keypoint count, the exact keypoint fields over the whole table by digest,
+    every 4th size / angle at the first-pairs bars, and the pair's match count and ransac move."""
+    from vfx_image_stitching_amd import _lib, data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    meta = gold_json("synthetic_1080p_spread.json")
+    z = gold_npz("synthetic_1080p_spread.npz")
+    sub = meta["sub"]
+    st = Stitcher("sift", cap=32768)
+    for want in meta["pairs"]:
+        p = want["pair"][0]
+        frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920, start=p, count=2)
+        cyl, _ = st.cylindrical(st.upload(frames), focals)
+        cyl_h = cyl.cpu().numpy()
+        kps, desc, counts = st.features(cyl)
+        n = counts.cpu().numpy()
+        for k in range(2):
+            i = p + k
+            pf = meta["per_frame"][str(i)]
+            assert digest(cyl_h[k]) == pf["cyl_digest"], i
+            assert n[k] == pf["count"], (i, n[k], pf["count"])
+            rec = kps[k, :n[k]].cpu().numpy().view(_lib.KP_NP).reshape(-1)
+            for name in ("x", "y", "response", "octave"):
+                assert digest(np.ascontiguousarray(rec[name])) == pf[f"{name}_digest"], (i, name)
+            np.testing.assert_allclose(rec["size"][::sub], z[f"f{i}_size_sub"], rtol=3e-7, atol=0)
+            da = np.abs(rec["angle"][::sub].astype(np.float64) - z[f"f{i}_angle_sub"])
+            da = np.minimum(da, 360 - da)
+            assert (da > 2e-3).mean() <= 1e-3 and da.max() < 1.0, i
+        recs, _ = st.pair_records((kps, desc, counts), [(0, 1)])
+        r = recs.cpu().numpy().view(_lib.PAIR_NP).reshape(-1)[0]
+        assert r["status"] == _lib.PANO_OK
+        assert abs(int(r["n_matches"]) - want["n_matches"]) <= max(2, want["n_matches"] // 1000), (p, r, want)
+        assert abs(r["dx"] - want["move"][0]) <= 1e-3 and abs(r["dy"] - want["move"][1]) <= 1e-3, (p, r, want)
+
+
 @pytest.mark.parametrize("tt", ["32", "64"])
 def test_fused_pair_blur_bit_exact(gpu, tt):
     """The fused two-level blur (blur_pair: levels (1, 2) and (4, 5) of the small octaves in one

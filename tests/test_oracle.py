@@ -185,3 +185,18 @@ def test_numpy_semantics_used_by_the_oracle():
     np.add.at(t, np.array([0, 0]), np.array([0.1, 1e-9]))
     assert t[0] == np.float32(np.float64(np.float32(0.1)) + 1e-9)
     assert not (np.float32(0.04) < 0.04)          # NEP 50: the Python float is cast to f32
+
+
+@pytest.mark.parametrize("name", ["synthetic_1080p.json", "synthetic_1080p_spread.json"])
+def test_config5_goldens_recover_the_generator_shift(name, gold_json):
+    """The oracle's config-5 pairs (tests/golden/make_golden_1080p*.py) against the sequence's
+    ground truth: dx = -1229 (the strip step), dy = the jitter difference, within 1.5 px --
+    the property test_gpu_config5 checks on every pair of the GPU run."""
+    jit = np.random.default_rng(1).integers(-3, 4, 144)      # data.synthetic_sequence's jitter
+    pairs = gold_json(name)["pairs"]
+    assert pairs
+    for want in pairs:
+        p = want["pair"][0]
+        dx, dy = want["move"]
+        assert abs(dx + 1229) <= 1.5 and abs(dy - (jit[p + 1] - jit[p])) <= 1.5, (p, want["move"])
+        assert want["n_matches"] > 1000
