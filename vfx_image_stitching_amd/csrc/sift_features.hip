@@ -294,7 +294,7 @@ extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
     }
 }
 
-// Streaming form of the same test: one WAVE per item = a 62-column strip of XSR output rows
+// Streaming form of the same test: one WAVE per item = a 62-column strip of SR output rows (extrema_xsr)
 // of one octave of one frame.  Lane = column (lanes 0 and 63 are the 1-px halo); the wave
 // walks down the rows with the NL DoG values of PD rows prefetched in registers, forms the
 // horizontal 3-max/min of each level with two lane shifts, keeps the last three rows of those
@@ -302,7 +302,6 @@ extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
 // barrier: each wave streams its rows as a chain of coalesced 256-byte loads.  Hits (rare)
 // are gathered in a per-wave LDS buffer and appended with one atomic per flush.
 constexpr int XSW = 62;          // output columns per strip
-constexpr int XSR = 32;          // output rows per item (default; PANO_EXTREMA_XSR=16 halves it)
 #ifndef PANO_XPD
 #define PANO_XPD 3
 #endif
@@ -317,6 +316,7 @@ struct XArgs {
     int strips_x[PANO_MAX_OCTAVES];
     int item_start[PANO_MAX_OCTAVES + 1];
     int n_oct;
+    int sr;                      // output rows per item (extrema_xsr)
 };
 
 // Whole-wave lane shifts by one through DPP (wave_shr:1 / wave_shl:1, GFX9 DPP controls):
@@ -2490,16 +2490,47 @@ int kp_bufs(pano_ctx *ctx, KpBufs &b) {
     return PANO_OK;
 }
 
-// Rows per streaming extrema item (PANO_EXTREMA_XSR=16 halves them) and the smallest octave
+// The smallest octave
 // height the streaming kernel takes (0 disables it).  Measured (same box): 96 -- parrington's
 // octave 3 joins the streaming launch instead of its own scan -- 164-167 us per extrema class
 // against 175-178 us at 192; 48 within noise of 96.
-int extrema_xsr() {
-    static const int v = [] {
+// Output rows per extrema_stream item, by the batch's size: a wave's walk costs its first
+// XPD rows of load latency and two halo rows, so taller strips are cheaper per row -- but the
+// launch must still hold about two rounds of resident waves, or its last partial round leaves
+// the chip idle.  The tallest of kXsrs whose item count is >= 2 rounds of resident waves (else
+// the shortest).  Measured (tools/feat_time.py, profiles/r06_extrema_xsr_ab.txt): parrington
+// 24 rows 0.1445 ms against 0.147 (32) and 0.151 (48); 1080p 48 rows 1.105-1.112 against
+// 1.16-1.18 (32) and 1.26-1.28 (24).  PANO_EXTREMA_XSR=<one of kXsrs> forces one height.
+constexpr int kXsrs[] = {24, 32, 48, 64};
+int extrema_items(const pano_ctx *ctx, int border, int xsr) {
+    int items = 0;
+    for (int o = 0; o < ctx->n_oct; ++o) {
+        const int iw = ctx->oct_w[o] - 2 * border, ih = ctx->oct_h[o] - 2 * border;
+        if (iw > 0 && ih > 0) items += ((iw + XSW - 1) / XSW) * ((ih + xsr - 1) / xsr);
+    }
+    return items;
+}
+int extrema_xsr(const pano_ctx *ctx, int border) {
+    static const int forced = [] {
         const char *e = getenv("PANO_EXTREMA_XSR");
-        return e && atoi(e) == 16 ? 16 : XSR;
+        const int v = e ? atoi(e) : 0;
+        for (int x : kXsrs) if (v == x) return v;
+        return 0;
     }();
-    return v;
+    if (forced) return forced;
+    static long long resident = 0;                  // waves the chip holds at the kernel's occupancy
+    if (!resident) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, extrema_stream<5, 32>, 256, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+            per_cu <= 0 || cus <= 0)
+            per_cu = 6, cus = 256;
+        resident = 4LL * per_cu * cus;
+    }
+    int pick = kXsrs[0];
+    for (int x : kXsrs)
+        if ((long long)ctx->n * extrema_items(ctx, border, x) >= 2 * resident) pick = x;
+    return pick;
 }
 int extrema_min_h() {
     static const int v = [] {
@@ -2512,8 +2543,9 @@ int extrema_min_h() {
 // The streaming kernel's items (strips of xsr rows) of every octave, octave-major.
 XArgs x_args(const pano_ctx *ctx, int border) {
     XArgs xa{};
-    const int no = ctx->n_oct, nl = ctx->n_lvl, xsr = extrema_xsr();
+    const int no = ctx->n_oct, nl = ctx->n_lvl, xsr = extrema_xsr(ctx, border);
     int items = 0;
+    xa.sr = xsr;
     xa.n_oct = no;
     for (int o = 0; o < no; ++o) {
         xa.H[o] = ctx->oct_h[o];
@@ -2535,23 +2567,32 @@ double extrema_thresh(const pano_sift_params *p) {
 int launch_extrema_stream(pano_ctx *ctx, const pano_sift_params *p, const XArgs &xa, const KpBufs &b,
                           int t0, int t1, hipStream_t st) {
     if (t1 <= t0) return PANO_OK;
-    const int n = ctx->n, ni = p->num_intervals, xsr = extrema_xsr();
+    const int n = ctx->n, ni = p->num_intervals, xsr = xa.sr;
     const double thresh = extrema_thresh(p);
     dim3 grid((unsigned)((t1 - t0 + 3) / 4), n);
     {
         PanoProf prof_(ctx, PK_EXTREMA, st);
-#define PANO_EXTREMA(NLV)                                                                          \
-    (xsr == 16 ? extrema_stream<NLV, 16><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext,   \
-                                                              b.ext_cnt, (int)b.ext_cap, t0, t1)  \
-               : extrema_stream<NLV, XSR><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext,  \
-                                                               b.ext_cnt, (int)b.ext_cap, t0, t1))
-        switch (ni + 2) {
-            case 3: PANO_EXTREMA(3); break;
-            case 4: PANO_EXTREMA(4); break;
-            case 5: PANO_EXTREMA(5); break;
-            case 6: PANO_EXTREMA(6); break;
-            case 7: PANO_EXTREMA(7); break;
-            default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "num_intervals above 5");
+#define PANO_EXTREMA(NLV, SR) \
+    extrema_stream<NLV, SR><<<grid, 256, 0, st>>>(xa, p->border, thresh, b.raw_ext, b.ext_cnt, (int)b.ext_cap, t0, t1)
+        // every strip height for the default 5 DoG levels; the other level counts at 32 rows
+        // (x_args numbered their items at xa.sr: fail rather than scan the wrong rows)
+        if (ni + 2 == 5) {
+            switch (xsr) {
+                case 24: PANO_EXTREMA(5, 24); break;
+                case 32: PANO_EXTREMA(5, 32); break;
+                case 48: PANO_EXTREMA(5, 48); break;
+                case 64: PANO_EXTREMA(5, 64); break;
+                default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "extrema strip height");
+            }
+        } else {
+            if (xsr != 32) return pano_fail(ctx, PANO_E_UNSUPPORTED, "extrema strip height");
+            switch (ni + 2) {
+                case 3: PANO_EXTREMA(3, 32); break;
+                case 4: PANO_EXTREMA(4, 32); break;
+                case 6: PANO_EXTREMA(6, 32); break;
+                case 7: PANO_EXTREMA(7, 32); break;
+                default: return pano_fail(ctx, PANO_E_UNSUPPORTED, "num_intervals above 5");
+            }
         }
 #undef PANO_EXTREMA
     }
