@@ -558,7 +558,8 @@ localize(DogArgs a, LocParams lp, const uint64_t *__restrict__ raw,
 
 // ------------------------------------------------------------------ S7
 #ifndef PANO_ORI_ABL
-#define PANO_ORI_ABL 0         // timing ablations of orientation only (bit 1: no atan2f, 2: no expf)
+#define PANO_ORI_ABL 0         // timing ablations of orientation only (bit 1: no atan2f, 2: no expf,
+                               // 4: no patch loads, 8: no emit atomic -- slots from the work index)
 #endif
 #ifndef PANO_ORI_COPIES
 #define PANO_ORI_COPIES 1      // histogram copies per wave (measured: 4 and 8 no faster)
@@ -870,7 +871,11 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         const unsigned long long m = __ballot(emit);
         if (m) {
             int base = 0;
+#if PANO_ORI_ABL & 8
+            base = (gk * 2) % (raw_cap - 64);
+#else
             if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&raw_cnt[f * kCntStride], __popcll(m));
+#endif
             base = __shfl(base, __ffsll((long long)m) - 1);
             if (emit) {
                 RawKp q;
