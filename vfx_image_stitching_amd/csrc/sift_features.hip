@@ -674,10 +674,32 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef PANO_ORI_FAST_WALK
+#define PANO_ORI_FAST_WALK 1   // interior candidates walk without per-sample bounds tests (identical bins)
+#endif
+constexpr bool kOriFastWalk = PANO_ORI_FAST_WALK != 0;
+#ifndef PANO_ORI_TIMING
+#define PANO_ORI_TIMING 0      // 1: diagnostics build, per-wave phase clocks of orientation (tools/ori_clock.py)
+#endif
+#if PANO_ORI_TIMING
+constexpr int kOriClkWaves = 16384;
+__device__ unsigned long long g_ori_clk[kOriClkWaves][8];
+#define PANO_ORI_NOW() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
+extern "C" int pano_dbg_ori_clock(unsigned long long *out, int reset) {
+    if (reset) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ori_clk)) != hipSuccess) return -1;
+        return hipMemset(p, 0, sizeof(g_ori_clk)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ori_clk), sizeof(g_ori_clk)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H, int W, int o, float kx, float ky,
                                            float ksize, const OriParams &op,
                                            unsigned long long (*hs)[PANO_ORI_BINS], double *hd, double *sm,
-                                           float *pt, int lane, double &angle) {
+                                           float *pt, int lane, double &angle,
+                                           unsigned long long *ts = nullptr) {
     for (int i = lane; i < kOriCopies * PANO_ORI_BINS; i += 64) (&hs[0][0])[i] = 0ull;
     {
         const float scale = (float)(op.scale_factor * (double)ksize) / (float)(1 << (o + 1));
@@ -717,47 +739,75 @@ __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H,
             }
         }
         wave_sync_lds();
+#if PANO_ORI_TIMING
+        if (ts) ts[0] = PANO_ORI_NOW();
+#endif
         // lane l walks its own run of Q consecutive column-major samples (neighbouring
         // lanes are Q samples apart: different bins, fewer same-address LDS atomics)
         const int Q = (S + 63) / 64;
         const int j0 = lane * Q;
-        int xi = j0 / side, yi = j0 - (j0 / side) * side;
         const int jend = min(j0 + Q, S);
-        for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
-            const int dx = xi - radius, dy = yi - radius;
-            const int yy = cy + dy, xx = cx + dx;
-            if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
-            float gx, gy;
-            if (staged) {
-                const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
-                gx = q[1] - q[-1];
-                gy = q[-kOriPatch] - q[kOriPatch];
-            } else {
-                gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
-                gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
-            }
-            const float mag = sqrtf(gx * gx + gy * gy);
+        // INTERIOR: every sample of the square and its four taps inside the image and staged,
+        // so no per-sample bounds test and LDS taps only (kOriFastWalk)
+        auto walk = [&](auto interior) {
+            constexpr bool INTERIOR = decltype(interior)::value;
+            int xi = j0 / side, yi = j0 - (j0 / side) * side;
+            for (int j = j0; j < jend; ++j, (++yi == side) ? (yi = 0, ++xi) : 0) {
+                const int dx = xi - radius, dy = yi - radius;
+                float gx, gy;
+                if constexpr (INTERIOR) {
+                    const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
+                    gx = q[1] - q[-1];
+                    gy = q[-kOriPatch] - q[kOriPatch];
+                } else {
+                    const int yy = cy + dy, xx = cx + dx;
+                    if (xx <= 0 || xx >= W - 1 || yy <= 0 || yy >= H - 1) continue;
+                    if (staged) {
+                        const float *q = pt + (yi + 1) * kOriPatch + xi + 1;
+                        gx = q[1] - q[-1];
+                        gy = q[-kOriPatch] - q[kOriPatch];
+                    } else {
+                        gx = img[(size_t)yy * W + xx + 1] - img[(size_t)yy * W + xx - 1];
+                        gy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+                    }
+                }
+                const float mag = sqrtf(gx * gx + gy * gy);
 #if PANO_ORI_ABL & 1                                  // timing ablation: no atan2f
-            const float ang = fabsf(gy + gx) * 3.0f;
+                const float ang = fabsf(gy + gx) * 3.0f;
 #else
-            const float ang = np_remainder_pos_f(atan2f(gy, gx) * kRad2DegF32, 360.0f);
+                // np.remainder(a, 360) for |a| <= 180 (atan2f in [-pi, pi] times the f32 rad2deg):
+                // np_remainder_pos_f's in-range branch without its general fallback
+                const float a = atan2f(gy, gx) * kRad2DegF32;
+                const float ang = kOriFastWalk ? (a < 0.0f ? a + 360.0f : (a == 0.0f ? 0.0f : a))
+                                               : np_remainder_pos_f(a, 360.0f);
 #endif
+                // dx^2 + dy^2 as the exact f32 sum of exact f32 squares (|d| <= 2^7): the same
+                // value as the integer expression converted, without the integer multiplies
+                const float fdx = (float)dx, fdy = (float)dy;
+                const float d2 = kOriFastWalk ? fdx * fdx + fdy * fdy : (float)(dx * dx + dy * dy);
 #if PANO_ORI_ABL & 2                                  // timing ablation: no expf
-            const float w = wfac * (float)(dx * dx + dy * dy) + 1.0f;
+                const float w = wfac * d2 + 1.0f;
 #else
-            const float w = expf(wfac * (float)(dx * dx + dy * dy));
+                const float w = expf(wfac * d2);
 #endif
-            // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same
-            // bin as the IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
-            const float a36 = ang * 36.0f;
-            const float q0 = a36 * kInv360;
-            int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
-            bin = bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
-            const double val = (double)(w * mag);
-            atomicAdd(&hs[lane % kOriCopies][bin], rint_fix(val * kHistScale));
-        }
+                // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same
+                // bin as the IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
+                const float a36 = ang * 36.0f;
+                const float q0 = a36 * kInv360;
+                int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
+                bin = bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
+                const double val = (double)(w * mag);
+                atomicAdd(&hs[lane % kOriCopies][bin], rint_fix(val * kHistScale));
+            }
+        };
+        const bool interior = staged && cx - radius > 0 && cx + radius < W - 1 && cy - radius > 0 && cy + radius < H - 1;
+        if (kOriFastWalk && interior) walk(std::true_type{});
+        else walk(std::false_type{});
     }
     wave_sync_lds();
+#if PANO_ORI_TIMING
+    if (ts) ts[1] = PANO_ORI_NOW();
+#endif
     if (lane < PANO_ORI_BINS) {
         unsigned long long t = 0;
 #pragma unroll
@@ -836,8 +886,15 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         cl_next = ((int)(blockIdx.x >> 3) * 4 + wv) * kOriClaim;
         cl_end = cl_next + kOriClaim;
     }
+#if PANO_ORI_TIMING
+    unsigned long long t_entry = PANO_ORI_NOW(), acc[4] = {0, 0, 0, 0}, ts[2] = {0, 0}, tq = 0, t1 = 0;
+    int ncand = 0;
+#endif
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
+#if PANO_ORI_TIMING
+        tq = PANO_ORI_NOW();
+#endif
         int gk;
         if constexpr (kClaimAhead) {
             gk = lo_k + __shfl(claim, 0);
@@ -865,9 +922,16 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
         const Cand k = cands[(size_t)f * cand_cap + ci];
         double angle;
         const int p = lane;
+#if PANO_ORI_TIMING
+        __builtin_amdgcn_s_waitcnt(0);                // the candidate record has arrived
+        t1 = PANO_ORI_NOW();
+        unsigned long long *tsp = ts;
+#else
+        unsigned long long *tsp = nullptr;
+#endif
         const bool emit = orient_one(pa.gauss[k.octave][k.layer] + (size_t)f * pa.H[k.octave] * pa.W[k.octave],
                                      pa.H[k.octave], pa.W[k.octave], k.octave, k.x, k.y, k.size, op, hist[wv],
-                                     hd[wv], sm[wv], patch[wv], lane, angle);
+                                     hd[wv], sm[wv], patch[wv], lane, angle, tsp);
         const unsigned long long m = __ballot(emit);
         if (m) {
             int base = 0;
@@ -892,7 +956,30 @@ orientation(PyrArgs pa, OriParams op, const Cand *__restrict__ cands,
             }
         }
         wave_sync_lds();                   // hist / hd / sm / patch reused by the next candidate
+#if PANO_ORI_TIMING
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t_end = PANO_ORI_NOW();
+        acc[0] += t1 - tq;                 // claim, locate, candidate load
+        acc[1] += ts[0] - t1;              // patch staging
+        acc[2] += ts[1] - ts[0];           // sample walk
+        acc[3] += t_end - ts[1];           // histogram, smoothing, peaks, emit
+        ++ncand;
+#endif
     }
+#if PANO_ORI_TIMING
+    const int gw = (int)blockIdx.x * 4 + wv;
+    if (lane == 0 && gw < kOriClkWaves) {
+        unsigned long long *o = g_ori_clk[gw];
+        o[0] = t_entry;
+        o[1] = PANO_ORI_NOW();
+        o[2] = (unsigned long long)ncand;
+        o[3] = acc[0];
+        o[4] = acc[1];
+        o[5] = acc[2];
+        o[6] = acc[3];
+        o[7] = (unsigned long long)(xcd + 1);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ S6 / S7 per caller candidate
