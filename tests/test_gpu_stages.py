@@ -335,6 +335,20 @@ def test_float_images_take_the_reference_sequence(gpu, frames00):
         iss.compute_shift_sift(f, f)
 
 
+@pytest.mark.parametrize("ni", [2, 4])
+def test_other_interval_counts_vs_oracle(gpu, frames00, ni):
+    """num_intervals 2 and 4 (4 and 6 DoG levels per octave) through the batched u8 path: the
+    streaming extrema scan at its 32-row strips (the size-based strip heights are built for the
+    default 5 DoG levels only), equal to the oracle's chain."""
+    from oracle import sift as osift
+    from oracle.cv2_compat import bgr_to_gray_u8
+    from vfx_image_stitching_amd import sift_impl
+    bgr = np.ascontiguousarray(frames00["prtn00"][96:224, 144:304])          # 128 x 160
+    kps, desc = sift_impl.compute_keypoints_and_descriptors(bgr, num_intervals=ni)
+    okps, odesc = osift.detect_and_describe(bgr_to_gray_u8(bgr), num_intervals=ni)
+    _assert_same_features(kps, desc, okps, odesc)
+
+
 def test_bgr_depths_cv2_refuses(gpu):
     """cv2.cvtColor(BGR2GRAY) takes uint8, uint16 and float32 BGR only (sift_impl.py:27-28):
     float64 BGR is refused with ValueError (cv2's "Unsupported depth"), uint16 with

@@ -2635,7 +2635,8 @@ int extrema_min_h() {
 // The streaming kernel's items (strips of xsr rows) of every octave, octave-major.
 XArgs x_args(const pano_ctx *ctx, int border) {
     XArgs xa{};
-    const int no = ctx->n_oct, nl = ctx->n_lvl, xsr = extrema_xsr(ctx, border);
+    // every strip height is instantiated for the default 5 DoG levels only (launch_extrema_stream)
+    const int no = ctx->n_oct, nl = ctx->n_lvl, xsr = nl - 1 == 5 ? extrema_xsr(ctx, border) : 32;
     int items = 0;
     xa.sr = xsr;
     xa.n_oct = no;
