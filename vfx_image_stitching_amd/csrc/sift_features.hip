@@ -302,6 +302,9 @@ extrema_scan(DogArgs a, int border, double thresh, uint64_t *__restrict__ raw,
 // barrier: each wave streams its rows as a chain of coalesced 256-byte loads.  Hits (rare)
 // are gathered in a per-wave LDS buffer and appended with one atomic per flush.
 constexpr int XSW = 62;          // output columns per strip
+#ifndef PANO_XNT
+#define PANO_XNT 0               // A/B: cache-policy bits of the streaming scan's DoG loads (2: nt)
+#endif
 #ifndef PANO_XPD
 #define PANO_XPD 3
 #endif
@@ -372,7 +375,7 @@ extrema_stream(XArgs a, int border, double thresh, uint64_t *__restrict__ raw,
     for (int l = 0; l < NL; ++l)
         rs[l] = __builtin_amdgcn_make_buffer_rsrc((void *)(a.dog[o][l] + (size_t)f * H * W), 0, H * W * 4, 0x00020000);
     auto ld = [&](int l, int r) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs[l], (r * W + gx) * 4, 0, 0));
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs[l], (r * W + gx) * 4, 0, PANO_XNT));
     };
     int nbuf = 0;                                                   // wave-uniform
     auto flush = [&]() {

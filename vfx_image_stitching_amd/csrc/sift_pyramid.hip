@@ -518,6 +518,14 @@ constexpr int tall_rows(int NT) { return ((128 - (NT - 1)) / 8) * 8; }
 #endif
 constexpr bool base_patch = PANO_BASE_PATCH != 0;
 
+// blur_fast's DoG planes go out as nontemporal (streaming) stores: nothing reads them until the
+// extrema scan after the octave's last level, and the level planes the next launch reads at
+// once keep the caches.  Measured (profiles/r06_blur_nt_ab.txt, two boxes): blur class -2 to
+// -4 %, pooled parrington step -1 to -3 %; the level planes nontemporal too (bit 1) slows the
+// next level's reads; nontemporal DoG loads in the scan (PANO_XNT=2) slow it at 1080p.
+#ifndef PANO_BLUR_NT
+#define PANO_BLUR_NT 1      // bit 0: DoG stores nontemporal; bit 1: level stores too (A/B)
+#endif
 template <int MODE, int NT, int TYT = TY, int TXT = TX, int NTHR = 512>
 __global__ void __launch_bounds__(NTHR, 6)
 blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
@@ -596,9 +604,17 @@ blur_fast(LoadArgs la, float *__restrict__ out, float *__restrict__ dog,
             if (o[j] == -1.2345f) out[gi] = o[j] + cen[j];    // never true: keeps the work live
             continue;
         }
-        if (out) out[gi] = o[j];
+        if constexpr ((PANO_BLUR_NT & 2) != 0) {
+            if (out) __builtin_nontemporal_store(o[j], out + gi);
+        } else {
+            if (out) out[gi] = o[j];
+        }
         if constexpr (CENTER) {
-            if (dog) dog[gi] = o[j] - cen[j];
+            if constexpr ((PANO_BLUR_NT & 1) != 0) {
+                if (dog) __builtin_nontemporal_store(o[j] - cen[j], dog + gi);
+            } else {
+                if (dog) dog[gi] = o[j] - cen[j];
+            }
             if (in_copy) in_copy[gi] = cen[j];
         }
     }
