@@ -1506,6 +1506,22 @@ __device__ __forceinline__ bool locate_keypoint(const int32_t *__restrict__ coun
     return false;
 }
 
+#ifndef PANO_DESC_TIMING
+#define PANO_DESC_TIMING 0     // 1: diagnostics build, per-wave clocks of descriptor_wave (tools/desc_clock.py)
+#endif
+#if PANO_DESC_TIMING
+constexpr int kDescClkWaves = 16384;
+__device__ unsigned long long g_desc_clk[kDescClkWaves][4];
+extern "C" int pano_dbg_desc_clock(unsigned long long *out, int reset) {
+    if (reset) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_desc_clk)) != hipSuccess) return -1;
+        return hipMemset(p, 0, sizeof(g_desc_clk)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_desc_clk), sizeof(g_desc_clk)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // OCC: waves per SIMD the register budget is sized for.  With a strip change's rows loaded
 // when reached (PANO_DESC_NS_PREFETCH=0, 12 VGPRs fewer) the 4-wave budget spills 5 registers
 // instead of 13, and measures best at both sizes (same box, feature-stage timing): parrington
@@ -1583,6 +1599,10 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         cl_next = ((int)(blockIdx.x >> 3) * kDescWaves + wv) * kDescClaim;
         cl_end = cl_next + kDescClaim;
     }
+#if PANO_DESC_TIMING
+    const unsigned long long t_entry = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+    int nkp = 0;
+#endif
     if (kClaimAhead && lane == 0) claim = atomicAdd(wq, 1);
     for (;;) {
         int gk;
@@ -2425,7 +2445,22 @@ descriptor_wave(PyrArgs pa, DescParams dp, const pano_kp *__restrict__ kps,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();                   // h / column tables reused next
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if PANO_DESC_TIMING
+        ++nkp;
+#endif
     }
+#if PANO_DESC_TIMING
+    {
+        const int gw = (int)blockIdx.x * kDescWaves + wv;
+        if (lane == 0 && gw < kDescClkWaves) {
+            unsigned long long *o = g_desc_clk[gw];
+            o[0] = t_entry;
+            o[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+            o[2] = (unsigned long long)nkp;
+            o[3] = (unsigned long long)(xcd + 1);
+        }
+    }
+#endif
 }
 
 // Processing order of the descriptor waves: keypoints are emitted x-sorted (the reference's
