@@ -1888,6 +1888,13 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         return chain_taps && o >= chain_min_oct && ctx->oct_h[o] >= 64 && ctx->oct_w[o] >= 64;
     };
     const bool chain_base = src.bgr && !src.base_only && chain_ok(0) && tb.n == 11;
+    // A/B (PANO_BASE_PAIR=1, read per call): the base level and level 1 of octave 0 in one
+    // blur_chain launch (G0 on the tile plus level 1's halo in LDS, never written unless the full
+    // pyramid is asked): one launch and G0's HBM round trip fewer, the base's FMAs on the halo.
+    // Measured (profiles/r06_base_pair_ab.txt): bit-exact, blur class +1 %, pooled step +2 %: off
+    const char *bp_env = getenv("PANO_BASE_PAIR");
+    const bool base_pair = bp_env && atoi(bp_env) != 0 && !chain_on && src.bgr && !src.base_only && nl >= 3 &&
+                           tb.n == 11 && tl[1].n == 11 && ctx->oct_h[0] >= 64 && ctx->oct_w[0] >= 64;
     // streaming cascades (blur_cascade, PANO_BLUR_CASCADE=1): per octave walker A (octave 0 from
     // the gray frames: base, 1, 2; else levels 1, 2) and walker B (levels 3, 4, 5 from G2)
     const char *cas_env = getenv("PANO_BLUR_CASCADE");     // read per call: tests compare both forms
@@ -1924,7 +1931,7 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         rc = launch_blur<MODE_BASEF>(ctx, la, G + ctx->gauss_off[0][0], nullptr, nullptr, n,
                                      ctx->oct_h[0], ctx->oct_w[0], tb);
         if (rc) return rc;
-    } else if (chain_base || cas_base) {
+    } else if (chain_base || cas_base || base_pair) {
         // gray frames only: the base level is the first level of octave 0's first chain
         const size_t npx = (size_t)n * h * w;
         rc = pano_grow(ctx, (void **)&ctx->gray, &ctx->gray_bytes, npx + 16);
@@ -2175,7 +2182,21 @@ int launch_sift_pyramid_src(pano_ctx *ctx, const PyrSource &src, int n, int h, i
         }();
         const bool pairs_here = (o >= 1 || pair_o0) && nl == 6 && H >= 32 && W >= 32 &&
                                 (long)((W + 63) / 64) * ((H + 63) / 64) * n < pair_tiles;
-        for (int l = 1; l < nl; ++l) {
+        int l_first = 1;
+        if (o == 0 && base_pair) {
+            LoadArgs la{};
+            la.gray = ctx->gray;
+            la.sh = h;
+            la.sw = w;
+            ChainOut ca{};
+            ca.g[0] = full ? G + ctx->gauss_off[0][0] : nullptr;
+            ca.g[1] = (full || 1 < nl - 1) ? G + ctx->gauss_off[0][1] : nullptr;
+            ca.d[1] = D + ctx->dog_off[0][0];
+            rc = launch_chain<MODE_BASE, 11, 11, 0>(ctx, la, ca, n, H, W, 0);
+            if (rc) { ctx->stream = main_stream; return rc; }
+            l_first = 2;
+        }
+        for (int l = l_first; l < nl; ++l) {
             if (fork_lvl && l == nl - 2) {
                 if (!ctx->lvl_side) {
                     int lo_prio = 0, hi_prio = 0;
