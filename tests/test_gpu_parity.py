@@ -972,3 +972,31 @@ def test_early_extrema_identical(gpu, parrington, monkeypatch):
         st.release_graphs()
     for a, b in zip(res["0"], res["1"]):
         assert a.tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("work", ["parrington", "synthetic"])
+def test_orientation_fast_bin_identical(gpu, work, monkeypatch):
+    """Orientation bins from atan2_oct away from the bin edges (PANO_ORI_FAST_BIN=1, the
+    default) against the exact f32 atan2f sequence for every gradient (=0): the same keypoint
+    tables (angles included) and descriptor bytes, at parrington and on 4 synthetic 1080p frames
+    (~1.5 M candidates' worth of gradient samples, every bin edge crossed many times)."""
+    from vfx_image_stitching_amd import data
+    from vfx_image_stitching_amd.pipeline import Stitcher
+    if work == "synthetic":
+        frames, focals, _ = data.synthetic_sequence(n_frames=144, h=1080, w=1920, start=40, count=4)
+        cap = 32768
+    else:
+        _, frames, focals, _ = data.load_set("parrington")
+        cap = 4096
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PANO_ORI_FAST_BIN", mode)
+        st = Stitcher("sift", cap=cap)
+        cyl, _ = st.cylindrical(st.upload(frames), focals)
+        k, d, c = st.features(cyl)
+        cnt = c.cpu().numpy()
+        kh, dh = k.cpu().numpy(), d.cpu().numpy()
+        res[mode] = (cnt, *[kh[i, :cnt[i]] for i in range(len(cnt))], *[dh[i, :cnt[i]] for i in range(len(cnt))])
+    assert all(n > 500 for n in res["1"][0])
+    for a, b in zip(res["0"], res["1"]):
+        assert a.tobytes() == b.tobytes()

@@ -582,9 +582,69 @@ constexpr int kOriStage = PANO_ORI_STAGE;
 #define PANO_ORI_BLOCKS 6        // waves per SIMD the register budget is sized for (80 VGPRs; measured 1-3 % faster than 88)
 #endif   // patch loads per lane in flight (37^2 / 64 <= 22: two rounds)
 
+// atan2(y, x) in units of pi/4 ("octants", (-4, 4]): octant reduction to a = min/max in
+// [0, 1] and an odd minimax polynomial of degree 15 (f32 Horner, |error| < 2.1e-7 octant).
+// The descriptor only uses the angle through the continuous trilinear weights, so a few
+// ulps here move each contribution by ~1e-7 relative -- the size of the reference's own f32
+// np.add.at rounding (sift_impl.py:499-500); atan2(0, 0) = 0 as numpy's.
+__device__ __forceinline__ float atan2_oct(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    // v_rcp_f32 flushes a subnormal argument (0 * inf = NaN): gradients that small (flat
+    // black borders of the cylindrical frames after the cascaded blurs) have magnitude 0 in
+    // f32 anyway, so their angle is taken as 0, numpy's atan2(0, 0)
+    const float a = mx >= 1.17549435e-38f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float t = a * a;
+    float p = -0.005166319198906422f;
+    p = fmaf(p, t, 0.027850419282913208f);
+    p = fmaf(p, t, -0.07120880484580994f);
+    p = fmaf(p, t, 0.1227816641330719f);
+    p = fmaf(p, t, -0.1770951747894287f);
+    p = fmaf(p, t, 0.2539685070514679f);
+    p = fmaf(p, t, -0.42436903715133667f);
+    p = fmaf(p, t, 1.2732386589050293f);
+    float r = p * a;                               // atan(a) / (pi / 4), in [0, 1]
+    r = ay > ax ? 2.0f - r : r;
+    r = x < 0.0f ? 4.0f - r : r;
+    return y < 0.0f ? -r : r;
+}
+
 struct OriParams {
     double scale_factor, radius_factor, peak_ratio;
+    int fast_bin;           // orientation bins from atan2_oct away from bin edges (PANO_ORI_FAST_BIN)
 };
+
+// The orientation bin of a gradient (sift_impl.py:268-275): np.rad2deg(np.arctan2(dy, dx)) in
+// f32, np.remainder(., 360), round(angle * 36 / 360) mod 36 -- the exact f32 sequence.
+__device__ __forceinline__ int ori_bin_exact(float gx, float gy) {
+    const float a = atan2f(gy, gx) * kRad2DegF32;
+    // np.remainder(a, 360) for |a| <= 180 (atan2f in [-pi, pi] times the f32 rad2deg)
+    const float ang = a < 0.0f ? a + 360.0f : (a == 0.0f ? 0.0f : a);
+    // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same bin as the
+    // IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
+    const float a36 = ang * 36.0f;
+    const float q0 = a36 * kInv360;
+    const int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
+    return bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
+}
+
+// The same bin from atan2_oct (|error| < 2.1e-7 octant = 1e-5 deg) wherever the angle is more
+// than kOriBinGuard bins (2e-3 deg, 100x the error of either path) from a bin edge
+// (10k + 5 deg); within the guard, ori_bin_exact.  Identical bins for every gradient of
+// non-zero magnitude (a zero magnitude adds 0 to any bin): test_orientation_fast_bin_identical.
+constexpr float kOriBinGuard = 2e-4f;
+__device__ __forceinline__ int ori_bin(float gx, float gy, bool fast) {
+    if (fast && PANO_ORI_BINS == 36) {
+        float u = atan2_oct(gy, gx) * 4.5f;        // octants -> bins of 10 deg, (-18, 18]
+        u = u < 0.0f ? u + 36.0f : u;
+        const float fu = u - floorf(u);
+        if (fabsf(fu - 0.5f) > kOriBinGuard) {
+            const int bin = (int)floorf(u + 0.5f);
+            return bin >= 36 ? bin - 36 : bin;
+        }
+    }
+    return ori_bin_exact(gx, gy);
+}
 
 // Dense candidate index gk (frames back to back, counts strided kCntStride and clamped to
 // [0, cap]) -> (frame, index); false past the last candidate.
@@ -775,15 +835,6 @@ __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H,
                     }
                 }
                 const float mag = sqrtf(gx * gx + gy * gy);
-#if PANO_ORI_ABL & 1                                  // timing ablation: no atan2f
-                const float ang = fabsf(gy + gx) * 3.0f;
-#else
-                // np.remainder(a, 360) for |a| <= 180 (atan2f in [-pi, pi] times the f32 rad2deg):
-                // np_remainder_pos_f's in-range branch without its general fallback
-                const float a = atan2f(gy, gx) * kRad2DegF32;
-                const float ang = kOriFastWalk ? (a < 0.0f ? a + 360.0f : (a == 0.0f ? 0.0f : a))
-                                               : np_remainder_pos_f(a, 360.0f);
-#endif
                 // dx^2 + dy^2 as the exact f32 sum of exact f32 squares (|d| <= 2^7): the same
                 // value as the integer expression converted, without the integer multiplies
                 const float fdx = (float)dx, fdy = (float)dy;
@@ -793,12 +844,11 @@ __device__ __forceinline__ bool orient_one(const float *__restrict__ img, int H,
 #else
                 const float w = expf(wfac * d2);
 #endif
-                // (ang * 36) / 360 by the reciprocal and one exact-residual correction: the same
-                // bin as the IEEE division for every f32 (exhaustive: tools/probes/div360_check.c)
-                const float a36 = ang * 36.0f;
-                const float q0 = a36 * kInv360;
-                int bin = (int)rintf(fmaf(fmaf(-q0, 360.0f, a36), kInv360, q0));
-                bin = bin >= PANO_ORI_BINS ? bin - PANO_ORI_BINS : bin;
+#if PANO_ORI_ABL & 1                                  // timing ablation: no atan2f
+                const int bin = (int)(fabsf(gy + gx) * 0.1f) % PANO_ORI_BINS;
+#else
+                const int bin = ori_bin(gx, gy, op.fast_bin != 0);
+#endif
                 const double val = (double)(w * mag);
                 atomicAdd(&hs[lane % kOriCopies][bin], rint_fix(val * kHistScale));
             }
@@ -1313,33 +1363,6 @@ __device__ __forceinline__ float sdot_skx_wave128(float lo, float hi) {
     const float h = v + __shfl(v, (j + 4) & 7);                      // h[j] = v[j] + v[j + 4], j < 4
     const float kern = (__shfl(h, 0) + __shfl(h, 1)) + (__shfl(h, 2) + __shfl(h, 3));
     return (float)((double)kern + 0.0);
-}
-
-// atan2(y, x) in units of pi/4 ("octants", (-4, 4]): octant reduction to a = min/max in
-// [0, 1] and an odd minimax polynomial of degree 15 (f32 Horner, |error| < 2.1e-7 octant).
-// The descriptor only uses the angle through the continuous trilinear weights, so a few
-// ulps here move each contribution by ~1e-7 relative -- the size of the reference's own f32
-// np.add.at rounding (sift_impl.py:499-500); atan2(0, 0) = 0 as numpy's.
-__device__ __forceinline__ float atan2_oct(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    // v_rcp_f32 flushes a subnormal argument (0 * inf = NaN): gradients that small (flat
-    // black borders of the cylindrical frames after the cascaded blurs) have magnitude 0 in
-    // f32 anyway, so their angle is taken as 0, numpy's atan2(0, 0)
-    const float a = mx >= 1.17549435e-38f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
-    const float t = a * a;
-    float p = -0.005166319198906422f;
-    p = fmaf(p, t, 0.027850419282913208f);
-    p = fmaf(p, t, -0.07120880484580994f);
-    p = fmaf(p, t, 0.1227816641330719f);
-    p = fmaf(p, t, -0.1770951747894287f);
-    p = fmaf(p, t, 0.2539685070514679f);
-    p = fmaf(p, t, -0.42436903715133667f);
-    p = fmaf(p, t, 1.2732386589050293f);
-    float r = p * a;                               // atan(a) / (pi / 4), in [0, 1]
-    r = ay > ax ? 2.0f - r : r;
-    r = x < 0.0f ? 4.0f - r : r;
-    return y < 0.0f ? -r : r;
 }
 
 // Descriptors, one WAVE per keypoint, persistent: waves stride over the keypoints of the
@@ -2734,6 +2757,12 @@ int launch_extrema_stream(pano_ctx *ctx, const pano_sift_params *p, const XArgs 
 // Fraction of the resident workgroups the persistent orientation / descriptor grids take
 // (PANO_PERSIST_FRAC, default 1): below 1, a stitch overlapping on another context
 // (pipeline.StitchPool) keeps CU slots while they run.
+// PANO_ORI_FAST_BIN=0 (read per call): every orientation bin through ori_bin_exact (A/B and
+// test_orientation_fast_bin_identical)
+int ori_fast_bin() {
+    const char *e = getenv("PANO_ORI_FAST_BIN");
+    return e && atoi(e) == 0 ? 0 : 1;
+}
 double persist_frac() {
     static const double v = [] {
         const char *e = getenv("PANO_PERSIST_FRAC");
@@ -2903,7 +2932,7 @@ int sift_keypoints_impl(pano_ctx *ctx, const pano_sift_params *p, pano_kp *kps, 
         pa.W[o] = ctx->oct_w[o];
         for (int l = 0; l < nl; ++l) pa.gauss[o][l] = ctx->pyr + ctx->gauss_off[o][l];
     }
-    OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio};
+    OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio, ori_fast_bin()};
     const int nb = ctx->oct_w[0] + 1;                   // sort: floor(x) buckets over the base width
     const size_t per = raw_cap * n;
     rc = pano_grow(ctx, (void **)&ctx->sorted, &ctx->sorted_bytes, (3 * per + (size_t)nb * n) * sizeof(uint32_t));
@@ -3166,7 +3195,7 @@ int launch_sift_localize(pano_ctx *ctx, const pano_sift_params *p, const float *
 int launch_sift_orient(pano_ctx *ctx, const pano_sift_params *p, const float *gauss, int h, int w, int octave,
                        const pano_kp *kps, int n, pano_kp *out, int32_t *counts) {
     if (n <= 0) return PANO_OK;
-    OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio};
+    OriParams op{p->scale_factor, p->radius_factor, p->peak_ratio, ori_fast_bin()};
     const unsigned blocks = (unsigned)std::min(4096, (n + 3) / 4);
     {
         PanoProf prof_(ctx, PK_ORIENT);
