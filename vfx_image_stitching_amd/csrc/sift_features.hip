@@ -573,7 +573,10 @@ constexpr int kOriCopies = PANO_ORI_COPIES;
 #endif
 constexpr int kOriClaim = PANO_ORI_CLAIM;
 constexpr float kInv360 = 1.0f / 360.0f;   // RN(1 / 360)
-constexpr int kOriPatch = 37;   // staged patch side: radius <= 17 (default params: <= 16)
+#ifndef PANO_ORI_PATCH
+#define PANO_ORI_PATCH 37
+#endif
+constexpr int kOriPatch = PANO_ORI_PATCH;   // staged patch side: radius <= 17 (default params: <= 16)
 #ifndef PANO_ORI_STAGE
 #define PANO_ORI_STAGE 8
 #endif
